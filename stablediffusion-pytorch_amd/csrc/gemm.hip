@@ -1,0 +1,398 @@
+// MFMA bf16 GEMM family for gfx950 with implicit-GEMM convolution gathers.
+//
+// One kernel template covers every contraction of the denoiser step (reference aten calls:
+// nn.Conv2d models/blocks.py:48-53,67-72,102-109; nn.ConvTranspose2d blocks.py:457-459;
+// nn.Linear blocks.py:58-61,97 and MHA in/out projections blocks.py:83,94) in forward and
+// backward:
+//   conv fwd / dgrad : A = im2col(NHWC activation) [m=pixel][k=(tap,cin)],  B = packed weight [n][k]
+//   conv wgrad       : A = dY^T (col-major),                               B = im2col(X) [k=pixel][n=(tap,cin)]
+//   linear fwd/dgrad/wgrad : plain row/col-major operands.
+//
+// Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16x32 bf16 tiles.
+// Operands are register-staged (so the conv gathers can zero-pad) into two LDS buffers:
+//   "K-contiguous" tiles [128 rows][64 k] (A row-major / conv, B [n][k]) read with ds_read_b128,
+//      16-B chunk c of row r stored at chunk (c ^ (r & 7))  -> conflict-free b128 fragment reads;
+//   "MN-contiguous" tiles [64 k][128 cols] (A col-major, B [k][n]) read with ds_read_b64_tr_b16
+//      (hardware transpose), chunk c of row r stored at c ^ (((r&3) | ((r>>1)&4)) << 1)
+//      -> conflict-free transposed reads.
+// Split-K (for the small-grid weight-gradient and deep low-resolution GEMMs) writes fp32 slabs that
+// a second kernel reduces while applying the same epilogue.
+#include "common.h"
+#include "../../include/sdmi.h"
+#include <string.h>
+#include <algorithm>
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = 128 * 64 * 2;  // 16 KiB per operand tile (both layouts)
+
+struct Args {
+  int M, N, K;
+  const bf16_t* A; int lda;
+  const bf16_t* B; int ldb;
+  // gather geometry
+  int ih, iw, cin, ldx, kw, ohl, owl, sy, sx, oy0, ox0;
+  int ktiles_per_split, nsplit;
+  // epilogue
+  void* C; int ldc; int c_f32; long long split_stride;
+  const float* bias; const bf16_t* rowbias; int rb_ld, rb_shift;
+  const bf16_t* resid; int ldr;
+  float alpha; int act;
+  int remap, r_ghl, r_gwl, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
+  int perm, p_cin, p_taps;
+  int raw;  // 1: write raw fp32 partials (split-K), epilogue applied by the reducer
+};
+
+__device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+__device__ __forceinline__ int tr_swz(int r) { return ((r & 3) | ((r >> 1) & 4)) << 1; }
+__device__ __forceinline__ int tr_off(int r, int c) { return r * 256 + ((c ^ tr_swz(r)) << 4); }
+
+struct Epi {
+  __device__ __forceinline__ static void store(const Args& g, int row, int col, float acc, int z) {
+    if (row >= g.M || col >= g.N) return;
+    if (g.raw) {
+      ((float*)g.C)[(long long)z * g.split_stride + (long long)row * g.N + col] = acc;
+      return;
+    }
+    float v = g.alpha * acc;
+    if (g.bias) v += g.bias[col];
+    if (g.rowbias) v += bf2f(g.rowbias[(long long)(row >> g.rb_shift) * g.rb_ld + col]);
+    long long orow = row;
+    if (g.remap) {
+      int b = row >> (g.r_ghl + g.r_gwl);
+      int oy = (row >> g.r_gwl) & ((1 << g.r_ghl) - 1);
+      int ox = row & ((1 << g.r_gwl) - 1);
+      orow = ((long long)b * g.r_oh + oy * g.r_sy + g.r_oy) * g.r_ow + ox * g.r_sx + g.r_ox;
+    }
+    if (g.resid) v += bf2f(g.resid[orow * g.ldr + col]);
+    if (g.act == 1) v = silu_f(v);
+    long long ocol = col;
+    if (g.perm) {
+      int tap = col / g.p_cin;
+      int c = col - tap * g.p_cin;
+      ocol = (long long)c * g.p_taps + tap;
+    }
+    if (g.c_f32) ((float*)g.C)[orow * g.ldc + ocol] = v;
+    else ((bf16_t*)g.C)[orow * g.ldc + ocol] = f2bf(v);
+  }
+};
+
+template <int AM, int BMODE>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+  // buffer b: A tile at smem + 2*b*TILE_BYTES, B tile right after it
+#define SA(b) (smem + (b) * 2 * TILE_BYTES)
+#define SB(b) (smem + (b) * 2 * TILE_BYTES + TILE_BYTES)
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int z = blockIdx.z;
+  const int nkt_total = (g.K + BK - 1) / BK;
+  const int kt0 = z * g.ktiles_per_split;
+  const int kt1 = min(nkt_total, kt0 + g.ktiles_per_split);
+
+  // ---------------- per-thread staging coordinates ----------------
+  // K-contiguous staging: rows (tid>>3)+32i, chunk tid&7.   MN-contiguous: k-rows (tid>>4)+16i, chunk tid&15.
+  int a_pb[4], a_iy[4], a_ix[4];
+  bool a_ok[4];
+  if (AM == SDMI_A_CONV) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int m = m0 + (tid >> 3) + 32 * i;
+      a_ok[i] = m < g.M;
+      int b = m >> (g.ohl + g.owl);
+      int oy = (m >> g.owl) & ((1 << g.ohl) - 1);
+      int ox = m & ((1 << g.owl) - 1);
+      a_pb[i] = b * g.ih;
+      a_iy[i] = oy * g.sy + g.oy0;
+      a_ix[i] = ox * g.sx + g.ox0;
+    }
+  }
+  int b_ty = 0, b_tx = 0, b_ci = 0;
+  bool b_nok = true;
+  if (BMODE == SDMI_B_KN_CONV) {
+    int n = n0 + (tid & 15) * 8;
+    b_nok = n < g.N;
+    int tap = n / g.cin;
+    b_ci = n - tap * g.cin;
+    b_ty = tap / g.kw;
+    b_tx = tap - b_ty * g.kw;
+  }
+
+  uint4 ra[4], rb[4];
+  // Buffer descriptors: out-of-range offsets return zeros in hardware, which is how padding taps,
+  // ragged tiles and k >= K are zero-filled without a select on a pointer.
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, 0x7fffffff, 0x00020000);
+  constexpr int OOB = (int)0x80000000;
+#define BUF_LD(rs, off) __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128((rs), (off), 0, 0))
+
+  auto load_tiles = [&](int kt) __attribute__((always_inline)) {
+    const int k0 = kt * BK;
+    // ---- A ----
+    if (AM == SDMI_A_ROWMAJOR) {
+      int k = k0 + (tid & 7) * 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int m = m0 + (tid >> 3) + 32 * i;
+        int off = (m < g.M && k < g.K) ? (m * g.lda + k) * 2 : OOB;
+        ra[i] = BUF_LD(rsA, off);
+      }
+    } else if (AM == SDMI_A_CONV) {
+      int k = k0 + (tid & 7) * 8;
+      int tap = k / g.cin;
+      int ci = k - tap * g.cin;
+      int ty = tap / g.kw;
+      int tx = tap - ty * g.kw;
+      bool kok = k < g.K;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int iy = a_iy[i] + ty, ix = a_ix[i] + tx;
+        bool ok = kok && a_ok[i] && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
+        int off = ok ? (((a_pb[i] + iy) * g.iw + ix) * g.ldx + ci) * 2 : OOB;
+        ra[i] = BUF_LD(rsA, off);
+      }
+    } else {  // col-major A: A[k*lda + m]
+      int m = m0 + (tid & 15) * 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int k = k0 + (tid >> 4) + 16 * i;
+        int off = (m < g.M && k < g.K) ? (k * g.lda + m) * 2 : OOB;
+        ra[i] = BUF_LD(rsA, off);
+      }
+    }
+    // ---- B ----
+    if (BMODE == SDMI_B_NK) {
+      int k = k0 + (tid & 7) * 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int n = n0 + (tid >> 3) + 32 * i;
+        int off = (n < g.N && k < g.K) ? (n * g.ldb + k) * 2 : OOB;
+        rb[i] = BUF_LD(rsB, off);
+      }
+    } else if (BMODE == SDMI_B_KN) {
+      int n = n0 + (tid & 15) * 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int k = k0 + (tid >> 4) + 16 * i;
+        int off = (n < g.N && k < g.K) ? (k * g.ldb + n) * 2 : OOB;
+        rb[i] = BUF_LD(rsB, off);
+      }
+    } else {  // conv gather, k = pixel of the (oh x ow) grid
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int p = k0 + (tid >> 4) + 16 * i;
+        int b = p >> (g.ohl + g.owl);
+        int oy = (p >> g.owl) & ((1 << g.ohl) - 1);
+        int ox = p & ((1 << g.owl) - 1);
+        int iy = oy * g.sy + g.oy0 + b_ty, ix = ox * g.sx + g.ox0 + b_tx;
+        bool ok = b_nok && p < g.K && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
+        int off = ok ? (((b * g.ih + iy) * g.iw + ix) * g.ldx + b_ci) * 2 : OOB;
+        rb[i] = BUF_LD(rsB, off);
+      }
+    }
+  };
+
+  auto store_tiles = [&](int buf) __attribute__((always_inline)) {
+    if (AM == SDMI_A_COLMAJOR) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *(uint4*)(SA(buf) + tr_off((tid >> 4) + 16 * i, tid & 15)) = ra[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *(uint4*)(SA(buf) + kc_off((tid >> 3) + 32 * i, tid & 7)) = ra[i];
+    }
+    if (BMODE == SDMI_B_NK) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *(uint4*)(SB(buf) + kc_off((tid >> 3) + 32 * i, tid & 7)) = rb[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *(uint4*)(SB(buf) + tr_off((tid >> 4) + 16 * i, tid & 15)) = rb[i];
+    }
+  };
+
+  // fragment readers
+  auto read_kc = [&](const char* tile, int rbase, int ks) __attribute__((always_inline)) -> s16x8 {
+    int r = rbase + (lane & 15);
+    int c = ks * 4 + (lane >> 4);
+    return *(const s16x8*)(tile + kc_off(r, c));
+  };
+  auto read_tr = [&](const char* tile, int cbase, int ks) __attribute__((always_inline)) -> s16x8 {
+    int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    int r1 = ks * 32 + gq * 8 + q;
+    int c = (cbase >> 3) + (p >> 1);
+    int o1 = tr_off(r1, c) + (p & 1) * 8;
+    int o2 = tr_off(r1 + 4, c) + (p & 1) * 8;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SDMI_LDS s16x4*)(tile + o1));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SDMI_LDS s16x4*)(tile + o2));
+    s16x8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (kt0 < kt1) {
+    load_tiles(kt0);
+    store_tiles(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load_tiles(kt + 1);
+      const char* ta = SA(cur);
+      const char* tb = SB(cur);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        s16x8 fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          fa[i] = (AM == SDMI_A_COLMAJOR) ? read_tr(ta, wm + 16 * i, ks) : read_kc(ta, wm + 16 * i, ks);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fb[j] = (BMODE == SDMI_B_NK) ? read_kc(tb, wn + 16 * j, ks) : read_tr(tb, wn + 16 * j, ks);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) store_tiles(cur ^ 1);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // ---------------- epilogue ----------------
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int col = n0 + wn + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+        Epi::store(g, row, col, acc[i][j][r], z);
+      }
+    }
+}
+
+// Sum split-K slabs and apply the epilogue.
+__global__ void splitk_reduce_kernel(Args g) {
+  long long total = (long long)g.M * g.N;
+  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long stride = (long long)gridDim.x * blockDim.x;
+  const float* ws = (const float*)g.A;  // the launcher passes the slab workspace through A
+  for (; idx < total; idx += stride) {
+    float s = 0.f;
+    for (int zz = 0; zz < g.nsplit; ++zz) s += ws[(long long)zz * g.split_stride + idx];
+    int row = (int)(idx / g.N), col = (int)(idx - (long long)row * g.N);
+    Epi::store(g, row, col, s, 0);
+  }
+}
+
+template <int AM, int BMODE>
+hipError_t launch_t(const Args& a, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a);
+  return hipGetLastError();
+}
+
+int fill_args(const sdmi_gemm_desc* d, Args& a) {
+  if (!d || d->m <= 0 || d->n <= 0 || d->k <= 0) return -1;
+  if (d->k % 8) return -2;
+  if ((d->a_mode == SDMI_A_COLMAJOR) && (d->m % 8)) return -3;
+  if ((d->b_mode != SDMI_B_NK) && (d->n % 8)) return -4;
+  if (d->a_mode == SDMI_A_CONV || d->b_mode == SDMI_B_KN_CONV) {
+    const sdmi_conv_geom& q = d->geom;
+    if (q.cin <= 0 || q.cin % 8 || q.kw <= 0 || q.ldx % 8) return -5;
+  }
+  memset(&a, 0, sizeof(a));
+  a.M = d->m; a.N = d->n; a.K = d->k;
+  a.A = (const bf16_t*)d->a; a.lda = d->lda;
+  a.B = (const bf16_t*)d->b; a.ldb = d->ldb;
+  a.ih = d->geom.ih; a.iw = d->geom.iw; a.cin = d->geom.cin; a.ldx = d->geom.ldx; a.kw = d->geom.kw;
+  a.ohl = d->geom.oh_log2; a.owl = d->geom.ow_log2;
+  a.sy = d->geom.sy; a.sx = d->geom.sx; a.oy0 = d->geom.oy0; a.ox0 = d->geom.ox0;
+  a.C = d->c; a.ldc = d->ldc; a.c_f32 = d->c_f32;
+  a.bias = d->bias; a.rowbias = (const bf16_t*)d->rowbias; a.rb_ld = d->rb_ld; a.rb_shift = d->rb_shift;
+  a.resid = (const bf16_t*)d->resid; a.ldr = d->ldr;
+  a.alpha = d->alpha; a.act = d->act;
+  a.remap = d->remap; a.r_ghl = d->r_gh_log2; a.r_gwl = d->r_gw_log2; a.r_oh = d->r_oh; a.r_ow = d->r_ow;
+  a.r_sy = d->r_sy; a.r_sx = d->r_sx; a.r_oy = d->r_oy; a.r_ox = d->r_ox;
+  a.perm = d->perm; a.p_cin = d->p_cin; a.p_taps = d->p_taps;
+  return 0;
+}
+
+int plan_splits(const sdmi_gemm_desc* d) {
+  long long tiles = (long long)((d->m + BM - 1) / BM) * ((d->n + BN - 1) / BN);
+  int nkt = (d->k + BK - 1) / BK;
+  int s = 1;
+  // aim for >= ~2 waves of workgroups over 256 CUs, keep >= 8 k-tiles per slice
+  while (tiles * s < 384 && nkt / (s * 2) >= 8 && s < 16) s *= 2;
+  return s;
+}
+
+}  // namespace
+
+extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) {
+  Args a;
+  int rc = fill_args(d, a);
+  if (rc) return rc;
+  int s = plan_splits(d);
+  if (splits) *splits = s;
+  if (ws) *ws = s > 1 ? (size_t)s * d->m * d->n * sizeof(float) : 0;
+  return 0;
+}
+
+extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_bytes, sdmi_stream_t stream) {
+  Args a;
+  int rc = fill_args(d, a);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  int splits = plan_splits(d);
+  if (splits > 1 && (!workspace || ws_bytes < (size_t)splits * d->m * d->n * sizeof(float))) splits = 1;
+  int nkt = (d->k + BK - 1) / BK;
+  a.ktiles_per_split = (nkt + splits - 1) / splits;
+  splits = (nkt + a.ktiles_per_split - 1) / a.ktiles_per_split;
+  a.nsplit = splits;
+  Args run = a;
+  if (splits > 1) {
+    run.raw = 1;
+    run.C = workspace;
+    run.split_stride = (long long)d->m * d->n;
+  }
+  dim3 grid((d->n + BN - 1) / BN, (d->m + BM - 1) / BM, splits);
+  hipError_t e;
+  int key = d->a_mode * 3 + d->b_mode;
+  switch (key) {
+    case SDMI_A_ROWMAJOR * 3 + SDMI_B_NK: e = launch_t<SDMI_A_ROWMAJOR, SDMI_B_NK>(run, grid, s); break;
+    case SDMI_A_ROWMAJOR * 3 + SDMI_B_KN: e = launch_t<SDMI_A_ROWMAJOR, SDMI_B_KN>(run, grid, s); break;
+    case SDMI_A_CONV * 3 + SDMI_B_NK: e = launch_t<SDMI_A_CONV, SDMI_B_NK>(run, grid, s); break;
+    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN: e = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN>(run, grid, s); break;
+    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN_CONV: e = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN_CONV>(run, grid, s); break;
+    default: return -6;
+  }
+  if (e != hipSuccess) return (int)e;
+  if (splits > 1) {
+    Args red = a;
+    red.raw = 0;
+    // reducer reads slabs from workspace and writes the real output
+    red.split_stride = (long long)d->m * d->n;
+    long long total = (long long)d->m * d->n;
+    int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+    // pass the workspace through A (unused by the reducer)
+    red.A = (const bf16_t*)workspace;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, red);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
+}

@@ -1,0 +1,108 @@
+"""GPU numerics of the MFMA GEMM family (libsdmi.so sdmi_gemm) against torch fp32 references of
+the same op on bf16-rounded operands.  Tolerance: bf16 output rounding (2^-8 relative) plus fp32
+accumulation-order differences."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _k():
+    from sdmi import kernels, _lib
+    return kernels, _lib
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def close(out, ref, tol=1e-2):
+    err = (out.float() - ref.float()).abs().max().item()
+    scale = ref.float().abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 136), (128, 128, 64), (17, 40, 8), (64, 768, 4608)])
+def test_rowmajor_nk(M, N, K):
+    k, L = _k()
+    torch.manual_seed(0)
+    a = bf(torch.randn(M, K, device="cuda"))
+    w = bf(torch.randn(N, K, device="cuda"))
+    bias = torch.randn(N, device="cuda")
+    res = bf(torch.randn(M, N, device="cuda"))
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    k.gemm(M, N, K, a, L.A_ROWMAJOR, K, w, L.B_NK, K, c, N, bias=bias, resid=res, ldr=N)
+    ref = a.float() @ w.float().t() + bias + res.float()
+    close(c, ref)
+    c32 = torch.empty(M, N, device="cuda")
+    k.gemm(M, N, K, a, L.A_ROWMAJOR, K, w, L.B_NK, K, c32, N, act=1, alpha=0.5)
+    close(c32, F.silu(0.5 * (a.float() @ w.float().t())), 2e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(257, 136, 72), (2048, 512, 384)])
+def test_rowmajor_kn(M, N, K):
+    k, L = _k()
+    torch.manual_seed(1)
+    a = bf(torch.randn(M, K, device="cuda"))
+    b = bf(torch.randn(K, N, device="cuda"))
+    c = torch.empty(M, N, device="cuda")
+    k.gemm(M, N, K, a, L.A_ROWMAJOR, K, b, L.B_KN, N, c, N)
+    close(c, a.float() @ b.float(), 2e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(136, 264, 200), (512, 512, 32768)])
+def test_colmajor_kn(M, N, K):
+    k, L = _k()
+    torch.manual_seed(2)
+    at = bf(torch.randn(K, M, device="cuda"))
+    b = bf(torch.randn(K, N, device="cuda"))
+    c = torch.empty(M, N, device="cuda")
+    k.gemm(M, N, K, at, L.A_COLMAJOR, M, b, L.B_KN, N, c, N)
+    close(c, at.float().t() @ b.float(), 2e-3)
+
+
+@pytest.mark.parametrize("B,H,cin,cout,ks,stride,pad", [
+    (2, 8, 16, 24, 3, 1, 1), (2, 16, 8, 32, 3, 1, 1), (3, 8, 64, 64, 4, 2, 1), (2, 4, 32, 16, 1, 1, 0),
+    (4, 32, 128, 136, 3, 1, 1)])
+def test_conv_fwd_and_wgrad(B, H, cin, cout, ks, stride, pad):
+    k, L = _k()
+    torch.manual_seed(3)
+    x = bf(torch.randn(B, cin, H, H, device="cuda"))
+    w = bf(torch.randn(cout, cin, ks, ks, device="cuda") * 0.1)
+    ref = F.conv2d(x.float(), w.float(), stride=stride, padding=pad)
+    OH = ref.shape[-1]
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    wpk = w.permute(0, 2, 3, 1).contiguous()
+    out = torch.empty(B, OH, OH, cout, device="cuda", dtype=torch.bfloat16)
+    rowbias = bf(torch.randn(B, cout, device="cuda"))
+    k.conv_fwd(xn, B, H, H, cin, cin, wpk, cout, ks, ks, stride, pad, out, cout, rowbias=rowbias)
+    close(out.permute(0, 3, 1, 2), ref + rowbias.float()[:, :, None, None])
+    # weight gradient
+    dy = bf(torch.randn(B, cout, OH, OH, device="cuda"))
+    xr = x.float().requires_grad_(True)
+    wr = w.float().requires_grad_(True)
+    F.conv2d(xr, wr, stride=stride, padding=pad).backward(dy.float())
+    dw = torch.empty(cout, cin, ks, ks, device="cuda")
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    k.conv_wgrad(dyn, cout, xn, B, H, H, cin, cin, cout, ks, ks, stride, pad, dw, OH, OH)
+    close(dw, wr.grad, 2e-3)
+
+
+@pytest.mark.parametrize("B,H,cin,cout", [(2, 4, 16, 24), (3, 8, 64, 32)])
+def test_convT_phases(B, H, cin, cout):
+    k, L = _k()
+    torch.manual_seed(4)
+    x = bf(torch.randn(B, cin, H, H, device="cuda"))
+    w = bf(torch.randn(cin, cout, 4, 4, device="cuda") * 0.1)
+    ref = F.conv_transpose2d(x.float(), w.float(), stride=2, padding=1)
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    wph = []
+    for ph in range(2):
+        for pw in range(2):
+            th, tw = k.phase_taps(ph), k.phase_taps(pw)
+            sub = w[:, :, th][:, :, :, tw]            # (cin, cout, 2, 2) [a][b]
+            wph.append(sub.permute(1, 2, 3, 0).contiguous())  # [cout][a][b][cin]
+    out = torch.empty(B, 2 * H, 2 * H, cout, device="cuda", dtype=torch.bfloat16)
+    k.convT_fwd_phases(xn, B, H, H, cin, cin, wph, cout, out, cout)
+    close(out.permute(0, 3, 1, 2), ref)
