@@ -1,0 +1,43 @@
+"""Model configs used by the golden fixtures and the tests (plain dicts in the reference's
+model_config format, models/unet_cond_base.py:17-27)."""
+
+
+def _cond(text_dim, text=True, image=True):
+    types = ([] if not text else ["text"]) + ([] if not image else ["image"])
+    return {
+        "condition_types": types,
+        "text_condition_config": {"text_embed_model": "clip", "train_text_embed_model": False,
+                                  "text_embed_dim": text_dim, "cond_drop_prob": 0.1},
+        "image_condition_config": {"image_condition_input_channels": 18, "image_condition_output_channels": 3,
+                                   "image_condition_h": 512, "image_condition_w": 512, "cond_drop_prob": 0.1},
+    }
+
+
+SMALL_UNCOND = {
+    "down_channels": [64, 128, 128, 256], "mid_channels": [256, 128], "down_sample": [True, True, True],
+    "attn_down": [True, True, True], "time_emb_dim": 128, "norm_channels": 32, "num_heads": 8,
+    "conv_out_channels": 64, "num_down_layers": 2, "num_mid_layers": 1, "num_up_layers": 2,
+}
+SMALL_COND = dict(SMALL_UNCOND, condition_config=_cond(64))
+
+
+def full_cond_config():
+    """config/celebhq_text_image_cond.py:36-118 (c_factor = 1)."""
+    return {
+        "down_channels": [256, 384, 512, 768], "mid_channels": [768, 512], "down_sample": [True, True, True],
+        "attn_down": [True, True, True], "time_emb_dim": 512, "norm_channels": 32, "num_heads": 16,
+        "conv_out_channels": 128, "num_down_layers": 2, "num_mid_layers": 2, "num_up_layers": 2,
+        "condition_config": _cond(512),
+    }
+
+
+def full_uncond_config():
+    """config/celebhq.yaml ldm_params."""
+    c = full_cond_config()
+    c.pop("condition_config")
+    return c
+
+
+# scheduler configs: (num_timesteps, beta_start, beta_end)
+SCHED_COND = (1000, 0.00085, 0.012)     # config/celebhq_text_image_cond.py:31-33
+SCHED_UNCOND = (1000, 0.0015, 0.0195)   # config/celebhq.yaml diffusion_params
