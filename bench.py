@@ -1,0 +1,183 @@
+"""Benchmark: DDPM train steps/sec of the conditional UNet (config/celebhq_text_image_cond.py, CelebHQ-256
+latents (B,4,32,32), per-GPU batch 32, text (B,77,512) + mask (B,18,512,512) conditioning) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+One step = the reference's training step (train_ddpm_cond_celebhq_multi_gpu.py:299-378) on a synthetic
+batch already resident in HBM: cond-drop, noise/t draw, add_noise, forward, MSE, backward, RCCL
+all-reduce (N > 1), clip(1.0), Adam(1e-5), EMA(0.9999), bf16 weight repack. Prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "stablediffusion-pytorch_amd")
+for p in (PKG, REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "DDPM train steps/sec (cond-UNet, CelebHQ-256 latents, B=32) at 1/2/4/8 MI355X"
+FLOP_PER_STEP = 3.8815e12      # cond-UNet fwd+bwd at B=32 (FlopCounterMode on the oracle)
+PEAK_BF16 = 2.5e15             # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM = 8.0e12
+
+
+def cond_config():
+    from tests.golden.configs import full_cond_config
+    return full_cond_config()
+
+
+def synthetic_batch(B, device, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x0 = torch.randn(B, 4, 32, 32, generator=g)
+    text = torch.randn(B, 77, 512, generator=g)
+    empty = torch.randn(1, 77, 512, generator=g)  # stand-in for the CLIP embedding of "" (text_utils.py)
+    cmap = torch.randint(0, 19, (B, 512, 512), generator=g)
+    x0, text, empty = x0.to(device), text.to(device), empty.to(device)
+    mask = torch.nn.functional.one_hot(cmap.to(device).long(), 19).movedim(-1, 1)[:, 1:].float().contiguous()
+    return x0, text, empty, mask
+
+
+def cpu_baseline(cfg, B=32):
+    """The oracle (CPU fp32 restatement of the reference step) on the host cores; bounded sample."""
+    from oracle import sd_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = O.deterministic_state(O.unet_param_shapes(cfg), seed=0)
+    ema = {k: v.clone() for k, v in sd.items()}
+    opt = O.AdamState(sd)
+    sched = O.SchedulerTables(1000, 0.00085, 0.012)
+    g = torch.Generator().manual_seed(1111)
+    x0 = torch.randn(B, 4, 32, 32, generator=g)
+    text = torch.randn(B, 77, 512, generator=g)
+    cmap = torch.randint(0, 19, (B, 512, 512), generator=g)
+    mask = torch.nn.functional.one_hot(cmap, 19).movedim(-1, 1)[:, 1:].float()
+    times = []
+    for i in range(2):  # 1 warm-up + 1 timed
+        noise = torch.randn(x0.shape, generator=g)
+        t = torch.randint(0, 1000, (B,), generator=g)
+        t0 = time.perf_counter()
+        O.train_step(sd, ema, opt, cfg, sched, x0, noise, t, {"text": text, "image": mask})
+        times.append(time.perf_counter() - t0)
+    return dict(value=1.0 / times[-1], unit="steps/s", cores=threads, kind="port",
+                sample=f"oracle fp32 train step (fwd+bwd+clip+Adam+EMA), B={B}, 1 warm-up + 1 timed step, "
+                       f"{times[-1]:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-gemm", action="store_true", default=True)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from sdmi.trainer import DDPMTrainer, S_LOSS, S_NORM, S_SKIP
+    from sdmi import kernels as K
+    import models.unet_cond_base as mc
+
+    cfg = cond_config()
+    torch.manual_seed(1111)  # identical initial weights on every rank (DDP broadcasts rank 0's)
+    init = mc.Unet(4, cfg).state_dict()
+    trainer = DDPMTrainer(cfg, init, device, group=dist.group.WORLD if world > 1 else None)
+    B = args.batch
+    x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
+    gen = torch.Generator(device=device).manual_seed(1111 + rank)
+
+    def one_step():
+        noise = torch.randn(x0.shape, device=device, generator=gen)
+        t = torch.randint(0, 1000, (B,), device=device, generator=gen)
+        drop_t = torch.rand(B, device=device, generator=gen) < 0.1       # diffusion_utils.py:21-28
+        txt = torch.where(drop_t[:, None, None], empty, text)
+        keep = (torch.rand(B, device=device, generator=gen) > 0.1).float()  # diffusion_utils.py:31-37
+        trainer.step(x0, noise, t, txt, mask, mask_keep=keep)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = e.item()
+    steps_per_s = args.steps / elapsed
+    state = trainer.state.tolist()
+
+    # dominant-kernel roofline: the implicit-GEMM conv/linear launches of one extra (untimed) step, timed
+    # with HIP events on the stream they run on
+    roof = None
+    if args.profile_gemm:
+        K.PROFILE = []
+        one_step()
+        torch.cuda.synchronize()
+        prof, K.PROFILE = K.PROFILE, None
+        by = {}
+        for tag, fl, e0, e1, sp in prof:
+            ms = e0.elapsed_time(e1)
+            a = by.setdefault(tag, [0.0, 0.0, 0])
+            a[0] += fl
+            a[1] += ms
+            a[2] += 1
+        tot_fl = sum(v[0] for v in by.values())
+        tot_ms = sum(v[1] for v in by.values())
+        dom = max(by.items(), key=lambda kv: kv[1][1])
+        roof = {"bound": "mfma", "kernel": "sdmi gemm_kernel (all implicit-GEMM conv + linear launches of one step)",
+                "achieved": tot_fl / (tot_ms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
+                "frac": tot_fl / (tot_ms * 1e-3) / PEAK_BF16, "traffic": None,
+                "launches": sum(v[2] for v in by.values()), "gemm_ms_per_step": tot_ms,
+                "per_mode": {k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms": v[1], "launches": v[2]}
+                             for k, v in by.items()},
+                "dominant_mode": dom[0]}
+
+    result = {
+        "metric": METRIC, "value": steps_per_s * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 / steps_per_s, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded CelebHQ-shaped latents, text, masks; "
+                                                        "random-init weights of the reference architecture)",
+        "config": {"workload": "cond-UNet celebhq_text_image_cond training step", "model": "cond-UNet 118.5M",
+                   "global_batch": B * world, "per_gpu_batch": B, "latent": [4, 32, 32],
+                   "text": [77, 512], "mask": [18, 512, 512], "parallelism": f"dp{world}"},
+        "per_gpu_steps_per_s": steps_per_s, "samples_per_s": steps_per_s * B * world,
+        "model_flops_utilization": FLOP_PER_STEP * steps_per_s / PEAK_BF16,
+        "last_loss": state[S_LOSS], "last_grad_norm": state[S_NORM], "last_step_skipped": bool(state[S_SKIP]),
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -72,8 +72,12 @@ typedef struct sdmi_gemm_desc {
   /* row remap (stride-2 sub-pixel phases of a transposed conv): m -> (b, oy, ox) on a
    * (2^r_gh_log2 x 2^r_gw_log2) grid, orow = (b*r_oh + oy*r_sy + r_oy)*r_ow + ox*r_sx + r_ox */
   int remap, r_gh_log2, r_gw_log2, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
-  /* column permute (weight-gradient layouts): n = tap*p_cin + c  ->  ocol = c*p_taps + tap */
-  int perm, p_cin, p_taps;
+  /* column permute (weight-gradient layouts): n = tap*p_cin + c  ->  ocol = c*p_taps + tap, stored only
+   * for c < p_cvalid (0 = all): gradients of zero-padded input channels are dropped */
+  int perm, p_cin, p_taps, p_cvalid;
+  /* store limits (0 = m / n): rows >= m_store and columns >= n_store are computed but not stored,
+   * and the bias is read only for stored columns (zero-padded output channels) */
+  int m_store, n_store;
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */

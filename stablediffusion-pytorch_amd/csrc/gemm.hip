@@ -40,7 +40,8 @@ struct Args {
   const bf16_t* resid; int ldr;
   float alpha; int act;
   int remap, r_ghl, r_gwl, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
-  int perm, p_cin, p_taps;
+  int perm, p_cin, p_taps, p_cvalid;
+  int m_store, n_store;
   int raw;  // 1: write raw fp32 partials (split-K), epilogue applied by the reducer
 };
 
@@ -55,6 +56,7 @@ struct Epi {
       ((float*)g.C)[(long long)z * g.split_stride + (long long)row * g.N + col] = acc;
       return;
     }
+    if (row >= g.m_store || col >= g.n_store) return;
     float v = g.alpha * acc;
     if (g.bias) v += g.bias[col];
     if (g.rowbias) v += bf2f(g.rowbias[(long long)(row >> g.rb_shift) * g.rb_ld + col]);
@@ -71,6 +73,7 @@ struct Epi {
     if (g.perm) {
       int tap = col / g.p_cin;
       int c = col - tap * g.p_cin;
+      if (c >= g.p_cvalid) return;
       ocol = (long long)c * g.p_taps + tap;
     }
     if (g.c_f32) ((float*)g.C)[orow * g.ldc + ocol] = v;
@@ -307,7 +310,8 @@ hipError_t launch_t(const Args& a, dim3 grid, hipStream_t s) {
 
 int fill_args(const sdmi_gemm_desc* d, Args& a) {
   if (!d || d->m <= 0 || d->n <= 0 || d->k <= 0) return -1;
-  if (d->k % 8) return -2;
+  // K is the contiguous (16-B chunked) dimension of row-major / conv A and of [n][k] B only
+  if ((d->a_mode != SDMI_A_COLMAJOR || d->b_mode == SDMI_B_NK) && (d->k % 8)) return -2;
   if ((d->a_mode == SDMI_A_COLMAJOR) && (d->m % 8)) return -3;
   if ((d->b_mode != SDMI_B_NK) && (d->n % 8)) return -4;
   if (d->a_mode == SDMI_A_CONV || d->b_mode == SDMI_B_KN_CONV) {
@@ -328,6 +332,9 @@ int fill_args(const sdmi_gemm_desc* d, Args& a) {
   a.remap = d->remap; a.r_ghl = d->r_gh_log2; a.r_gwl = d->r_gw_log2; a.r_oh = d->r_oh; a.r_ow = d->r_ow;
   a.r_sy = d->r_sy; a.r_sx = d->r_sx; a.r_oy = d->r_oy; a.r_ox = d->r_ox;
   a.perm = d->perm; a.p_cin = d->p_cin; a.p_taps = d->p_taps;
+  a.p_cvalid = d->p_cvalid > 0 ? d->p_cvalid : d->p_cin;
+  a.m_store = d->m_store > 0 ? d->m_store : d->m;
+  a.n_store = d->n_store > 0 ? d->n_store : d->n;
   return 0;
 }
 

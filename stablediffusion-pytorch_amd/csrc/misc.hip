@@ -1,0 +1,330 @@
+// Small fused kernels around the denoiser: input staging (mask gather + 1x1 mask projection),
+// output layout, scheduler add_noise, MSE loss, time embedding, SiLU, channel-slice copies and
+// bf16 weight packing.
+#include "common.h"
+#include "../../include/sdmi.h"
+
+namespace {
+constexpr int NT = 256;
+
+int grid_for(long long work) {
+  long long g = (work + NT - 1) / NT;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Input staging (unet_cond_base.py:131-140): x (B,cx,H,W) fp32 NCHW -> NHWC bf16 [B*H*W][cpad];
+// channels cx .. cx+cmo-1 = 1x1 conv (no bias) of the nearest-resized mask (B,cmi,MH,MW) fp32
+// (F.interpolate default 'nearest': src = min(floor(dst * (in/out)), in-1)), rest zero.
+// ---------------------------------------------------------------------------------------------
+__global__ void prep_input_kernel(const float* x, int B, int cx, int H, int W, const float* mask, int cmi, int MH,
+                                  int MW, const float* wcond, int cmo, bf16_t* out, int cpad, const float* keep) {
+  long long total = (long long)B * H * W;
+  float sh = (float)MH / (float)H, sw = (float)MW / (float)W;
+  for (long long p = (long long)blockIdx.x * NT + threadIdx.x; p < total; p += (long long)gridDim.x * NT) {
+    int b = (int)(p / (H * W));
+    int yx = (int)(p - (long long)b * H * W);
+    int y = yx / W, xx = yx - y * W;
+    float v[16];
+    for (int c = 0; c < 16; ++c) v[c] = 0.f;
+    for (int c = 0; c < cx; ++c) v[c] = x[(((long long)b * cx + c) * H + y) * W + xx];
+    if (mask) {
+      int sy = min((int)floorf((float)y * sh), MH - 1), sx = min((int)floorf((float)xx * sw), MW - 1);
+      for (int o = 0; o < cmo; ++o) {
+        float acc = 0.f;
+        for (int i = 0; i < cmi; ++i)
+          acc += wcond[o * cmi + i] * mask[(((long long)b * cmi + i) * MH + sy) * MW + sx];
+        v[cx + o] = keep ? acc * keep[b] : acc;
+      }
+    }
+    bf16_t* dst = out + p * cpad;
+    for (int c = 0; c < cpad; c += 8) *(uint4*)(dst + c) = pack8(v + c);
+  }
+}
+
+// d wcond[o][i] = sum_{b,p} dxin[p][cx + o] * mask_resized[b][i][p]    (one block per (o, i))
+__global__ void cond_wgrad_kernel(const bf16_t* dxin, int ld, int cx, int B, int H, int W, const float* mask, int cmi,
+                                  int MH, int MW, float* dw, const float* keep) {
+  int o = blockIdx.x / cmi, i = blockIdx.x - o * cmi;
+  float sh = (float)MH / (float)H, sw = (float)MW / (float)W;
+  long long total = (long long)B * H * W;
+  float acc = 0.f;
+  for (long long p = threadIdx.x; p < total; p += NT) {
+    int b = (int)(p / (H * W));
+    int yx = (int)(p - (long long)b * H * W);
+    int y = yx / W, xx = yx - y * W;
+    int sy = min((int)floorf((float)y * sh), MH - 1), sx = min((int)floorf((float)xx * sw), MW - 1);
+    float mv = mask[(((long long)b * cmi + i) * MH + sy) * MW + sx];
+    acc += bf2f(dxin[p * ld + cx + o]) * (keep ? mv * keep[b] : mv);
+  }
+  __shared__ float red[NT / 64];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < NT / 64; ++w) s += red[w];
+    dw[o * cmi + i] = s;
+  }
+}
+
+// NHWC (fp32 or bf16, row stride ld) -> NCHW fp32 (first C channels), and the reverse for gradients
+__global__ void nhwc_to_nchw_kernel(const void* src, int src_f32, int ld, int B, int C, int HW, float* dst) {
+  long long total = (long long)B * C * HW;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    int p = (int)(i % HW);
+    long long bc = i / HW;
+    int c = (int)(bc % C);
+    int b = (int)(bc / C);
+    long long s = ((long long)b * HW + p) * ld + c;
+    dst[i] = src_f32 ? ((const float*)src)[s] : bf2f(((const bf16_t*)src)[s]);
+  }
+}
+
+__global__ void nchw_to_nhwc_bf16_kernel(const float* src, int B, int C, int HW, bf16_t* dst, int ld) {
+  long long total = (long long)B * HW * ld;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    int c = (int)(i % ld);
+    long long bp = i / ld;
+    int p = (int)(bp % HW);
+    int b = (int)(bp / HW);
+    dst[i] = c < C ? f2bf(src[((long long)b * C + c) * HW + p]) : (bf16_t)0;
+  }
+}
+
+// x_t = sqrt(abar[t]) * x0 + sqrt(1-abar[t]) * eps   (scheduler :26-48; separate mul/mul/add, no FMA,
+// so the result is bit-identical to the reference's fp32 CPU arithmetic)
+__global__ void add_noise_kernel(const float* x0, const float* eps, const long long* t, const float* sa,
+                                 const float* s1a, int B, long long per, float* out) {
+#pragma clang fp contract(off)
+  long long total = (long long)B * per;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    int b = (int)(i / per);
+    long long ti = t[b];
+    out[i] = __fadd_rn(__fmul_rn(sa[ti], x0[i]), __fmul_rn(s1a[ti], eps[i]));
+  }
+}
+
+// MSE(pred, target): pred NHWC fp32 (ld), target NCHW fp32. Writes per-block partial sums and
+// grad = 2 (pred - target) / n * gscale as NHWC bf16 (ld, pad channels zero).
+__global__ void mse_kernel(const float* pred, int ld, const float* target, int B, int C, int HW, float gscale,
+                           const float* gscale_dev, bf16_t* grad, float* partial) {
+  if (gscale_dev) gscale = *gscale_dev;
+  long long total = (long long)B * HW * ld;
+  float n = (float)((long long)B * C * HW);
+  float acc = 0.f;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    int c = (int)(i % ld);
+    long long bp = i / ld;
+    int p = (int)(bp % HW);
+    int b = (int)(bp / HW);
+    float g = 0.f;
+    if (c < C) {
+      float d = pred[i] - target[((long long)b * C + c) * HW + p];
+      acc += d * d;
+      g = 2.f * d / n * gscale;
+    }
+    if (grad) grad[i] = f2bf(g);
+  }
+  __shared__ float red[NT / 64];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < NT / 64; ++w) s += red[w];
+    partial[blockIdx.x] = s;
+  }
+}
+
+__global__ void sum_partials_kernel(const float* partial, int n, float scale, float* out) {
+  __shared__ float red[NT / 64];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += NT) acc += partial[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < NT / 64; ++w) s += red[w];
+    out[0] = s * scale;
+  }
+}
+
+// sinusoidal embedding (blocks.py:5-24): [sin(t / 10000^(i/half)), cos(...)] -> bf16 [B][ld]
+__global__ void time_embedding_kernel(const long long* t, int tstride, int B, int dim, bf16_t* out, int ld,
+                                      float* out_f32) {
+  int half = dim / 2;
+  int total = B * half;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    int b = i / half, j = i - b * half;
+    float f = powf(10000.f, (float)j / (float)half);
+    float a = (float)t[b * tstride] / f;
+    float s = sinf(a), c = cosf(a);
+    out[(long long)b * ld + j] = f2bf(s);
+    out[(long long)b * ld + half + j] = f2bf(c);
+    if (out_f32) {
+      out_f32[(long long)b * dim + j] = s;
+      out_f32[(long long)b * dim + half + j] = c;
+    }
+  }
+}
+
+// y = silu(x) (bf16), or dx = dy * silu'(x) when dy != null
+__global__ void silu_kernel(const bf16_t* x, const bf16_t* dy, bf16_t* y, long long n) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    float v = bf2f(x[i]);
+    y[i] = dy ? f2bf(bf2f(dy[i]) * silu_grad_f(v)) : f2bf(silu_f(v));
+  }
+}
+
+// dst[p][0:C] (+)= src[p][0:C]  (bf16 NHWC channel slices, C % 8 == 0)
+__global__ void copy_slice_kernel(const bf16_t* src, int lds, bf16_t* dst, int ldd, long long P, int C, int accumulate) {
+  int C8 = C >> 3;
+  long long total = P * C8;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    long long p = i / C8;
+    int c = (int)(i - p * C8) * 8;
+    uint4 v = *(const uint4*)(src + p * lds + c);
+    if (accumulate) {
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(*(const uint4*)(dst + p * ldd + c), b);
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+      v = pack8(a);
+    }
+    *(uint4*)(dst + p * ldd + c) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// batched fp32 -> bf16 weight packing:  dst[o][a][b][i] = src[o*so + i*si + kh(a)*skh + kw(b)*skw]
+// with kh(a) = kh_off + kh_mul*a (identity, spatial flip, sub-pixel phase taps), zero for i >= I.
+// ---------------------------------------------------------------------------------------------
+}  // namespace
+
+extern "C" {
+typedef struct sdmi_pack_desc {
+  const float* src;
+  void* dst;
+  long long so, si, skh, skw;
+  int O, I, Ipad, KH, KW, kh_off, kh_mul, kw_off, kw_mul;
+} sdmi_pack_desc;
+}
+
+namespace {
+constexpr int PACK_CHUNK = 4096;  // elements per workgroup; bmap[blk] = (descriptor, chunk)
+__global__ void pack_kernel(const sdmi_pack_desc* descs, const int2* bmap) {
+  const int2 bm = bmap[blockIdx.x];
+  const sdmi_pack_desc& d = descs[bm.x];
+  const long long n = (long long)d.O * d.KH * d.KW * d.Ipad;
+  const long long r0 = (long long)bm.y * PACK_CHUNK;
+  for (long long r = r0 + threadIdx.x; r < n && r < r0 + PACK_CHUNK; r += NT) {
+    int i = (int)(r % d.Ipad);
+    long long r2 = r / d.Ipad;
+    int b = (int)(r2 % d.KW);
+    long long r3 = r2 / d.KW;
+    int a = (int)(r3 % d.KH);
+    int o = (int)(r3 / d.KH);
+    float v = 0.f;
+    if (i < d.I) {
+      int kh = d.kh_off + d.kh_mul * a, kw = d.kw_off + d.kw_mul * b;
+      v = d.src[o * d.so + i * d.si + kh * d.skh + kw * d.skw];
+    }
+    ((bf16_t*)d.dst)[r] = f2bf(v);
+  }
+}
+}  // namespace
+
+extern "C" int sdmi_prep_input(const float* x, int B, int cx, int H, int W, const float* mask, int cmi, int MH, int MW,
+                               const float* wcond, int cmo, void* out, int cpad, const float* keep,
+                               sdmi_stream_t stream) {
+  if (cpad % 8 || cx + (mask ? cmo : 0) > cpad || cpad > 16) return -1;
+  hipLaunchKernelGGL(prep_input_kernel, dim3(grid_for((long long)B * H * W)), dim3(NT), 0, (hipStream_t)stream, x, B, cx,
+                     H, W, mask, cmi, MH, MW, wcond, cmo, (bf16_t*)out, cpad, keep);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_cond_wgrad(const void* dxin, int ld, int cx, int B, int H, int W, const float* mask, int cmi,
+                               int MH, int MW, int cmo, float* dw, const float* keep, sdmi_stream_t stream) {
+  hipLaunchKernelGGL(cond_wgrad_kernel, dim3(cmo * cmi), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)dxin, ld, cx,
+                     B, H, W, mask, cmi, MH, MW, dw, keep);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_nhwc_to_nchw(const void* src, int src_f32, int ld, int B, int C, int HW, float* dst,
+                                 sdmi_stream_t stream) {
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for((long long)B * C * HW)), dim3(NT), 0, (hipStream_t)stream, src,
+                     src_f32, ld, B, C, HW, dst);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_nchw_to_nhwc_bf16(const float* src, int B, int C, int HW, void* dst, int ld, sdmi_stream_t stream) {
+  hipLaunchKernelGGL(nchw_to_nhwc_bf16_kernel, dim3(grid_for((long long)B * HW * ld)), dim3(NT), 0, (hipStream_t)stream,
+                     src, B, C, HW, (bf16_t*)dst, ld);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_add_noise(const float* x0, const float* eps, const long long* t, const float* sqrt_abar,
+                              const float* sqrt_one_minus_abar, int B, long long per_sample, float* out,
+                              sdmi_stream_t stream) {
+  hipLaunchKernelGGL(add_noise_kernel, dim3(grid_for((long long)B * per_sample)), dim3(NT), 0, (hipStream_t)stream, x0,
+                     eps, t, sqrt_abar, sqrt_one_minus_abar, B, per_sample, out);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" size_t sdmi_mse_workspace(void) { return 1024 * sizeof(float); }
+
+extern "C" int sdmi_mse(const float* pred, int ld, const float* target, int B, int C, int HW, float gscale,
+                        const float* gscale_dev, void* grad, float* ws, float* loss, sdmi_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  int blocks = grid_for((long long)B * HW * ld);
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(mse_kernel, dim3(blocks), dim3(NT), 0, s, pred, ld, target, B, C, HW, gscale, gscale_dev,
+                     (bf16_t*)grad, ws);
+  SDMI_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(NT), 0, s, ws, blocks, 1.0f / (float)((long long)B * C * HW),
+                     loss);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_time_embedding(const long long* t, int tstride, int B, int dim, void* out, int ld, float* out_f32,
+                                   sdmi_stream_t stream) {
+  if (dim % 2) return -1;
+  hipLaunchKernelGGL(time_embedding_kernel, dim3(grid_for((long long)B * dim / 2)), dim3(NT), 0, (hipStream_t)stream, t,
+                     tstride, B, dim, (bf16_t*)out, ld, out_f32);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_silu(const void* x, const void* dy, void* y, long long n, sdmi_stream_t stream) {
+  hipLaunchKernelGGL(silu_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     (const bf16_t*)dy, (bf16_t*)y, n);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_copy_slice(const void* src, int lds, void* dst, int ldd, long long P, int C, int accumulate,
+                               sdmi_stream_t stream) {
+  if (C % 8 || lds % 8 || ldd % 8) return -1;
+  hipLaunchKernelGGL(copy_slice_kernel, dim3(grid_for(P * C / 8)), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)src,
+                     lds, (bf16_t*)dst, ldd, P, C, accumulate);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_pack_chunk(void) { return PACK_CHUNK; }
+
+// descs_dev: device array of descriptors; bmap_dev: device array of int2 (descriptor, chunk), one per workgroup
+extern "C" int sdmi_pack_weights(const sdmi_pack_desc* descs_dev, const void* bmap_dev, int nblocks, sdmi_stream_t stream) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(pack_kernel, dim3(nblocks), dim3(NT), 0, (hipStream_t)stream, descs_dev, (const int2*)bmap_dev);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,321 @@
+// GroupNorm (+ fused SiLU) forward/backward and per-(batch, channel) pixel reductions on NHWC bf16.
+//
+// Replaces nn.GroupNorm(32, C) -> nn.SiLU() (models/blocks.py:45-47, 64-66 and the Mid/Up copies),
+// the attention pre-norms on the (B, C, HW) view (blocks.py:124-126, 137-139: same statistics as
+// 4-D) and unet_cond_base.py:179-180. Statistics are fp32 (partials) / fp64 (final merge), eps 1e-5.
+//
+// All kernels see an activation as x[b][p][c] = x[(b*P + p)*ld + c], P = H*W pixels.
+//  1. sdmi_chan_reduce  : per (b, c) partial sums over a pixel slice (grid = B x splits):
+//        mode 0: (sum x, sum x^2)                                   -> GN statistics
+//        mode 1: (sum dz, sum dz*xhat), dz = dy [* silu'(z)]          -> GN backward
+//        mode 2: (sum dy, 0)                                         -> bias / time-embedding grads
+//  2. finalize kernels turn partials into mean/rstd, GN backward coefficients, dgamma/dbeta, bias grads.
+//  3. sdmi_gn_apply / sdmi_gn_bwd_apply : vectorised elementwise passes (8 channels per lane).
+#include "common.h"
+#include "../../include/sdmi.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+struct RedArgs {
+  const bf16_t* x; int ldx;   // GN input
+  const bf16_t* dy; int ldy;  // upstream grad (modes 1, 2)
+  const float* mean; const float* rstd; const float* gamma; const float* beta;
+  int B, P, C, G, silu, mode, splits;
+  float* part;  // [B][splits][C][2]
+};
+
+__global__ __launch_bounds__(NT) void chan_reduce_kernel(RedArgs a) {
+  const int b = blockIdx.x, sp = blockIdx.y;
+  const int C8 = a.C >> 3;
+  const int rows = NT / C8;  // pixel rows processed per iteration
+  const int t = threadIdx.x;
+  const int col = t % C8, r = t / C8;
+  const bool active = r < rows;
+  const int p_per = (a.P + a.splits - 1) / a.splits;
+  const int p0 = sp * p_per, p1 = min(a.P, p0 + p_per);
+  const int c0 = col * 8;
+  const int Cg = a.C / a.G;
+
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  float mu[8], rs[8], ga[8], be[8];
+  if (a.mode == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int g = (c0 + e) / Cg;
+      mu[e] = a.mean[b * a.G + g];
+      rs[e] = a.rstd[b * a.G + g];
+      ga[e] = a.gamma[c0 + e];
+      be[e] = a.beta[c0 + e];
+    }
+  }
+  if (active) {
+    for (int p = p0 + r; p < p1; p += rows) {
+      long long pix = (long long)b * a.P + p;
+      float xv[8], gv[8];
+      if (a.mode == 0) {
+        unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] += xv[e]; s2[e] += xv[e] * xv[e]; }
+      } else if (a.mode == 1) {
+        unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
+        unpack8(*(const uint4*)(a.dy + pix * a.ldy + c0), gv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float xh = (xv[e] - mu[e]) * rs[e];
+          float dz = gv[e];
+          if (a.silu) dz *= silu_grad_f(xh * ga[e] + be[e]);
+          s1[e] += dz;
+          s2[e] += dz * xh;
+        }
+      } else {
+        unpack8(*(const uint4*)(a.dy + pix * a.ldy + c0), gv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s1[e] += gv[e];
+      }
+    }
+  }
+  // reduce across the `rows` threads sharing a column
+  __shared__ float red[NT][17];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[t][e] = s1[e]; red[t][8 + e] = s2[e]; }
+  __syncthreads();
+  // thread j < C (channel) sums over rows
+  for (int ch = t; ch < a.C; ch += NT) {
+    int cc = ch >> 3, e = ch & 7;
+    float u = 0.f, v = 0.f;
+    for (int rr = 0; rr < rows; ++rr) {
+      u += red[rr * C8 + cc][e];
+      v += red[rr * C8 + cc][8 + e];
+    }
+    float* o = a.part + (((long long)b * a.splits + sp) * a.C + ch) * 2;
+    o[0] = u;
+    o[1] = v;
+  }
+}
+
+// mean/rstd per (b, g) from partial sums
+__global__ void gn_stats_finalize_kernel(const float* part, int B, int splits, int C, int G, int P, float eps,
+                                         float* mean, float* rstd) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * G) return;
+  int b = idx / G, g = idx - b * G;
+  int Cg = C / G;
+  double s1 = 0, s2 = 0;
+  for (int sp = 0; sp < splits; ++sp)
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      const float* o = part + (((long long)b * splits + sp) * C + c) * 2;
+      s1 += o[0];
+      s2 += o[1];
+    }
+  double n = (double)P * Cg;
+  double mu = s1 / n;
+  double var = s2 / n - mu * mu;
+  if (var < 0) var = 0;
+  mean[idx] = (float)mu;
+  rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// GN backward coefficients per (b, g): A = sum_c gamma_c * S1[b,c], Bc = sum_c gamma_c * S2[b,c]
+// and per-channel dgamma = sum_b S2, dbeta = sum_b S1.
+__global__ void gn_bwd_finalize_kernel(const float* part, int B, int splits, int C, int G, const float* gamma,
+                                       float* coef /*[B][G][2]*/, float* dgamma, float* dbeta) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  int Cg = C / G;
+  if (idx < B * G) {
+    int b = idx / G, g = idx - b * G;
+    float A = 0.f, Bc = 0.f;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      float u = 0.f, v = 0.f;
+      for (int sp = 0; sp < splits; ++sp) {
+        const float* o = part + (((long long)b * splits + sp) * C + c) * 2;
+        u += o[0];
+        v += o[1];
+      }
+      A += gamma[c] * u;
+      Bc += gamma[c] * v;
+    }
+    coef[idx * 2] = A;
+    coef[idx * 2 + 1] = Bc;
+  }
+  if (idx < C && dgamma) {
+    float u = 0.f, v = 0.f;
+    for (int b = 0; b < B; ++b)
+      for (int sp = 0; sp < splits; ++sp) {
+        const float* o = part + (((long long)b * splits + sp) * C + idx) * 2;
+        u += o[0];
+        v += o[1];
+      }
+    dbeta[idx] = u;
+    dgamma[idx] = v;
+  }
+}
+
+// per-(b,c) sums (mode 2) -> per_bc[b*ld + c] (bf16) and per_c[c] = per_c2[c] = sum_b (fp32)
+__global__ void chan_sum_finalize_kernel(const float* part, int B, int splits, int C, bf16_t* per_bc, int ld,
+                                         float* per_c, float* per_c2, int c_store) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < B * C && per_bc) {
+    int b = idx / C, c = idx - b * C;
+    float u = 0.f;
+    for (int sp = 0; sp < splits; ++sp) u += part[(((long long)b * splits + sp) * C + c) * 2];
+    per_bc[(long long)b * ld + c] = f2bf(u);
+  }
+  if (idx < c_store && (per_c || per_c2)) {
+    float u = 0.f;
+    for (int b = 0; b < B; ++b)
+      for (int sp = 0; sp < splits; ++sp) u += part[(((long long)b * splits + sp) * C + idx) * 2];
+    if (per_c) per_c[idx] = u;
+    if (per_c2) per_c2[idx] = u;
+  }
+}
+
+struct ApplyArgs {
+  const bf16_t* x; int ldx;
+  bf16_t* y; int ldy;
+  const bf16_t* dy; int lddy;
+  bf16_t* dx; int lddx;
+  const float* mean; const float* rstd; const float* gamma; const float* beta; const float* coef;
+  const bf16_t* add; int ldadd;
+  int B, P, C, G, silu;
+};
+
+__global__ __launch_bounds__(NT) void gn_apply_kernel(ApplyArgs a) {
+  const int C8 = a.C >> 3;
+  long long total = (long long)a.B * a.P * C8;
+  const int Cg = a.C / a.G;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    long long pix = i / C8;
+    int c0 = (int)(i - pix * C8) * 8;
+    int b = (int)(pix / a.P);
+    float xv[8], yv[8];
+    unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int g = (c0 + e) / Cg;
+      float z = (xv[e] - a.mean[b * a.G + g]) * a.rstd[b * a.G + g] * a.gamma[c0 + e] + a.beta[c0 + e];
+      yv[e] = a.silu ? silu_f(z) : z;
+    }
+    *(uint4*)(a.y + pix * a.ldy + c0) = pack8(yv);
+  }
+}
+
+// dx = rstd * (dz*gamma - A/n - xhat*Bc/n)
+__global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
+  const int C8 = a.C >> 3;
+  long long total = (long long)a.B * a.P * C8;
+  const int Cg = a.C / a.G;
+  const float inv_n = 1.0f / ((float)a.P * Cg);
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    long long pix = i / C8;
+    int c0 = (int)(i - pix * C8) * 8;
+    int b = (int)(pix / a.P);
+    float xv[8], gv[8], ov[8], av[8];
+    unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
+    unpack8(*(const uint4*)(a.dy + pix * a.lddy + c0), gv);
+    if (a.add) unpack8(*(const uint4*)(a.add + pix * a.ldadd + c0), av);
+    else for (int e = 0; e < 8; ++e) av[e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int g = (c0 + e) / Cg;
+      int bg = b * a.G + g;
+      float rs = a.rstd[bg];
+      float xh = (xv[e] - a.mean[bg]) * rs;
+      float dz = gv[e];
+      if (a.silu) dz *= silu_grad_f(xh * a.gamma[c0 + e] + a.beta[c0 + e]);
+      ov[e] = av[e] + rs * (dz * a.gamma[c0 + e] - a.coef[bg * 2] * inv_n - xh * a.coef[bg * 2 + 1] * inv_n);
+    }
+    *(uint4*)(a.dx + pix * a.lddx + c0) = pack8(ov);
+  }
+}
+
+int pick_splits(int B, int P) {
+  int s = 1;
+  while (B * s < 512 && P / (s * 2) >= 16) s *= 2;
+  return s;
+}
+
+int grid_for(long long work) {
+  long long g = (work + NT - 1) / NT;
+  return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+extern "C" size_t sdmi_chan_reduce_workspace(int B, int P, int C) {
+  return (size_t)B * pick_splits(B, P) * C * 2 * sizeof(float);
+}
+
+extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, float* ws, float* mean,
+                             float* rstd, sdmi_stream_t stream) {
+  if (C % 8 || C > 8 * NT || G <= 0 || C % G) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  RedArgs a = {};
+  a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.mode = 0;
+  a.splits = pick_splits(B, P); a.part = ws;
+  hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, a.splits), dim3(NT), 0, s, a);
+  SDMI_CHECK_LAUNCH();
+  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3((B * G + 255) / 256), dim3(256), 0, s, ws, B, a.splits, C, G, P,
+                     eps, mean, rstd);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* mean, const float* rstd,
+                             const float* gamma, const float* beta, int B, int P, int C, int G, int silu,
+                             sdmi_stream_t stream) {
+  if (C % 8 || C % G) return -1;
+  ApplyArgs a = {};
+  a.x = (const bf16_t*)x; a.ldx = ldx; a.y = (bf16_t*)y; a.ldy = ldy;
+  a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.B = B; a.P = P; a.C = C; a.G = G; a.silu = silu;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid_for((long long)B * P * C / 8)), dim3(NT), 0, (hipStream_t)stream, a);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* mean,
+                           const float* rstd, const float* gamma, const float* beta, int B, int P, int C, int G,
+                           int silu, float* ws, float* coef_ws, float* dgamma, float* dbeta, const void* addend,
+                           int ldadd, sdmi_stream_t stream) {
+  if (C % 8 || C > 8 * NT || C % G) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  RedArgs r = {};
+  r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy;
+  r.mean = mean; r.rstd = rstd; r.gamma = gamma; r.beta = beta;
+  r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.mode = 1; r.splits = pick_splits(B, P); r.part = ws;
+  hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, r.splits), dim3(NT), 0, s, r);
+  SDMI_CHECK_LAUNCH();
+  int n = B * G > C ? B * G : C;
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ws, B, r.splits, C, G, gamma,
+                     coef_ws, dgamma, dbeta);
+  SDMI_CHECK_LAUNCH();
+  ApplyArgs a = {};
+  a.x = (const bf16_t*)x; a.ldx = ldx; a.dy = (const bf16_t*)dy; a.lddy = lddy; a.dx = (bf16_t*)dx; a.lddx = lddx;
+  a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.coef = coef_ws;
+  a.add = (const bf16_t*)addend; a.ldadd = ldadd;
+  a.B = B; a.P = P; a.C = C; a.G = G; a.silu = silu;
+  hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3(grid_for((long long)B * P * C / 8)), dim3(NT), 0, s, a);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// per-(b, c) and per-c sums of dy over pixels (bias and time-embedding-bias gradients)
+extern "C" int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, float* ws, void* per_bc, int ld_bc,
+                             float* per_c, float* per_c2, int c_store, sdmi_stream_t stream) {
+  if (c_store <= 0 || c_store > C) c_store = C;
+  if (C % 8 || C > 8 * NT) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  RedArgs r = {};
+  r.dy = (const bf16_t*)dy; r.ldy = lddy; r.B = B; r.P = P; r.C = C; r.G = 1; r.mode = 2;
+  r.splits = pick_splits(B, P); r.part = ws;
+  hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, r.splits), dim3(NT), 0, s, r);
+  SDMI_CHECK_LAUNCH();
+  int n = B * C;
+  hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ws, B, r.splits, C,
+                     (bf16_t*)per_bc, ld_bc, per_c, per_c2, c_store);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}

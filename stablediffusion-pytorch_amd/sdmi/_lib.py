@@ -34,7 +34,8 @@ class GemmDesc(ctypes.Structure):
         ("remap", ctypes.c_int), ("r_gh_log2", ctypes.c_int), ("r_gw_log2", ctypes.c_int),
         ("r_oh", ctypes.c_int), ("r_ow", ctypes.c_int), ("r_sy", ctypes.c_int), ("r_sx", ctypes.c_int),
         ("r_oy", ctypes.c_int), ("r_ox", ctypes.c_int),
-        ("perm", ctypes.c_int), ("p_cin", ctypes.c_int), ("p_taps", ctypes.c_int),
+        ("perm", ctypes.c_int), ("p_cin", ctypes.c_int), ("p_taps", ctypes.c_int), ("p_cvalid", ctypes.c_int),
+        ("m_store", ctypes.c_int), ("n_store", ctypes.c_int),
     ]
 
 
@@ -42,9 +43,42 @@ _lib = None
 
 # (name, argtypes) of every exported entry point; used for loading and for the export test.
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlong
+_SZ = ctypes.c_size_t
+
+
+class PackDesc(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p),
+                ("so", ctypes.c_longlong), ("si", ctypes.c_longlong), ("skh", ctypes.c_longlong),
+                ("skw", ctypes.c_longlong)] + [(n, ctypes.c_int) for n in
+                                                ("O", "I", "Ipad", "KH", "KW", "kh_off", "kh_mul", "kw_off", "kw_mul")]
+
+
 SIGNATURES = {
-    "sdmi_gemm_plan": [ctypes.POINTER(GemmDesc), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)],
-    "sdmi_gemm": [ctypes.POINTER(GemmDesc), _P, ctypes.c_size_t, _P],
+    "sdmi_gemm_plan": ([ctypes.POINTER(GemmDesc), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)], _I),
+    "sdmi_gemm": ([ctypes.POINTER(GemmDesc), _P, _SZ, _P], _I),
+    "sdmi_attn_fwd": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _P], _I),
+    "sdmi_attn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I,
+                       _I, _I, _I, _I, _I, _P], _I),
+    "sdmi_chan_reduce_workspace": ([_I, _I, _I], _SZ),
+    "sdmi_gn_stats": ([_P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P], _I),
+    "sdmi_gn_apply": ([_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P], _I),
+    "sdmi_gn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P], _I),
+    "sdmi_chan_sum": ([_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _I, _P], _I),
+    "sdmi_prep_input": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),
+    "sdmi_cond_wgrad": ([_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P], _I),
+    "sdmi_nhwc_to_nchw": ([_P, _I, _I, _I, _I, _I, _P, _P], _I),
+    "sdmi_nchw_to_nhwc_bf16": ([_P, _I, _I, _I, _P, _I, _P], _I),
+    "sdmi_add_noise": ([_P, _P, _P, _P, _P, _I, _L, _P, _P], _I),
+    "sdmi_mse_workspace": ([], _SZ),
+    "sdmi_mse": ([_P, _I, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
+    "sdmi_time_embedding": ([_P, _I, _I, _I, _P, _I, _P, _P], _I),
+    "sdmi_silu": ([_P, _P, _P, _L, _P], _I),
+    "sdmi_copy_slice": ([_P, _I, _P, _I, _L, _I, _I, _P], _I),
+    "sdmi_pack_chunk": ([], _I),
+    "sdmi_pack_weights": ([_P, _P, _I, _P], _I),
+    "sdmi_optim_workspace": ([], _SZ),
+    "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
+    "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P], _I),
 }
 
 
@@ -55,10 +89,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libsdmi.so not built ({LIB_PATH}); run __graft_entry__.build()")
         L = ctypes.CDLL(LIB_PATH)
-        for name, argt in SIGNATURES.items():
+        for name, (argt, rest) in SIGNATURES.items():
             fn = getattr(L, name)
             fn.argtypes = argt
-            fn.restype = ctypes.c_int
+            fn.restype = rest
         _lib = L
     return _lib
 

@@ -27,8 +27,12 @@ def _log2(v):
     return l
 
 
+# optional per-launch timing hook (bench.py): list of (tag, flops, start_event, end_event)
+PROFILE = None
+
+
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
-         rb_ld=0, rb_shift=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None):
+         rb_ld=0, rb_shift=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0):
     """C[m][n] = epi(sum_k A[m][k] B[k][n]).  a/b/c/resid/rowbias are tensors (pointer = data_ptr,
     offsets already applied by slicing); see include/sdmi.h for the operand modes."""
     L = _lib.lib()
@@ -54,15 +58,24 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
         d.remap = 1
     if perm is not None:
         d.perm = 1
-        d.p_cin, d.p_taps = perm
+        d.p_cin, d.p_taps = perm[0], perm[1]
+        d.p_cvalid = perm[2] if len(perm) > 2 else 0
+    d.m_store, d.n_store = m_store, n_store
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
     ws = None
     if ws_bytes.value:
         ws = torch.empty(ws_bytes.value // 4, dtype=torch.float32, device=c.device)
+    if PROFILE is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     check(L.sdmi_gemm(ctypes.byref(d), ws.data_ptr() if ws is not None else None, ws_bytes.value, _stream()),
           "sdmi_gemm")
+    if PROFILE is not None:
+        ev1.record()
+        PROFILE.append((f"gemm_a{a_mode}b{b_mode}", 2.0 * m * n * k, ev0, ev1, splits.value))
     return c
 
 
@@ -76,7 +89,7 @@ def conv_geom(ih, iw, cin, ldx, kh, kw, oh, ow, sy, sx, oy0, ox0):
 
 
 def conv_fwd(x, B, H, W, cin, ldx, wpk, cout, kh, kw, stride, pad, out, ldo, *, bias=None, rowbias=None,
-             resid=None, ldr=0, act=0):
+             rb_ld=0, resid=None, ldr=0, act=0, n_store=0):
     """y[b,oy,ox,co] = sum_{ty,tx,ci} x[b, oy*s+ty-pad, ox*s+tx-pad, ci] * wpk[co, (ty*kw+tx)*cin + ci].
     x: NHWC bf16 buffer (row stride ldx), wpk: bf16 [cout][kh*kw*cin]."""
     OH = (H + 2 * pad - kh) // stride + 1
@@ -84,16 +97,18 @@ def conv_fwd(x, B, H, W, cin, ldx, wpk, cout, kh, kw, stride, pad, out, ldo, *, 
     g = conv_geom(H, W, cin, ldx, kh, kw, OH, OW, stride, stride, -pad, -pad)
     rb_shift = _log2(OH * OW)
     return gemm(B * OH * OW, cout, kh * kw * cin, x, _lib.A_CONV, 0, wpk, _lib.B_NK, kh * kw * cin, out, ldo,
-                geom=g, bias=bias, rowbias=rowbias, rb_ld=cout if rowbias is not None else 0, rb_shift=rb_shift,
-                resid=resid, ldr=ldr, act=act)
+                geom=g, bias=bias, rowbias=rowbias, rb_ld=(rb_ld or cout) if rowbias is not None else 0,
+                rb_shift=rb_shift, resid=resid, ldr=ldr, act=act, n_store=n_store)
 
 
-def conv_wgrad(dy, ldy, x, B, H, W, cin, ldx, cout, kh, kw, stride, pad, out, OH, OW, *, perm=True):
+def conv_wgrad(dy, ldy, x, B, H, W, cin, ldx, cout, kh, kw, stride, pad, out, OH, OW, *, perm=True, cvalid=0,
+               m_store=0):
     """dW[co][(ty,tx,ci)] = sum_pixels dy[p, co] * x[gather(p, ty, tx), ci]; written fp32 in torch
-    layout (co, ci, kh, kw) when perm."""
+    layout (co, ci, kh, kw) when perm (only ci < cvalid, co < m_store when given)."""
     g = conv_geom(H, W, cin, ldx, kh, kw, OH, OW, stride, stride, -pad, -pad)
+    cv = cvalid or cin
     return gemm(cout, kh * kw * cin, B * OH * OW, dy, _lib.A_COLMAJOR, ldy, x, _lib.B_KN_CONV, 0, out,
-                kh * kw * cin, geom=g, perm=(cin, kh * kw) if perm else None)
+                kh * kw * cv, geom=g, perm=(cin, kh * kw, cv) if perm else None, m_store=m_store)
 
 
 # stride-2, 4x4, pad-1 transposed convolution as four 2x2 sub-pixel convolutions.
@@ -112,3 +127,126 @@ def convT_fwd_phases(x, B, H, W, cin, ldx, wph, cout, out, ldo, *, bias=None, re
             gemm(B * H * W, cout, 4 * cin, x, _lib.A_CONV, 0, wph[ph * 2 + pw], _lib.B_NK, 4 * cin, out, ldo,
                  geom=g, bias=bias, resid=resid, ldr=ldr, remap=remap)
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# tensor helpers
+# ------------------------------------------------------------------------------------------------
+def ld_of(t):
+    """row stride (elements) of a 2-D [rows, C] view with unit column stride."""
+    assert t.dim() == 2 and t.stride(1) == 1, "activation views must be 2-D with unit column stride"
+    return t.stride(0)
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def linear(x, w, out, *, bias=None, resid=None, act=0, alpha=1.0, n_store=0):
+    """out[m][n] = act(alpha * x[m] . w[n] + bias[n] + resid[m][n]);  x [M,K] bf16 view, w [N,K] bf16."""
+    M, K = x.shape
+    N = w.shape[0]
+    return gemm(M, N, K, x, _lib.A_ROWMAJOR, ld_of(x), w, _lib.B_NK, K, out, ld_of(out), bias=bias, resid=resid,
+                ldr=ld_of(resid) if resid is not None else 0, act=act, alpha=alpha)
+
+
+def linear_dgrad(dy, w, out, *, resid=None):
+    """out[m][k] = sum_n dy[m][n] w[n][k] (+ resid);  w [N,K] bf16 used as B[k=n][n=k] (row-major)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    return gemm(M, K, N, dy, _lib.A_ROWMAJOR, ld_of(dy), w, _lib.B_KN, K, out, ld_of(out), resid=resid,
+                ldr=ld_of(resid) if resid is not None else 0)
+
+
+def linear_wgrad(dy, x, out):
+    """out[n][k] = sum_m dy[m][n] x[m][k]  (fp32 weight gradient, out [N,K] contiguous rows)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    return gemm(N, K, M, dy, _lib.A_COLMAJOR, ld_of(dy), x, _lib.B_KN, ld_of(x), out, out.stride(0))
+
+
+def gn_stats(x, B, P, C, G, eps=1e-5):
+    L = _lib.lib()
+    ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=x.device)
+    mean = torch.empty(B * G, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    check(L.sdmi_gn_stats(_p(x), ld_of(x), B, P, C, G, eps, _p(ws), _p(mean), _p(rstd), _stream()), "sdmi_gn_stats")
+    return mean, rstd
+
+
+def gn_apply(x, mean, rstd, gamma, beta, B, P, C, G, silu, out):
+    check(_lib.lib().sdmi_gn_apply(_p(x), ld_of(x), _p(out), ld_of(out), _p(mean), _p(rstd), _p(gamma), _p(beta),
+                                   B, P, C, G, 1 if silu else 0, _stream()), "sdmi_gn_apply")
+    return out
+
+
+def gn_bwd(x, dy, dx, mean, rstd, gamma, beta, B, P, C, G, silu, dgamma, dbeta, addend=None):
+    L = _lib.lib()
+    ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=x.device)
+    coef = torch.empty(B * G * 2, dtype=torch.float32, device=x.device)
+    check(L.sdmi_gn_bwd(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(mean), _p(rstd), _p(gamma),
+                        _p(beta), B, P, C, G, 1 if silu else 0, _p(ws), _p(coef), _p(dgamma), _p(dbeta),
+                        _p(addend), ld_of(addend) if addend is not None else 0, _stream()), "sdmi_gn_bwd")
+    return dx
+
+
+def chan_sum(dy, B, P, C, *, per_bc=None, per_c=None, per_c2=None, c_store=0):
+    """per-(b,c) sums over pixels -> per_bc (bf16 2-D view [B, ld]) and per-channel sums (fp32)."""
+    if C > 1024:  # the reduction kernel covers <= 2048 channels per launch; split wide rows
+        for c0 in range(0, C, 1024):
+            c1 = min(C, c0 + 1024)
+            chan_sum(dy[:, c0:c1], B, P, c1 - c0,
+                     per_bc=per_bc[:, c0:c1] if per_bc is not None else None,
+                     per_c=per_c[c0:c1] if per_c is not None else None,
+                     per_c2=per_c2[c0:c1] if per_c2 is not None else None)
+        return
+    L = _lib.lib()
+    ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=dy.device)
+    check(L.sdmi_chan_sum(_p(dy), ld_of(dy), B, P, C, _p(ws), _p(per_bc), ld_of(per_bc) if per_bc is not None else 0,
+                          _p(per_c), _p(per_c2), c_store, _stream()), "sdmi_chan_sum")
+
+
+def attn_fwd(q, k, v, out, B, H, N, S, d):
+    lse = torch.empty(B * H * N, dtype=torch.float32, device=q.device)
+    check(_lib.lib().sdmi_attn_fwd(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(out), ld_of(out), _p(lse),
+                                   B, H, N, S, d, _stream()), "sdmi_attn_fwd")
+    return lse
+
+
+def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, B, H, N, S, d):
+    delta = torch.empty(B * H * N, dtype=torch.float32, device=q.device)
+    check(_lib.lib().sdmi_attn_bwd(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(o), ld_of(o), _p(dout),
+                                   ld_of(dout), _p(lse), _p(delta), _p(dq), ld_of(dq), _p(dk), ld_of(dk), _p(dv),
+                                   ld_of(dv), B, H, N, S, d, _stream()), "sdmi_attn_bwd")
+
+
+def conv_dgrad_phases(dy, B, H, W, cout, ldy, wph, cin, out, ldo, *, resid=None, ldr=0):
+    """Gradient of a k4 s2 p1 convolution (input H x W -> output H/2 x W/2) w.r.t. its input, as four
+    2x2 sub-pixel convolutions over dy (B, H/2, W/2, cout). wph[ph*2+pw]: bf16 [cin][2*2*cout]."""
+    h, w = H // 2, W // 2
+    for ph in range(2):
+        for pw in range(2):
+            g = conv_geom(h, w, cout, ldy, 2, 2, h, w, 1, 1, ph - 1, pw - 1)
+            remap = (_log2(h), _log2(w), H, W, 2, 2, ph, pw)
+            gemm(B * h * w, cin, 4 * cout, dy, _lib.A_CONV, 0, wph[ph * 2 + pw], _lib.B_NK, 4 * cout, out, ldo,
+                 geom=g, resid=resid, ldr=ldr, remap=remap)
+    return out
+
+
+def add_noise(x0, eps, t, sqrt_abar, sqrt_1m_abar, out):
+    B = x0.shape[0]
+    check(_lib.lib().sdmi_add_noise(_p(x0), _p(eps), _p(t), _p(sqrt_abar), _p(sqrt_1m_abar), B, x0.numel() // B,
+                                    _p(out), _stream()), "sdmi_add_noise")
+    return out
+
+
+def mse(pred, ld, target, B, C, HW, gscale, grad, loss, gscale_dev=None):
+    ws = torch.empty(_lib.lib().sdmi_mse_workspace() // 4, dtype=torch.float32, device=pred.device)
+    check(_lib.lib().sdmi_mse(_p(pred), ld, _p(target), B, C, HW, gscale, _p(gscale_dev), _p(grad), _p(ws), _p(loss),
+                              _stream()), "sdmi_mse")
+
+
+def copy_slice(src, dst, accumulate=False):
+    P, C = src.shape
+    check(_lib.lib().sdmi_copy_slice(_p(src), ld_of(src), _p(dst), ld_of(dst), P, C, 1 if accumulate else 0,
+                                     _stream()), "sdmi_copy_slice")

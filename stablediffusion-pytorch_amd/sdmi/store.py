@@ -1,0 +1,87 @@
+"""Flat fp32 parameter / gradient storage for the UNet family.
+
+Every parameter (and its gradient) is a view into one flat fp32 buffer, ordered so that
+  * the backward pass produces gradients roughly front-to-back (buckets can be all-reduced while
+    the rest of the backward runs),
+  * all t_emb_layers weights / biases form single contiguous runs (one GEMM covers them),
+  * the optimizer is one elementwise pass over three flat buffers.
+Keys are the reference's state-dict keys (models/unet_cond_base.py, models/blocks.py)."""
+import re
+
+import torch
+
+from .unet_engine import layout, resnet_list
+
+
+def param_label(key):
+    """Block label (engine tape label) whose backward finalises this parameter's gradient."""
+    m = re.match(r"(downs|mids|ups)\.(\d+)\.", key)
+    if ".t_emb_layers." in key and key.endswith(".weight"):
+        return "time"  # one GEMM for all t_emb_layers weights, after every block
+    if m:
+        return f"{m.group(1)}.{m.group(2)}"
+    if key.startswith("norm_out") or key.startswith("conv_out"):
+        return "head"
+    if key.startswith("t_proj") or key.startswith("class_emb"):
+        return "time"
+    return "input"
+
+
+def flat_order(cfg, keys):
+    L = layout(cfg)
+    nd = len(L["down"]) - 1
+    nm = len(L["mid"]) - 1
+    res = resnet_list(L)
+    tw = [f"{p}.t_emb_layers.{l}.1.weight" for (p, l, ci, co) in res]
+    tb = [f"{p}.t_emb_layers.{l}.1.bias" for (p, l, ci, co) in res]
+    special = set(tw) | set(tb)
+
+    def rank(k):
+        m = re.match(r"(downs|mids|ups)\.(\d+)\.", k)
+        if k.startswith("norm_out") or k.startswith("conv_out"):
+            return 0
+        if m:
+            kind, i = m.group(1), int(m.group(2))
+            if kind == "ups":
+                return 1 + (nd - 1 - i)
+            if kind == "mids":
+                return 1 + nd + (nm - 1 - i)
+            return 1 + nd + nm + (nd - 1 - i)
+        return 10_000  # t_proj, conv_in, cond_conv_in, class_emb: last in backward
+
+    rest = sorted([k for k in keys if k not in special], key=lambda k: (rank(k), keys.index(k)))
+    tail = [k for k in rest if rank(k) == 10_000]
+    body = [k for k in rest if rank(k) != 10_000]
+    return body + tw + tb + tail
+
+
+class FlatStore:
+    def __init__(self, shapes, cfg, device, with_grads=True):
+        keys = list(shapes.keys())
+        self.order = flat_order(cfg, keys)
+        self.shapes = dict(shapes)
+        self.offsets = {}
+        off = 0
+        for k in self.order:
+            n = 1
+            for s in shapes[k]:
+                n *= s
+            self.offsets[k] = (off, n)
+            off += n
+        self.numel = off
+        self.params = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grads = torch.zeros(off, dtype=torch.float32, device=device) if with_grads else None
+        self.p = {k: self.view(self.params, k) for k in self.order}
+        self.g = {k: self.view(self.grads, k) for k in self.order} if with_grads else None
+
+    def view(self, flat, k):
+        off, n = self.offsets[k]
+        return flat[off:off + n].view(self.shapes[k])
+
+    def load(self, state_dict):
+        with torch.no_grad():
+            for k in self.order:
+                self.p[k].copy_(state_dict[k])
+
+    def state_dict(self):
+        return {k: self.p[k] for k in self.shapes}

@@ -1,0 +1,120 @@
+"""The reference's DDPM training step (train_ddpm_cond_celebhq_multi_gpu.py:299-378) as one stream of
+gfx950 kernels:
+
+    add_noise -> UNet forward -> MSE (x loss scale) -> UNet backward
+      (-> bucketed RCCL all-reduce overlapped with the backward, N > 1)
+    -> unscale / clip_grad_norm(1.0) / non-finite skip -> Adam(lr) -> EMA(0.9999)
+    -> bf16 GEMM-layout weight repack for the next step
+
+Master weights, Adam moments and the EMA copy are flat fp32 buffers (sdmi.store.FlatStore order), the
+GradScaler state (scale, growth tracker, step, skip flag) lives on the device, so a step never
+synchronises with the host (the reference's .item()/isfinite syncs at :348-371 become device flags)."""
+import math
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from . import kernels as K
+from .reducer import BucketReducer
+from .store import FlatStore, param_label
+from .unet_engine import UNetEngine
+
+# state vector layout (see csrc/optim.hip)
+S_NORM, S_COEF, S_SCALE, S_GROWTH, S_STEP, S_SKIP, S_LOSS = range(7)
+
+
+def scheduler_tables(num_timesteps, beta_start, beta_end):
+    """Reference scheduler tables (scheduler/linear_noise_scheduler.py:18-24), built on the host in fp32."""
+    betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, num_timesteps) ** 2
+    abar = torch.cumprod(1. - betas, dim=0)
+    return torch.sqrt(abar), torch.sqrt(1 - abar)
+
+
+class DDPMTrainer:
+    def __init__(self, cfg, state_dict, device, *, base="cond", lr=1e-5, betas=(0.9, 0.999), eps=1e-8,
+                 max_grad_norm=1.0, ema_decay=0.9999, init_scale=65536.0, growth_interval=2000,
+                 sched=(1000, 0.00085, 0.012), group=None, bucket_bytes=64 << 20):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        shapes = {k: tuple(v.shape) for k, v in state_dict.items()}
+        self.store = FlatStore(shapes, cfg, self.device)
+        self.store.load(state_dict)
+        self.ema = self.store.params.clone()
+        self.m = torch.zeros_like(self.store.params)
+        self.v = torch.zeros_like(self.store.params)
+        self.state = torch.tensor([0, 0, init_scale, 0, 0, 0, 0, 0], dtype=torch.float32, device=self.device)
+        self.hp = dict(lr=lr, b1=betas[0], b2=betas[1], eps=eps, clip=max_grad_norm, ema=ema_decay,
+                       growth=growth_interval)
+        self.engine = UNetEngine(cfg, self.store.p, self.store.g, base=base)
+        sa, s1a = scheduler_tables(*sched)
+        self.sqrt_abar, self.sqrt_1m_abar = sa.to(self.device), s1a.to(self.device)
+        self.group = group
+        self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
+        self.reducer = BucketReducer(self.store.grads, group, bucket_bytes) if self.world > 1 else None
+        self._progress = None
+        self.engine.refresh_weights()
+
+    # ------------------------------------------------------------------------------------------
+    def _watermarks(self, tape):
+        """Per backward position k: flat offset below which every gradient is final."""
+        done_at = {}
+        for k in range(len(tape) - 1, -1, -1):  # a label is complete at its earliest tape entry
+            done_at[tape[k][1]["label"]] = k
+        order = self.store.order
+        comp = [done_at.get(param_label(key), 0) for key in order]
+        # prefix minimum of completion index over the flat order: prefix final once k <= that value
+        marks = []
+        run = math.inf
+        for key, c in zip(order, comp):
+            run = min(run, c)
+            marks.append((self.store.offsets[key][0] + self.store.offsets[key][1], run))
+        return marks
+
+    def _on_progress(self, tape, k):
+        # after finishing entry k (going backwards), every param whose label completed at >= k is final
+        marks = self._progress
+        upto = 0
+        for end, run in marks:
+            if run >= k:
+                upto = end
+            else:
+                break
+        self.reducer.ready(upto)
+
+    # ------------------------------------------------------------------------------------------
+    def step(self, x0, noise, t, text=None, mask=None, mask_keep=None):
+        """One training step on device tensors: x0/noise (B,4,H,W) fp32, t (B,) int64, text (B,S,C) fp32,
+        mask (B,18,MH,MW) fp32 (one-hot), mask_keep (B,) fp32 cond-drop multipliers or None."""
+        eng, st = self.engine, self.store
+        B, C, H, W = x0.shape
+        xt = torch.empty_like(x0)
+        K.add_noise(x0, noise, t, self.sqrt_abar, self.sqrt_1m_abar, xt)
+        pred, ctx = eng.forward(xt, t, text, mask, mask_keep=mask_keep)
+        dpred = torch.empty(B * H * W, 8, dtype=torch.bfloat16, device=self.device)
+        K.mse(pred, 8, noise, B, C, H * W, 1.0, dpred, self.state[S_LOSS:S_LOSS + 1],
+              gscale_dev=self.state[S_SCALE:S_SCALE + 1])
+        if self.reducer is not None:
+            self.reducer.reset()
+            if self._progress is None:
+                self._progress = self._watermarks(ctx["tape"])
+            eng.backward(ctx, dpred, on_progress=self._on_progress)
+            self.reducer.finish()
+        else:
+            eng.backward(ctx, dpred)
+        L = _lib.lib()
+        ws = torch.empty(L.sdmi_optim_workspace() // 4, dtype=torch.float32, device=self.device)
+        hp = self.hp
+        _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(), ws.data_ptr(),
+                                       hp["growth"], 1, float(self.world), K._stream()), "sdmi_clip_unscale")
+        _lib.check(L.sdmi_adam_ema(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                                   self.ema.data_ptr(), st.numel, self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"],
+                                   hp["eps"], hp["ema"], K._stream()), "sdmi_adam_ema")
+        eng.refresh_weights()
+        return self.state
+
+    def loss(self):
+        return self.state[S_LOSS]
+
+    def ema_state_dict(self):
+        return {k: self.store.view(self.ema, k) for k in self.store.order}

@@ -1,0 +1,765 @@
+"""Explicit forward/backward schedule of the reference UNet family on the HIP kernels of libsdmi.so.
+
+Mirrors models/unet_cond_base.py:124-183 (cond) and models/unet_base.py:68-100 (uncond) with the
+blocks of models/blocks.py (DownBlock :27-146, MidBlock :149-267, UpBlockUnet :373-499), re-planned
+for MI355X:
+  * activations are NHWC bf16 2-D views [pixels, C] (row stride = ld), so every 1x1 conv and
+    attention projection is a plain GEMM and channel concatenation is free: a skip tensor is
+    produced straight into the upper half of its concat buffer;
+  * each conv is one implicit-GEMM launch (fwd / dgrad / wgrad), stride-2 transposed convs and
+    stride-2 conv gradients are four sub-pixel 2x2 GEMMs;
+  * epilogues fuse bias, the per-(batch, channel) time-embedding bias and residual adds;
+  * all t_emb_layers of the network are one GEMM (their weights and gradients are contiguous);
+  * GroupNorm(+SiLU) statistics/apply/backward and attention are the dedicated kernels;
+  * the backward pass is an explicit reverse schedule (a tape), gradients of activations flow in
+    place through residual paths, parameter gradients are written once into caller-owned fp32
+    views (a flat buffer in the trainer), so no autograd graph or aten kernel runs per op.
+Parameters are referenced by the reference's state-dict keys.
+"""
+import math
+
+import torch
+
+from . import _lib
+from . import kernels as K
+
+
+def _log2(v):
+    return v.bit_length() - 1
+
+
+def layout(cfg):
+    down = list(cfg["down_channels"])
+    mid = list(cfg["mid_channels"])
+    cond = cfg.get("condition_config") or {}
+    types = cond.get("condition_types", []) if cond else []
+    L = dict(text="text" in types, image="image" in types, klass="class" in types,
+             G=cfg["norm_channels"], heads=cfg["num_heads"], T=cfg["time_emb_dim"],
+             n_down=cfg["num_down_layers"], n_mid=cfg["num_mid_layers"], n_up=cfg["num_up_layers"],
+             conv_out=cfg["conv_out_channels"], down=down, mid=mid,
+             down_sample=list(cfg["down_sample"]), attn=list(cfg["attn_down"]))
+    if L["text"]:
+        L["ctx_dim"] = cond["text_condition_config"]["text_embed_dim"]
+    if L["image"]:
+        ic = cond["image_condition_config"]
+        L["im_in"] = ic["image_condition_input_channels"]
+        L["im_out"] = ic["image_condition_output_channels"]
+    if L["klass"]:
+        L["num_classes"] = cond["class_condition_config"]["num_classes"]
+    return L
+
+
+def resnet_list(L):
+    """(prefix, index, cin, cout) of every resnet in forward order (its t_emb_layers share one GEMM)."""
+    out = []
+    nd = len(L["down"]) - 1
+    for i in range(nd):
+        for l in range(L["n_down"]):
+            out.append((f"downs.{i}", l, L["down"][i] if l == 0 else L["down"][i + 1], L["down"][i + 1]))
+    for i in range(len(L["mid"]) - 1):
+        for l in range(L["n_mid"] + 1):
+            out.append((f"mids.{i}", l, L["mid"][i] if l == 0 else L["mid"][i + 1], L["mid"][i + 1]))
+    for j, i in enumerate(reversed(range(nd))):
+        cin = L["down"][i] * 2
+        cout = L["down"][i - 1] if i != 0 else L["conv_out"]
+        for l in range(L["n_up"]):
+            out.append((f"ups.{j}", l, cin if l == 0 else cout, cout))
+    return out
+
+
+class PackPlan:
+    """bf16 GEMM-layout copies of the fp32 weights, refreshed by one batched pack launch."""
+
+    def __init__(self, device):
+        self.device = device
+        self.items = []  # (name, src tensor, dims, shape of packed view)
+        self.total = 0
+        self.views = {}
+
+    def add(self, name, src, O, I, Ipad, KH, KW, so, si, skh, skw, kh_off=0, kh_mul=1, kw_off=0, kw_mul=1,
+            rows=None, into=None, row0=0):
+        """Pack dst[o][a][b][i] = src[o*so + i*si + (kh_off+kh_mul*a)*skh + (kw_off+kw_mul*b)*skw]."""
+        n = (rows or O) * KH * KW * Ipad
+        if into is None:
+            off = self.total
+            self.total += (n + 63) // 64 * 64
+            self.views[name] = (off, (rows or O), KH * KW * Ipad)
+            dst_off = off
+        else:
+            base, _, width = self.views[into]
+            dst_off = base + row0 * width
+        self.items.append(dict(src=src, dst_off=dst_off, O=O, I=I, Ipad=Ipad, KH=KH, KW=KW, so=so, si=si, skh=skh,
+                               skw=skw, kh_off=kh_off, kh_mul=kh_mul, kw_off=kw_off, kw_mul=kw_mul))
+
+    def reserve(self, name, rows, width):
+        off = self.total
+        self.total += (rows * width + 63) // 64 * 64
+        self.views[name] = (off, rows, width)
+
+    def finalize(self):
+        self.buf = torch.zeros(max(self.total, 64), dtype=torch.bfloat16, device=self.device)
+        chunk = _lib.lib().sdmi_pack_chunk()
+        descs = (_lib.PackDesc * len(self.items))()
+        bmap = []
+        for j, it in enumerate(self.items):
+            d = descs[j]
+            d.src = it["src"].data_ptr()
+            d.dst = self.buf.data_ptr() + 2 * it["dst_off"]
+            d.so, d.si, d.skh, d.skw = it["so"], it["si"], it["skh"], it["skw"]
+            for f in ("O", "I", "Ipad", "KH", "KW", "kh_off", "kh_mul", "kw_off", "kw_mul"):
+                setattr(d, f, it[f])
+            n = it["O"] * it["KH"] * it["KW"] * it["Ipad"]
+            bmap += [(j, c) for c in range((n + chunk - 1) // chunk)]
+        raw = bytes(descs)
+        self.desc_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        self.bmap_dev = torch.tensor(bmap, dtype=torch.int32).reshape(-1).to(self.device)
+        self.nblocks = len(bmap)
+        self.ptrs = [it["src"].data_ptr() for it in self.items]
+
+    def view(self, name):
+        off, rows, width = self.views[name]
+        return self.buf[off:off + rows * width].view(rows, width)
+
+    def run(self):
+        _lib.check(_lib.lib().sdmi_pack_weights(self.desc_dev.data_ptr(), self.bmap_dev.data_ptr(), self.nblocks,
+                                                K._stream()), "sdmi_pack_weights")
+
+    def stale(self):
+        return any(it["src"].data_ptr() != p for it, p in zip(self.items, self.ptrs))
+
+
+class Grads:
+    """Activation-gradient buffers; names that share storage (concat halves) share one buffer."""
+
+    def __init__(self, device):
+        self.device = device
+        self.groups = {}   # name -> (group key, column offset, C)
+        self.shapes = {}   # group key -> (rows, width)
+        self.bufs = {}
+        self.init = {}
+
+    def declare_group(self, key, rows, width, members):
+        self.shapes[key] = (rows, width)
+        self.members = getattr(self, "members", {})
+        self.members[key] = list(members)
+        for name, off, C in members:
+            self.groups[name] = (key, off, C)
+
+    def declare(self, name, rows, C):
+        self.declare_group(name, rows, C, [(name, 0, C)])
+
+    def get(self, name):
+        key, off, C = self.groups[name]
+        if key not in self.bufs:
+            rows, width = self.shapes[key]
+            self.bufs[key] = torch.empty(rows, width, dtype=torch.bfloat16, device=self.device)
+        fresh = not self.init.get(name, False)
+        self.init[name] = True
+        for other, o2, c2 in getattr(self, "members", {}).get(key, ()):  # a written range initialises what it covers
+            if off <= o2 and o2 + c2 <= off + C:
+                self.init[other] = True
+        return self.bufs[key][:, off:off + C], fresh
+
+    def alias(self, name, view):
+        """Let activation `name` use `view` (same shape, compact) as its gradient buffer."""
+        self.bufs[name] = view
+        self.groups[name] = (name, 0, view.shape[1])
+        self.init[name] = True
+
+
+class Tape(list):
+    """Reverse-mode schedule; every entry is tagged with the block label it belongs to."""
+    label = "input"
+
+    def append(self, item):
+        fn, c = item
+        c["label"] = self.label
+        super().append(item)
+
+
+class UNetEngine:
+    def __init__(self, cfg, params, grads=None, base=None, im_channels=4):
+        """params / grads: {state-dict key: fp32 CUDA tensor}; grads may be None (inference)."""
+        self.cfg = cfg
+        self.L = layout(cfg)
+        self.base = base or ("cond" if cfg.get("condition_config") else "uncond")
+        self.P = params
+        self.Gd = grads
+        self.im_channels = im_channels
+        self.device = next(iter(params.values())).device
+        L = self.L
+        if L["klass"]:
+            raise NotImplementedError("class conditioning is not wired into the HIP engine yet")
+        self.resnets = resnet_list(L)
+        self.temb_off = {}
+        off = 0
+        for (p, l, cin, cout) in self.resnets:
+            self.temb_off[(p, l)] = off
+            off += cout
+        self.temb_total = off
+        self._build_pack()
+
+    # ------------------------------------------------------------------------------------------
+    def _build_pack(self):
+        P, L = self.P, self.L
+        pk = PackPlan(self.device)
+
+        def conv(key, fwd=True, dgrad=True, ipad=None, opad=None):
+            w = P[key + ".weight"]
+            O, I, KH, KW = w.shape
+            Ip = ipad or I
+            if fwd:
+                pk.add(key + "#f", w, O, I, Ip, KH, KW, I * KH * KW, KH * KW, KW, 1, rows=opad)
+            if dgrad:  # stride-1 dgrad: [I][KH][KW][O] with flipped taps
+                pk.add(key + "#d", w, I, O, opad or O, KH, KW, KH * KW, I * KH * KW, KW, 1, KH - 1, -1, KW - 1, -1,
+                       rows=ipad)
+
+        def lin(key):
+            w = P[key + ".weight"] if key + ".weight" in P else P[key]
+            N, Kd = w.shape
+            pk.add(key + "#f", w, N, Kd, Kd, 1, 1, Kd, 1, 0, 0)
+
+        cin_img = self.im_channels + (L["im_out"] if L["image"] else 0)
+        self.cin_pad = (cin_img + 7) // 8 * 8
+        first = "conv_in_concat" if L["image"] else "conv_in"
+        self.first = first
+        conv(first, ipad=self.cin_pad)
+        lin("t_proj.0")
+        lin("t_proj.2")
+        # concatenated t_emb_layers weight [sum C][T]
+        pk.reserve("temb_all", self.temb_total, L["T"])
+        for (p, l, cin, cout) in self.resnets:
+            w = P[f"{p}.t_emb_layers.{l}.1.weight"]
+            pk.add(None, w, cout, L["T"], L["T"], 1, 1, L["T"], 1, 0, 0, into="temb_all", row0=self.temb_off[(p, l)])
+        for (p, l, cin, cout) in self.resnets:
+            conv(f"{p}.resnet_conv_first.{l}.2")
+            conv(f"{p}.resnet_conv_second.{l}.2")
+            conv(f"{p}.residual_input_conv.{l}", dgrad=False)
+        nd = len(L["down"]) - 1
+        for i in range(nd):
+            p = f"downs.{i}"
+            for l in range(L["n_down"]):
+                if L["attn"][i]:
+                    lin(f"{p}.attentions.{l}.in_proj_weight")
+                    lin(f"{p}.attentions.{l}.out_proj")
+                if L["text"]:
+                    lin(f"{p}.cross_attentions.{l}.in_proj_weight")
+                    lin(f"{p}.cross_attentions.{l}.out_proj")
+                    lin(f"{p}.context_proj.{l}")
+            if L["down_sample"][i]:
+                key = f"{p}.down_sample_conv"
+                w = P[key + ".weight"]
+                C = w.shape[0]
+                conv(key, dgrad=False)
+                for ph in range(2):
+                    for pw in range(2):  # dgrad phases: [ci][a][b][co] = W[co][ci][3-ph-2a][3-pw-2b]
+                        pk.add(f"{key}#d{ph}{pw}", w, C, C, C, 2, 2, 16, C * 16, 4, 1, 3 - ph, -2, 3 - pw, -2)
+        for i in range(len(L["mid"]) - 1):
+            p = f"mids.{i}"
+            for l in range(L["n_mid"]):
+                lin(f"{p}.attentions.{l}.in_proj_weight")
+                lin(f"{p}.attentions.{l}.out_proj")
+                if L["text"]:
+                    lin(f"{p}.cross_attentions.{l}.in_proj_weight")
+                    lin(f"{p}.cross_attentions.{l}.out_proj")
+                    lin(f"{p}.context_proj.{l}")
+        for j, i in enumerate(reversed(range(nd))):
+            p = f"ups.{j}"
+            for l in range(L["n_up"]):
+                lin(f"{p}.attentions.{l}.in_proj_weight")
+                lin(f"{p}.attentions.{l}.out_proj")
+                if L["text"]:
+                    lin(f"{p}.cross_attentions.{l}.in_proj_weight")
+                    lin(f"{p}.cross_attentions.{l}.out_proj")
+                    lin(f"{p}.context_proj.{l}")
+            if L["down_sample"][i]:
+                key = f"{p}.up_sample_conv"
+                w = P[key + ".weight"]  # (Cx, Cy, 4, 4)
+                Cx, Cy = w.shape[0], w.shape[1]
+                for ph in range(2):
+                    for pw in range(2):  # fwd phases: [co][a][b][ci] = W[ci][co][3-ph-2a][3-pw-2b]
+                        pk.add(f"{key}#f{ph}{pw}", w, Cy, Cx, Cx, 2, 2, 16, Cy * 16, 4, 1, 3 - ph, -2, 3 - pw, -2)
+                # dgrad = stride-2 conv over dY: [ci][kh][kw][co] = W[ci][co][kh][kw]
+                pk.add(f"{key}#d", w, Cx, Cy, Cy, 4, 4, Cy * 16, 16, 4, 1)
+        conv("conv_out", ipad=None, opad=8)
+        pk.finalize()
+        self.pack = pk
+
+    def W(self, name):
+        return self.pack.view(name)
+
+    def refresh_weights(self):
+        if self.pack.stale():
+            self.pack.finalize()
+        self.pack.run()
+
+    # ------------------------------------------------------------------------------------------
+    def _new(self, rows, C, dtype=torch.bfloat16):
+        return torch.empty(rows, C, dtype=dtype, device=self.device)
+
+    def g(self, key):
+        return self.Gd[key] if self.Gd is not None else None
+
+    def forward(self, x, t, text=None, mask=None, need_backward=True, mask_keep=None):
+        """x: (B, C, H, W) fp32; t: int64 (B,), (1,) or 0-d; text: (B, S, ctx) ; mask: (B, cmi, MH, MW) fp32.
+        Returns (pred NHWC fp32 [B*H*W, 8] with the first im_channels valid, tape)."""
+        L, P = self.L, self.P
+        B, Cx, H, W = x.shape
+        assert Cx == self.im_channels
+        dev = self.device
+        G, Hh = L["G"], L["heads"]
+        tape = Tape()
+        st = dict(B=B, H=H, W=W)
+        grads = Grads(dev)
+        self._grads = grads
+        x = x.float().contiguous()
+        # ---- resolutions and concat buffers ----
+        nd = len(L["down"]) - 1
+        res = [(H, W)]
+        for i in range(nd):
+            h, w = res[-1]
+            res.append((h // 2, w // 2) if L["down_sample"][i] else (h, w))
+        cats = []
+        for i in range(nd):
+            h, w = res[i]
+            C = L["down"][i]
+            buf = self._new(B * h * w, 2 * C)
+            cats.append(buf)
+            grads.declare_group(f"cat{i}", B * h * w, 2 * C, [(f"up{i}", 0, C), (f"skip{i}", C, C), (f"cat{i}", 0, 2 * C)])
+
+        # ---- input staging + first conv (unet_cond_base.py:131-140) ----
+        xin = self._new(B * H * W, self.cin_pad)
+        if L["image"]:
+            m = mask.float().contiguous()
+            _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, m.data_ptr(), L["im_in"], m.shape[2],
+                                                  m.shape[3], P["cond_conv_in.weight"].data_ptr(), L["im_out"],
+                                                  xin.data_ptr(), self.cin_pad, K._p(mask_keep), K._stream()),
+                       "sdmi_prep_input")
+        else:
+            m = None
+            _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, None, 0, 1, 1, None, 0, xin.data_ptr(),
+                                                  self.cin_pad, None, K._stream()), "sdmi_prep_input")
+        skip0 = cats[0][:, L["down"][0]:]
+        K.conv_fwd(xin, B, H, W, self.cin_pad, self.cin_pad, self.W(self.first + "#f"), L["down"][0], 3, 3, 1, 1,
+                   skip0, K.ld_of(skip0), bias=P[self.first + ".bias"])
+        tape.append((self._bwd_input, dict(xin=xin, mask=m, keep=mask_keep, B=B, H=H, W=W)))
+
+        # ---- time embedding (blocks.py:5-24, unet_cond_base.py:148-149) ----
+        tape.label = "time"
+        T = L["T"]
+        t = torch.as_tensor(t, device=dev).long().reshape(-1)
+        if t.numel() not in (1, B):
+            raise ValueError("t must have 1 or B elements")
+        e = self._new(B, T)
+        _lib.check(_lib.lib().sdmi_time_embedding(t.data_ptr(), 0 if t.numel() == 1 else 1, B, T, e.data_ptr(), T,
+                                                  None, K._stream()), "sdmi_time_embedding")
+        h1 = self._new(B, T)
+        K.linear(e, self.W("t_proj.0#f"), h1, bias=P["t_proj.0.bias"])
+        s1 = self._new(B, T)
+        _lib.check(_lib.lib().sdmi_silu(h1.data_ptr(), None, s1.data_ptr(), B * T, K._stream()), "sdmi_silu")
+        temb = self._new(B, T)
+        K.linear(s1, self.W("t_proj.2#f"), temb, bias=P["t_proj.2.bias"])
+        stemb = self._new(B, T)
+        _lib.check(_lib.lib().sdmi_silu(temb.data_ptr(), None, stemb.data_ptr(), B * T, K._stream()), "sdmi_silu")
+        temb_all = self._new(B, self.temb_total)
+        # biases of all t_emb_layers: gathered once per call into a contiguous fp32 vector
+        bias_all = self._temb_bias()
+        K.linear(stemb, self.W("temb_all"), temb_all, bias=bias_all)
+        self.dtemb_all = None
+        tape.append((self._bwd_time, dict(e=e, h1=h1, s1=s1, temb=temb, stemb=stemb, B=B)))
+        st["temb_all"] = temb_all
+
+        ctx = None
+        if L["text"]:
+            txt = text.float().contiguous()
+            S = txt.shape[1]
+            ctx = self._new(B * S, txt.shape[2])
+            _lib.check(_lib.lib().sdmi_nchw_to_nhwc_bf16(txt.data_ptr(), B * S, txt.shape[2], 1, ctx.data_ptr(),
+                                                         txt.shape[2], K._stream()), "cast")
+            st["S"] = S
+        st["ctx"] = ctx
+
+        # ---- down blocks (blocks.py:111-146) ----
+        cur, cur_name = skip0, "skip0"
+        for i in range(nd):
+            p = f"downs.{i}"
+            tape.label = p
+            h, w = res[i]
+            cin, cout = L["down"][i], L["down"][i + 1]
+            ops = []
+            for l in range(L["n_down"]):
+                ops.append(("res", l, cin if l == 0 else cout))
+                if L["attn"][i]:
+                    ops.append(("self", l, cout))
+                if L["text"]:
+                    ops.append(("cross", l, cout))
+            if L["down_sample"][i]:
+                ops.append(("down", 0, cout))
+            # where the block's output goes: the next concat's skip half, or a fresh buffer for the mids
+            dst_name = f"skip{i + 1}" if i + 1 < nd else "mid_in"
+            for k, (kind, l, c) in enumerate(ops):
+                last = k == len(ops) - 1
+                out = None
+                oname = f"{p}.{kind}{l}"
+                if last:
+                    if i + 1 < nd:
+                        out = cats[i + 1][:, L["down"][i + 1]:]
+                    oname = dst_name
+                cur, cur_name = self._op(kind, p, l, c, cout, cur, cur_name, out, oname, B, h, w, st, tape, grads)
+
+        # ---- mid blocks (blocks.py:225-267) ----
+        h, w = res[-1]
+        for i in range(len(L["mid"]) - 1):
+            p = f"mids.{i}"
+            tape.label = p
+            cin, cout = L["mid"][i], L["mid"][i + 1]
+            cur, cur_name = self._op("res", p, 0, cin, cout, cur, cur_name, None, f"{p}.res0", B, h, w, st, tape, grads)
+            for l in range(L["n_mid"]):
+                cur, cur_name = self._op("self", p, l, cout, cout, cur, cur_name, None, f"{p}.self{l}", B, h, w, st,
+                                         tape, grads)
+                if L["text"]:
+                    cur, cur_name = self._op("cross", p, l, cout, cout, cur, cur_name, None, f"{p}.cross{l}", B, h, w,
+                                             st, tape, grads)
+                cur, cur_name = self._op("res", p, l + 1, cout, cout, cur, cur_name, None, f"{p}.res{l + 1}", B, h,
+                                         w, st, tape, grads)
+
+        # ---- up blocks (blocks.py:461-499) ----
+        for j, i in enumerate(reversed(range(nd))):
+            p = f"ups.{j}"
+            tape.label = p
+            h, w = res[i]
+            C = L["down"][i]
+            up_view = cats[i][:, :C]
+            if L["down_sample"][i]:
+                self._op("up", p, 0, C, C, cur, cur_name, up_view, f"up{i}", B, res[i + 1][0], res[i + 1][1], st,
+                         tape, grads)
+            else:
+                K.copy_slice(cur, up_view)
+                tape.append((self._bwd_copy, dict(src=cur_name, dst=f"up{i}")))
+            cur, cur_name = cats[i], f"cat{i}"
+            cin = 2 * C
+            cout = L["down"][i - 1] if i != 0 else L["conv_out"]
+            for l in range(L["n_up"]):
+                cur, cur_name = self._op("res", p, l, cin if l == 0 else cout, cout, cur, cur_name, None, f"{p}.res{l}",
+                                         B, h, w, st, tape, grads)
+                cur, cur_name = self._op("self", p, l, cout, cout, cur, cur_name, None, f"{p}.self{l}", B, h, w, st,
+                                         tape, grads)
+                if L["text"]:
+                    cur, cur_name = self._op("cross", p, l, cout, cout, cur, cur_name, None, f"{p}.cross{l}", B, h, w,
+                                             st, tape, grads)
+
+        # ---- head (unet_cond_base.py:179-181) ----
+        tape.label = "head"
+        C = L["conv_out"]
+        Pn = H * W
+        mean, rstd = K.gn_stats(cur, B, Pn, C, G)
+        hs = self._new(B * Pn, C)
+        K.gn_apply(cur, mean, rstd, P["norm_out.weight"], P["norm_out.bias"], B, Pn, C, G, True, hs)
+        pred = self._new(B * Pn, 8, torch.float32)
+        K.conv_fwd(hs, B, H, W, C, C, self.W("conv_out#f"), 8, 3, 3, 1, 1, pred, 8, bias=P["conv_out.bias"],
+                   n_store=self.im_channels)
+        tape.append((self._bwd_head, dict(x=cur, xn=cur_name, mean=mean, rstd=rstd, hs=hs, B=B, H=H, W=W)))
+        return pred, dict(tape=tape, st=st, grads=grads) if need_backward else None
+
+    # ------------------------------------------------------------------------------------------
+    def _temb_bias(self):
+        """The t_emb_layers biases are one contiguous fp32 vector of the flat store (forward order)."""
+        return contiguous_run(self.P, [f"{p}.t_emb_layers.{l}.1.bias" for (p, l, ci, co) in self.resnets],
+                              (self.temb_total,))
+
+    def _op(self, kind, p, l, cin, cout, x, xname, out, oname, B, h, w, st, tape, grads):
+        if kind == "res":
+            y = self._resnet_fwd(p, l, cin, cout, x, xname, out, oname, B, h, w, st, tape)
+        elif kind == "self":
+            y = self._attn_fwd(p, l, cout, x, xname, out, oname, B, h, w, st, tape, cross=False)
+        elif kind == "cross":
+            y = self._attn_fwd(p, l, cout, x, xname, out, oname, B, h, w, st, tape, cross=True)
+        elif kind == "down":
+            y = self._down_fwd(p, cout, x, xname, out, oname, B, h, w, tape)
+        elif kind == "up":
+            y = self._up_fwd(p, cin, x, xname, out, oname, B, h, w, tape)
+        else:
+            raise ValueError(kind)
+        if oname not in grads.groups:
+            grads.declare(oname, y.shape[0], y.shape[1])
+        return y, oname
+
+    # ---- resnet ----------------------------------------------------------------------------------
+    def _resnet_fwd(self, p, l, cin, cout, x, xname, out, oname, B, h, w, st, tape):
+        P, G = self.P, self.L["G"]
+        Pn = h * w
+        a, b = f"{p}.resnet_conv_first.{l}", f"{p}.resnet_conv_second.{l}"
+        m1, r1 = K.gn_stats(x, B, Pn, cin, G)
+        h0 = self._new(B * Pn, cin)
+        K.gn_apply(x, m1, r1, P[a + ".0.weight"], P[a + ".0.bias"], B, Pn, cin, G, True, h0)
+        h1 = self._new(B * Pn, cout)
+        off = self.temb_off[(p, l)]
+        K.conv_fwd(h0, B, h, w, cin, cin, self.W(a + ".2#f"), cout, 3, 3, 1, 1, h1, cout, bias=P[a + ".2.bias"],
+                   rowbias=st["temb_all"][:, off:], rb_ld=self.temb_total)
+        m2, r2 = K.gn_stats(h1, B, Pn, cout, G)
+        h2 = self._new(B * Pn, cout)
+        K.gn_apply(h1, m2, r2, P[b + ".0.weight"], P[b + ".0.bias"], B, Pn, cout, G, True, h2)
+        rc = f"{p}.residual_input_conv.{l}"
+        r = self._new(B * Pn, cout)
+        K.linear(x, self.W(rc + "#f"), r, bias=P[rc + ".bias"])
+        y = out if out is not None else self._new(B * Pn, cout)
+        K.conv_fwd(h2, B, h, w, cout, cout, self.W(b + ".2#f"), cout, 3, 3, 1, 1, y, K.ld_of(y), bias=P[b + ".2.bias"],
+                   resid=r, ldr=cout)
+        tape.append((self._resnet_bwd, dict(p=p, l=l, cin=cin, cout=cout, x=x, xn=xname, yn=oname, h0=h0, h1=h1, h2=h2,
+                                            m1=m1, r1=r1, m2=m2, r2=r2, B=B, h=h, w=w)))
+        return y
+
+    def _resnet_bwd(self, c, grads):
+        P, G = self.P, self.L["G"]
+        p, l, cin, cout, B, h, w = c["p"], c["l"], c["cin"], c["cout"], c["B"], c["h"], c["w"]
+        Pn = h * w
+        a, b = f"{p}.resnet_conv_first.{l}", f"{p}.resnet_conv_second.{l}"
+        rc = f"{p}.residual_input_conv.{l}"
+        dy, _ = grads.get(c["yn"])
+        ldy = K.ld_of(dy)
+        K.conv_wgrad(dy, ldy, c["h2"], B, h, w, cout, cout, cout, 3, 3, 1, 1, self.g(b + ".2.weight"), h, w)
+        K.chan_sum(dy, B, Pn, cout, per_c=self.g(b + ".2.bias"), per_c2=self.g(rc + ".bias"))
+        dh2 = self._new(B * Pn, cout)
+        K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout)
+        K.linear_wgrad(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
+        dx, fresh = grads.get(c["xn"])
+        K.linear_dgrad(dy, self.W(rc + "#f"), dx, resid=None if fresh else dx)
+        K.gn_bwd(c["h1"], dh2, dh2, c["m2"], c["r2"], P[b + ".0.weight"], P[b + ".0.bias"], B, Pn, cout, G, True,
+                 self.g(b + ".0.weight"), self.g(b + ".0.bias"))
+        off = self.temb_off[(p, l)]
+        K.chan_sum(dh2, B, Pn, cout, per_bc=self.dtemb_all[:, off:off + cout], per_c=self.g(a + ".2.bias"),
+                   per_c2=self.g(f"{p}.t_emb_layers.{l}.1.bias"))
+        K.conv_wgrad(dh2, cout, c["h0"], B, h, w, cin, cin, cout, 3, 3, 1, 1, self.g(a + ".2.weight"), h, w)
+        dh0 = self._new(B * Pn, cin)
+        K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin)
+        K.gn_bwd(c["x"], dh0, dx, c["m1"], c["r1"], P[a + ".0.weight"], P[a + ".0.bias"], B, Pn, cin, G, True,
+                 self.g(a + ".0.weight"), self.g(a + ".0.bias"), addend=dx)
+
+    # ---- self / cross attention --------------------------------------------------------------------
+    def _attn_fwd(self, p, l, C, x, xname, out, oname, B, h, w, st, tape, cross):
+        P, G, Hh = self.P, self.L["G"], self.L["heads"]
+        N = h * w
+        nk = f"{p}.cross_attention_norms.{l}" if cross else f"{p}.attention_norms.{l}"
+        mk = f"{p}.cross_attentions.{l}" if cross else f"{p}.attentions.{l}"
+        mean, rstd = K.gn_stats(x, B, N, C, G)
+        a = self._new(B * N, C)
+        K.gn_apply(x, mean, rstd, P[nk + ".weight"], P[nk + ".bias"], B, N, C, G, False, a)
+        Win = self.W(mk + ".in_proj_weight#f")
+        bin_ = P[mk + ".in_proj_bias"]
+        d = C // Hh
+        o = self._new(B * N, C)
+        c = dict(p=p, l=l, C=C, x=x, xn=xname, yn=oname, a=a, mean=mean, rstd=rstd, o=o, B=B, N=N, cross=cross, nk=nk,
+                 mk=mk)
+        if not cross:
+            qkv = self._new(B * N, 3 * C)
+            K.linear(a, Win, qkv, bias=bin_)
+            c["lse"] = K.attn_fwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], o, B, Hh, N, N, d)
+            c["qkv"] = qkv
+        else:
+            S = st["S"]
+            ctx = st["ctx"]
+            ck = f"{p}.context_proj.{l}"
+            q = self._new(B * N, C)
+            K.linear(a, Win[:C], q, bias=bin_[:C])
+            cp = self._new(B * S, C)
+            K.linear(ctx, self.W(ck + "#f"), cp, bias=P[ck + ".bias"])
+            kv = self._new(B * S, 2 * C)
+            K.linear(cp, Win[C:], kv, bias=bin_[C:])
+            c["lse"] = K.attn_fwd(q, kv[:, :C], kv[:, C:], o, B, Hh, N, S, d)
+            c.update(q=q, cp=cp, kv=kv, S=S, ctx=ctx, ck=ck)
+        y = out if out is not None else self._new(B * N, C)
+        K.linear(o, self.W(mk + ".out_proj#f"), y, bias=P[mk + ".out_proj.bias"], resid=x)
+        tape.append((self._attn_bwd, c))
+        return y
+
+    def _attn_bwd(self, c, grads):
+        P, G, Hh = self.P, self.L["G"], self.L["heads"]
+        C, B, N, mk, nk = c["C"], c["B"], c["N"], c["mk"], c["nk"]
+        d = C // Hh
+        dy, _ = grads.get(c["yn"])
+        K.linear_wgrad(dy, c["o"], self.g(mk + ".out_proj.weight"))
+        K.chan_sum(dy, 1, B * N, C, per_c=self.g(mk + ".out_proj.bias"))
+        do = self._new(B * N, C)
+        K.linear_dgrad(dy, self.W(mk + ".out_proj#f"), do)
+        Win = self.W(mk + ".in_proj_weight#f")
+        gW = self.g(mk + ".in_proj_weight")
+        gb = self.g(mk + ".in_proj_bias")
+        da = self._new(B * N, C)
+        if not c["cross"]:
+            qkv = c["qkv"]
+            dqkv = self._new(B * N, 3 * C)
+            K.attn_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], c["o"], do, c["lse"], dqkv[:, :C],
+                       dqkv[:, C:2 * C], dqkv[:, 2 * C:], B, Hh, N, N, d)
+            K.linear_wgrad(dqkv, c["a"], gW)
+            K.chan_sum(dqkv, 1, B * N, 3 * C, per_c=gb)
+            K.linear_dgrad(dqkv, Win, da)
+        else:
+            S, kv = c["S"], c["kv"]
+            dq = self._new(B * N, C)
+            dkv = self._new(B * S, 2 * C)
+            K.attn_bwd(c["q"], kv[:, :C], kv[:, C:], c["o"], do, c["lse"], dq, dkv[:, :C], dkv[:, C:], B, Hh, N, S, d)
+            K.linear_wgrad(dq, c["a"], gW[:C])
+            K.chan_sum(dq, 1, B * N, C, per_c=gb[:C])
+            K.linear_wgrad(dkv, c["cp"], gW[C:])
+            K.chan_sum(dkv, 1, B * S, 2 * C, per_c=gb[C:])
+            dcp = self._new(B * S, C)
+            K.linear_dgrad(dkv, Win[C:], dcp)
+            K.linear_wgrad(dcp, c["ctx"], self.g(c["ck"] + ".weight"))
+            K.chan_sum(dcp, 1, B * S, C, per_c=self.g(c["ck"] + ".bias"))
+            K.linear_dgrad(dq, Win[:C], da)
+        # x receives dy (residual) + GroupNorm-branch gradient
+        key, off, _ = grads.groups[c["xn"]]
+        if not grads.init.get(c["xn"], False) and dy.is_contiguous() and K.ld_of(dy) == C and \
+                grads.shapes.get(key, (0, 0))[1] == C:
+            grads.alias(c["xn"], dy)
+            dx, addend = dy, dy
+        else:
+            dx, fresh = grads.get(c["xn"])
+            if not fresh:
+                K.copy_slice(dy, dx, accumulate=True)
+                addend = dx
+            else:
+                addend = dy
+        K.gn_bwd(c["x"], da, dx, c["mean"], c["rstd"], P[nk + ".weight"], P[nk + ".bias"], B, N, C, G, False,
+                 self.g(nk + ".weight"), self.g(nk + ".bias"), addend=addend)
+
+    # ---- down / up sampling convs --------------------------------------------------------------------
+    def _down_fwd(self, p, C, x, xname, out, oname, B, h, w, tape):
+        key = f"{p}.down_sample_conv"
+        y = out if out is not None else self._new(B * (h // 2) * (w // 2), C)
+        K.conv_fwd(x, B, h, w, C, K.ld_of(x), self.W(key + "#f"), C, 4, 4, 2, 1, y, K.ld_of(y),
+                   bias=self.P[key + ".bias"])
+        tape.append((self._down_bwd, dict(key=key, C=C, x=x, xn=xname, yn=oname, B=B, h=h, w=w)))
+        return y
+
+    def _down_bwd(self, c, grads):
+        key, C, B, h, w = c["key"], c["C"], c["B"], c["h"], c["w"]
+        dy, _ = grads.get(c["yn"])
+        ldy = K.ld_of(dy)
+        K.conv_wgrad(dy, ldy, c["x"], B, h, w, C, K.ld_of(c["x"]), C, 4, 4, 2, 1, self.g(key + ".weight"), h // 2,
+                     w // 2)
+        K.chan_sum(dy, B, (h // 2) * (w // 2), C, per_c=self.g(key + ".bias"))
+        dx, fresh = grads.get(c["xn"])
+        wph = [self.W(f"{key}#d{ph}{pw}") for ph in range(2) for pw in range(2)]
+        K.conv_dgrad_phases(dy, B, h, w, C, ldy, wph, C, dx, K.ld_of(dx), resid=None if fresh else dx,
+                            ldr=K.ld_of(dx))
+
+    def _up_fwd(self, p, C, x, xname, out, oname, B, h, w, tape):
+        key = f"{p}.up_sample_conv"
+        wph = [self.W(f"{key}#f{ph}{pw}") for ph in range(2) for pw in range(2)]
+        K.convT_fwd_phases(x, B, h, w, C, K.ld_of(x), wph, C, out, K.ld_of(out), bias=self.P[key + ".bias"])
+        tape.append((self._up_bwd, dict(key=key, C=C, x=x, xn=xname, yn=oname, B=B, h=h, w=w)))
+        return out
+
+    def _up_bwd(self, c, grads):
+        key, C, B, h, w = c["key"], c["C"], c["B"], c["h"], c["w"]
+        dy, _ = grads.get(c["yn"])  # (B, 2h, 2w, C) slice of the concat gradient
+        ldy = K.ld_of(dy)
+        x = c["x"]
+        K.chan_sum(dy, B, 4 * h * w, C, per_c=self.g(key + ".bias"))
+        # dW[ci][co][kh][kw] = sum_{pixels of x} x[p][ci] * dy[2*iy-1+kh, 2*ix-1+kw][co]
+        g = K.conv_geom(2 * h, 2 * w, C, ldy, 4, 4, h, w, 2, 2, -1, -1)
+        K.gemm(C, 16 * C, B * h * w, x, _lib.A_COLMAJOR, K.ld_of(x), dy, _lib.B_KN_CONV, 0, self.g(key + ".weight"),
+               16 * C, geom=g, perm=(C, 16))
+        dx, fresh = grads.get(c["xn"])
+        K.conv_fwd(dy, B, 2 * h, 2 * w, C, ldy, self.W(key + "#d"), C, 4, 4, 2, 1, dx, K.ld_of(dx),
+                   resid=None if fresh else dx, ldr=K.ld_of(dx))
+
+    def _bwd_copy(self, c, grads):
+        dy, _ = grads.get(c["dst"])
+        dx, fresh = grads.get(c["src"])
+        K.copy_slice(dy, dx, accumulate=not fresh)
+
+    # ---- head / input / time embedding backward ------------------------------------------------------
+    def _bwd_head(self, c, grads):
+        P, G = self.P, self.L["G"]
+        B, H, W = c["B"], c["H"], c["W"]
+        C = self.L["conv_out"]
+        Pn = H * W
+        dpred = self.dpred
+        K.conv_wgrad(dpred, 8, c["hs"], B, H, W, C, C, 8, 3, 3, 1, 1, self.g("conv_out.weight"), H, W,
+                     m_store=self.im_channels)
+        K.chan_sum(dpred, B, Pn, 8, per_c=self.g("conv_out.bias"), c_store=self.im_channels)
+        dhs = self._new(B * Pn, C)
+        K.conv_fwd(dpred, B, H, W, 8, 8, self.W("conv_out#d"), C, 3, 3, 1, 1, dhs, C)
+        dx, fresh = grads.get(c["xn"])
+        K.gn_bwd(c["x"], dhs, dx, c["mean"], c["rstd"], P["norm_out.weight"], P["norm_out.bias"], B, Pn, C, G, True,
+                 self.g("norm_out.weight"), self.g("norm_out.bias"), addend=None if fresh else dx)
+
+    def _bwd_input(self, c, grads):
+        L = self.L
+        B, H, W = c["B"], c["H"], c["W"]
+        dy, _ = grads.get("skip0")
+        ldy = K.ld_of(dy)
+        C0 = L["down"][0]
+        cin_real = self.im_channels + (L["im_out"] if L["image"] else 0)
+        K.conv_wgrad(dy, ldy, c["xin"], B, H, W, self.cin_pad, self.cin_pad, C0, 3, 3, 1, 1,
+                     self.g(self.first + ".weight"), H, W, cvalid=cin_real)
+        K.chan_sum(dy, B, H * W, C0, per_c=self.g(self.first + ".bias"))
+        if L["image"]:
+            dxin = self._new(B * H * W, self.cin_pad)
+            K.conv_fwd(dy, B, H, W, C0, ldy, self.W(self.first + "#d"), self.cin_pad, 3, 3, 1, 1, dxin, self.cin_pad)
+            m = c["mask"]
+            _lib.check(_lib.lib().sdmi_cond_wgrad(dxin.data_ptr(), self.cin_pad, self.im_channels, B, H, W,
+                                                  m.data_ptr(), L["im_in"], m.shape[2], m.shape[3], L["im_out"],
+                                                  self.g("cond_conv_in.weight").data_ptr(), K._p(c["keep"]),
+                                                  K._stream()),
+                       "sdmi_cond_wgrad")
+
+    def _bwd_time(self, c, grads):
+        P, L = self.P, self.L
+        B, T = c["B"], L["T"]
+        d_all = self.dtemb_all
+        # t_emb_layers weights are contiguous in the gradient store: one GEMM for all of them
+        K.linear_wgrad(d_all, c["stemb"], self.temb_grad_all)
+        dst = self._new(B, T)
+        K.linear_dgrad(d_all, self.W("temb_all"), dst)
+        dtemb = self._new(B, T)
+        lib = _lib.lib()
+        _lib.check(lib.sdmi_silu(c["temb"].data_ptr(), dst.data_ptr(), dtemb.data_ptr(), B * T, K._stream()), "silu")
+        K.linear_wgrad(dtemb, c["s1"], self.g("t_proj.2.weight"))
+        K.chan_sum(dtemb, 1, B, T, per_c=self.g("t_proj.2.bias"))
+        ds1 = self._new(B, T)
+        K.linear_dgrad(dtemb, self.W("t_proj.2#f"), ds1)
+        dh1 = self._new(B, T)
+        _lib.check(lib.sdmi_silu(c["h1"].data_ptr(), ds1.data_ptr(), dh1.data_ptr(), B * T, K._stream()), "silu")
+        K.linear_wgrad(dh1, c["e"], self.g("t_proj.0.weight"))
+        K.chan_sum(dh1, 1, B, T, per_c=self.g("t_proj.0.bias"))
+
+    # ------------------------------------------------------------------------------------------
+    def backward(self, ctx, dpred, grads=None, on_progress=None):
+        """dpred: NHWC bf16 [B*H*W, 8] (zero in padded channels). Writes every parameter gradient into
+        `grads` ({key: fp32 view}, default: the engine's own) -- each is fully overwritten."""
+        if grads is not None:
+            self.Gd = grads
+        assert self.Gd is not None, "engine built without gradient buffers"
+        st = ctx["st"]
+        B = st["B"]
+        self.dpred = dpred
+        self.dtemb_all = self._new(B, self.temb_total)
+        self.temb_grad_all = self._temb_grad_view()
+        grads = ctx["grads"]
+        tape = ctx["tape"]
+        for k in range(len(tape) - 1, -1, -1):
+            fn, c = tape[k]
+            fn(c, grads)
+            if on_progress is not None:
+                on_progress(tape, k)
+        self.dpred = None
+
+    def _temb_grad_view(self):
+        """The t_emb_layers weight gradients are one contiguous [sum C][T] region of the flat store."""
+        return contiguous_run(self.Gd, [f"{p}.t_emb_layers.{l}.1.weight" for (p, l, ci, co) in self.resnets],
+                              (self.temb_total, self.L["T"]))
+
+
+def contiguous_run(tensors, keys, shape):
+    """View over tensors[keys[0]] .. tensors[keys[-1]] that must lie back to back in memory."""
+    first = tensors[keys[0]]
+    pos = first.data_ptr()
+    for k in keys:
+        t = tensors[k]
+        if t.data_ptr() != pos or not t.is_contiguous():
+            raise RuntimeError(f"{k} is not contiguous with the previous tensors of its run (use sdmi.store.FlatStore)")
+        pos += t.numel() * t.element_size()
+    return first.as_strided(shape, torch.empty(shape, device="meta").stride())

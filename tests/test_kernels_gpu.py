@@ -1,0 +1,108 @@
+"""GPU numerics of the GroupNorm, attention and small fused kernels against torch fp32 references
+of the same ops on bf16-rounded inputs.  Tolerances: bf16 output rounding (~4e-3 relative) plus
+fp32 reduction-order differences."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def K():
+    from sdmi import kernels
+    return kernels
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+def relerr(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("B,H,C,G,silu", [(2, 8, 64, 32, True), (3, 16, 384, 32, True), (2, 4, 768, 32, False),
+                                          (1, 32, 96, 32, True)])
+def test_groupnorm_fwd_bwd(B, H, C, G, silu):
+    k = K()
+    torch.manual_seed(0)
+    P = H * H
+    x = bf(torch.randn(B, P, C, device="cuda") * 2 + 0.5)
+    gamma = torch.randn(C, device="cuda") * 0.1 + 1
+    beta = torch.randn(C, device="cuda") * 0.1
+    dy = bf(torch.randn(B, P, C, device="cuda"))
+    xr = x.float().permute(0, 2, 1).clone().requires_grad_(True)  # (B, C, P)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    yr = F.group_norm(xr, G, gr, br, eps=1e-5)
+    if silu:
+        yr = F.silu(yr)
+    yr.backward(dy.float().permute(0, 2, 1))
+    x2 = x.view(B * P, C)
+    mean, rstd = k.gn_stats(x2, B, P, C, G)
+    y = torch.empty_like(x2)
+    k.gn_apply(x2, mean, rstd, gamma, beta, B, P, C, G, silu, y)
+    assert relerr(y.view(B, P, C).permute(0, 2, 1), yr.detach()) < 1e-2
+    dx = torch.empty_like(x2)
+    dg = torch.empty(C, device="cuda")
+    db = torch.empty(C, device="cuda")
+    k.gn_bwd(x2, dy.view(B * P, C), dx, mean, rstd, gamma, beta, B, P, C, G, silu, dg, db)
+    assert relerr(dx.view(B, P, C).permute(0, 2, 1), xr.grad) < 2e-2
+    assert relerr(dg, gr.grad) < 1e-2
+    assert relerr(db, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("B,Hh,N,S,d", [(2, 16, 64, 64, 8), (2, 16, 256, 256, 24), (1, 16, 16, 77, 32),
+                                        (2, 4, 1024, 1024, 16), (2, 16, 64, 77, 48), (1, 8, 100, 100, 64)])
+def test_attention_fwd_bwd(B, Hh, N, S, d):
+    k = K()
+    torch.manual_seed(1)
+    C = Hh * d
+    q = bf(torch.randn(B * N, C, device="cuda"))
+    kk = bf(torch.randn(B * S, C, device="cuda"))
+    v = bf(torch.randn(B * S, C, device="cuda"))
+    do = bf(torch.randn(B * N, C, device="cuda"))
+
+    def heads(t, L):
+        return t.float().view(B, L, Hh, d).transpose(1, 2)
+
+    qr, kr, vr = (heads(q, N).requires_grad_(True), heads(kk, S).requires_grad_(True),
+                  heads(v, S).requires_grad_(True))
+    att = torch.softmax(qr @ kr.transpose(-1, -2) / math.sqrt(d), -1)
+    orf = att @ vr
+    orf.backward(heads(do, N))
+    o = torch.empty(B * N, C, device="cuda", dtype=torch.bfloat16)
+    lse = k.attn_fwd(q, kk, v, o, B, Hh, N, S, d)
+    assert relerr(heads(o, N), orf.detach()) < 2e-2
+    dq = torch.empty_like(q)
+    dk = torch.empty_like(kk)
+    dv = torch.empty_like(v)
+    k.attn_bwd(q, kk, v, o, do, lse, dq, dk, dv, B, Hh, N, S, d)
+    assert relerr(heads(dq, N), qr.grad) < 3e-2
+    assert relerr(heads(dk, S), kr.grad) < 3e-2
+    assert relerr(heads(dv, S), vr.grad) < 3e-2
+
+
+def test_chan_sum_and_mse():
+    k = K()
+    torch.manual_seed(2)
+    B, P, C = 4, 256, 1536
+    dy = bf(torch.randn(B * P, C, device="cuda"))
+    per_bc = torch.empty(B, C, device="cuda", dtype=torch.bfloat16)
+    per_c = torch.empty(C, device="cuda")
+    k.chan_sum(dy, B, P, C, per_bc=per_bc, per_c=per_c)
+    ref = dy.float().view(B, P, C).sum(1)
+    assert relerr(per_bc, ref) < 1e-2
+    assert relerr(per_c, ref.sum(0)) < 1e-4
+    pred = torch.randn(B * 1024, 8, device="cuda")
+    tgt = torch.randn(B, 4, 32, 32, device="cuda")
+    grad = torch.empty(B * 1024, 8, device="cuda", dtype=torch.bfloat16)
+    loss = torch.empty(1, device="cuda")
+    k.mse(pred, 8, tgt, B, 4, 1024, 1.0, grad, loss)
+    p4 = pred.view(B, 32, 32, 8)[..., :4].permute(0, 3, 1, 2)
+    assert abs(loss.item() - F.mse_loss(p4, tgt).item()) < 1e-5
+    g4 = grad.float().view(B, 32, 32, 8)
+    assert relerr(g4[..., :4].permute(0, 3, 1, 2), 2 * (p4 - tgt) / p4.numel()) < 1e-2
+    assert g4[..., 4:].abs().max().item() == 0
