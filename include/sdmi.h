@@ -84,6 +84,92 @@ typedef struct sdmi_gemm_desc {
 int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* workspace_bytes);
 int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t workspace_bytes, sdmi_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Fused multi-head attention (flash-style), bf16 in/out, fp32 softmax statistics.
+ * Replaces the core of torch nn.MultiheadAttention as called at models/blocks.py:128 (self) and
+ * :140 (cross, kv = context_proj(context)): softmax((q / sqrt(d)) k^T) v per head, head h in columns
+ * [h*d, h*d+d) of row-major [batch*len][ld] buffers; d % 8 == 0, d <= 64; S (keys) may differ from N.
+ * lse: fp32 [B*H][N] (saved for the backward).  Backward: dq, dk, dv (no atomics); delta_ws fp32 [B*H*N].
+ * ------------------------------------------------------------------------------------------- */
+int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* out, int ldo,
+                  float* lse, int B, int H, int N, int S, int d, sdmi_stream_t stream);
+int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, const void* o, int ldo,
+                  const void* dout, int lddo, const float* lse, float* delta_ws, void* dq, int lddq, void* dk,
+                  int lddk, void* dv, int lddv, int B, int H, int N, int S, int d, sdmi_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * GroupNorm (+ fused SiLU) on NHWC bf16 x[b][p][c] = x[(b*P + p)*ld + c]; fp32 statistics.
+ * Replaces nn.GroupNorm -> nn.SiLU (models/blocks.py:45-47, 64-66; unet_cond_base.py:179-180) and the
+ * attention pre-norms on the (B, C, HW) view (blocks.py:124-126, 137-139).  ws: sdmi_chan_reduce_workspace
+ * bytes.  sdmi_gn_bwd: dx (+= addend if given), dgamma/dbeta (fp32, may be NULL), coef_ws fp32 [B*G*2].
+ * sdmi_chan_sum: per-(b,c) pixel sums (bf16, row stride ld_bc) and per-channel sums (fp32; c < c_store),
+ * i.e. the bias and time-embedding-bias gradients of the convs at blocks.py:48-61, 102-107.
+ * ------------------------------------------------------------------------------------------- */
+size_t sdmi_chan_reduce_workspace(int B, int P, int C);
+int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, float* ws, float* mean, float* rstd,
+                  sdmi_stream_t stream);
+int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* mean, const float* rstd, const float* gamma,
+                  const float* beta, int B, int P, int C, int G, int silu, sdmi_stream_t stream);
+int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* mean,
+                const float* rstd, const float* gamma, const float* beta, int B, int P, int C, int G, int silu,
+                float* ws, float* coef_ws, float* dgamma, float* dbeta, const void* addend, int ldadd,
+                sdmi_stream_t stream);
+int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, float* ws, void* per_bc, int ld_bc, float* per_c,
+                  float* per_c2, int c_store, sdmi_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Input / output staging, scheduler, loss, time embedding, elementwise.
+ *  sdmi_prep_input   : unet_cond_base.py:131-140 -- x NCHW fp32 -> NHWC bf16 (cpad channels) with the
+ *                      nearest-resized mask (F.interpolate default) through the 1x1 cond_conv_in
+ *                      (no bias) in channels cx..cx+cmo-1; keep[b] (optional) = cond-drop multiplier
+ *                      (utils/diffusion_utils.py:31-37) applied at gather time.
+ *  sdmi_cond_wgrad   : gradient of cond_conv_in.weight.
+ *  sdmi_add_noise    : scheduler/linear_noise_scheduler.py:26-48 (bit-exact fp32 mul/mul/add).
+ *  sdmi_mse          : nn.MSELoss (train_ddpm_cond_celebhq_multi_gpu.py:267,346) + its gradient times
+ *                      the loss scale (gscale or *gscale_dev, GradScaler :269,362).
+ *  sdmi_time_embedding: models/blocks.py:5-24 (t stride 0 broadcasts one timestep).
+ * ------------------------------------------------------------------------------------------- */
+int sdmi_prep_input(const float* x, int B, int cx, int H, int W, const float* mask, int cmi, int MH, int MW,
+                    const float* wcond, int cmo, void* out, int cpad, const float* keep, sdmi_stream_t stream);
+int sdmi_cond_wgrad(const void* dxin, int ld, int cx, int B, int H, int W, const float* mask, int cmi, int MH, int MW,
+                    int cmo, float* dw, const float* keep, sdmi_stream_t stream);
+int sdmi_nhwc_to_nchw(const void* src, int src_f32, int ld, int B, int C, int HW, float* dst, sdmi_stream_t stream);
+int sdmi_nchw_to_nhwc_bf16(const float* src, int B, int C, int HW, void* dst, int ld, sdmi_stream_t stream);
+int sdmi_add_noise(const float* x0, const float* eps, const long long* t, const float* sqrt_abar,
+                   const float* sqrt_one_minus_abar, int B, long long per_sample, float* out, sdmi_stream_t stream);
+size_t sdmi_mse_workspace(void);
+int sdmi_mse(const float* pred, int ld, const float* target, int B, int C, int HW, float gscale,
+             const float* gscale_dev, void* grad, float* ws, float* loss, sdmi_stream_t stream);
+int sdmi_time_embedding(const long long* t, int tstride, int B, int dim, void* out, int ld, float* out_f32,
+                        sdmi_stream_t stream);
+int sdmi_silu(const void* x, const void* dy, void* y, long long n, sdmi_stream_t stream);
+int sdmi_copy_slice(const void* src, int lds, void* dst, int ldd, long long P, int C, int accumulate,
+                    sdmi_stream_t stream);
+
+/* bf16 GEMM-layout weight packing (the per-step fp32 -> bf16 cast that autocast performs,
+ * train_ddpm_cond_celebhq_multi_gpu.py:281-283, fused with the layout change):
+ * dst[o][a][b][i] = bf16(src[o*so + i*si + (kh_off + kh_mul*a)*skh + (kw_off + kw_mul*b)*skw]), 0 for i >= I. */
+typedef struct sdmi_pack_desc {
+  const float* src;
+  void* dst;
+  long long so, si, skh, skw;
+  int O, I, Ipad, KH, KW, kh_off, kh_mul, kw_off, kw_mul;
+} sdmi_pack_desc;
+int sdmi_pack_chunk(void);
+int sdmi_pack_weights(const sdmi_pack_desc* descs_dev, const void* bmap_dev, int nblocks, sdmi_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Optimizer step over flat fp32 buffers (train_ddpm_cond_celebhq_multi_gpu.py:362-378):
+ * GradScaler.unscale_ + clip_grad_norm_(max_norm) + non-finite skip + scaler.update (state on device:
+ * float[8] = {norm, coef, scale, growth, step, skip, loss, -}), then Adam (torch defaults) + EMA.
+ * grad_div = data-parallel world size (gradients arrive summed).
+ * ------------------------------------------------------------------------------------------- */
+size_t sdmi_optim_workspace(void);
+int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws, int growth_interval,
+                      int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
+int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n, const float* state,
+                  float lr, float b1, float b2, float eps, float ema_decay, sdmi_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -203,14 +203,6 @@ __global__ void copy_slice_kernel(const bf16_t* src, int lds, bf16_t* dst, int l
 // ---------------------------------------------------------------------------------------------
 }  // namespace
 
-extern "C" {
-typedef struct sdmi_pack_desc {
-  const float* src;
-  void* dst;
-  long long so, si, skh, skw;
-  int O, I, Ipad, KH, KW, kh_off, kh_mul, kw_off, kw_mul;
-} sdmi_pack_desc;
-}
 
 namespace {
 constexpr int PACK_CHUNK = 4096;  // elements per workgroup; bmap[blk] = (descriptor, chunk)

@@ -97,79 +97,127 @@ __global__ __launch_bounds__(NT) void chan_reduce_kernel(RedArgs a) {
   }
 }
 
-// mean/rstd per (b, g) from partial sums
-__global__ void gn_stats_finalize_kernel(const float* part, int B, int splits, int C, int G, int P, float eps,
-                                         float* mean, float* rstd) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= B * G) return;
-  int b = idx / G, g = idx - b * G;
-  int Cg = C / G;
-  double s1 = 0, s2 = 0;
-  for (int sp = 0; sp < splits; ++sp)
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-      const float* o = part + (((long long)b * splits + sp) * C + c) * 2;
-      s1 += o[0];
-      s2 += o[1];
+// ---- finalize kernels: partials [B][splits][C][2] -> per-(b,c) / per-(b,g) / per-c results ----
+
+// column sums over all (b, split) rows for 64 channels [c0, c0+64): 256 threads = 64 channels x 4 row groups
+__device__ __forceinline__ void colsum64(const float* part, int rows, int C, int c0, float& u, float& v, bool& own) {
+  __shared__ float red[4][64][2];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int c = c0 + cx;
+  float a = 0.f, b = 0.f;
+  if (c < C) {
+    int r = ry;
+    for (; r + 28 < rows; r += 32) {  // 8 independent loads in flight per lane
+      float2 v2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v2[j] = *(const float2*)(part + ((long long)(r + 4 * j) * C + c) * 2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a += v2[j].x; b += v2[j].y; }
     }
-  double n = (double)P * Cg;
-  double mu = s1 / n;
-  double var = s2 / n - mu * mu;
-  if (var < 0) var = 0;
-  mean[idx] = (float)mu;
-  rstd[idx] = (float)(1.0 / sqrt(var + (double)eps));
+    for (; r < rows; r += 4) {
+      const float2 v2 = *(const float2*)(part + ((long long)r * C + c) * 2);
+      a += v2.x;
+      b += v2.y;
+    }
+  }
+  red[ry][cx][0] = a;
+  red[ry][cx][1] = b;
+  __syncthreads();
+  own = ry == 0 && c < C;
+  u = red[0][cx][0] + red[1][cx][0] + red[2][cx][0] + red[3][cx][0];
+  v = red[0][cx][1] + red[1][cx][1] + red[2][cx][1] + red[3][cx][1];
 }
 
-// GN backward coefficients per (b, g): A = sum_c gamma_c * S1[b,c], Bc = sum_c gamma_c * S2[b,c]
-// and per-channel dgamma = sum_b S2, dbeta = sum_b S1.
-__global__ void gn_bwd_finalize_kernel(const float* part, int B, int splits, int C, int G, const float* gamma,
-                                       float* coef /*[B][G][2]*/, float* dgamma, float* dbeta) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  int Cg = C / G;
-  if (idx < B * G) {
-    int b = idx / G, g = idx - b * G;
-    float A = 0.f, Bc = 0.f;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-      float u = 0.f, v = 0.f;
-      for (int sp = 0; sp < splits; ++sp) {
-        const float* o = part + (((long long)b * splits + sp) * C + c) * 2;
-        u += o[0];
-        v += o[1];
-      }
-      A += gamma[c] * u;
-      Bc += gamma[c] * v;
+// per-channel totals of one batch row b over the splits, into LDS (C <= 2048)
+__device__ __forceinline__ void batch_totals(const float* part, int b, int splits, int C, float2* tot) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f, d = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float2 v2 = *(const float2*)(part + (((long long)b * splits + sp) * C + c) * 2);
+      a += v2.x;
+      d += v2.y;
     }
-    coef[idx * 2] = A;
-    coef[idx * 2 + 1] = Bc;
+    tot[c] = make_float2(a, d);
   }
-  if (idx < C && dgamma) {
-    float u = 0.f, v = 0.f;
-    for (int b = 0; b < B; ++b)
-      for (int sp = 0; sp < splits; ++sp) {
-        const float* o = part + (((long long)b * splits + sp) * C + idx) * 2;
-        u += o[0];
-        v += o[1];
-      }
-    dbeta[idx] = u;
-    dgamma[idx] = v;
+  __syncthreads();
+}
+
+// mean/rstd per (b, g): one block per b
+__global__ __launch_bounds__(256) void gn_stats_finalize_kernel(const float* part, int B, int splits, int C, int G,
+                                                                int P, float eps, float* mean, float* rstd) {
+  __shared__ float2 tot[2048];
+  const int b = blockIdx.x;
+  batch_totals(part, b, splits, C, tot);
+  const int Cg = C / G;
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    double s1 = 0, s2 = 0;
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+      s1 += tot[c].x;
+      s2 += tot[c].y;
+    }
+    double n = (double)P * Cg;
+    double mu = s1 / n;
+    double var = s2 / n - mu * mu;
+    if (var < 0) var = 0;
+    mean[b * G + g] = (float)mu;
+    rstd[b * G + g] = (float)(1.0 / sqrt(var + (double)eps));
   }
 }
 
-// per-(b,c) sums (mode 2) -> per_bc[b*ld + c] (bf16) and per_c[c] = per_c2[c] = sum_b (fp32)
-__global__ void chan_sum_finalize_kernel(const float* part, int B, int splits, int C, bf16_t* per_bc, int ld,
-                                         float* per_c, float* per_c2, int c_store) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < B * C && per_bc) {
-    int b = idx / C, c = idx - b * C;
-    float u = 0.f;
-    for (int sp = 0; sp < splits; ++sp) u += part[(((long long)b * splits + sp) * C + c) * 2];
-    per_bc[(long long)b * ld + c] = f2bf(u);
+// GN backward: blocks [0, B): coef[b][g] = (sum_c gamma_c S1[b,c], sum_c gamma_c S2[b,c]);
+// blocks [B, B + ceil(C/64)): dbeta[c] = sum_b S1, dgamma[c] = sum_b S2.
+__global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(const float* part, int B, int splits, int C, int G,
+                                                              const float* gamma, float* coef, float* dgamma,
+                                                              float* dbeta) {
+  if ((int)blockIdx.x < B) {
+    __shared__ float2 tot[2048];
+    const int b = blockIdx.x;
+    batch_totals(part, b, splits, C, tot);
+    const int Cg = C / G;
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+      float A = 0.f, Bc = 0.f;
+      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
+        A += gamma[c] * tot[c].x;
+        Bc += gamma[c] * tot[c].y;
+      }
+      coef[(b * G + g) * 2] = A;
+      coef[(b * G + g) * 2 + 1] = Bc;
+    }
+    return;
   }
-  if (idx < c_store && (per_c || per_c2)) {
-    float u = 0.f;
-    for (int b = 0; b < B; ++b)
-      for (int sp = 0; sp < splits; ++sp) u += part[(((long long)b * splits + sp) * C + idx) * 2];
-    if (per_c) per_c[idx] = u;
-    if (per_c2) per_c2[idx] = u;
+  float u, v;
+  bool own;
+  const int c0 = ((int)blockIdx.x - B) * 64;
+  colsum64(part, B * splits, C, c0, u, v, own);
+  if (own && dgamma) {
+    dbeta[c0 + (threadIdx.x & 63)] = u;
+    dgamma[c0 + (threadIdx.x & 63)] = v;
+  }
+}
+
+// per-(b,c) sums (mode 2): blocks [0, nbc) write per_bc[b*ld + c] (bf16); blocks [nbc, nbc + ceil(C/64)) write
+// per_c[c] = per_c2[c] = sum_b for c < c_store (fp32)
+__global__ __launch_bounds__(256) void chan_sum_finalize_kernel(const float* part, int B, int splits, int C,
+                                                                bf16_t* per_bc, int ld, float* per_c, float* per_c2,
+                                                                int c_store, int nbc) {
+  if ((int)blockIdx.x < nbc) {
+    int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx < B * C) {
+      int b = idx / C, c = idx - b * C;
+      float u = 0.f;
+      for (int sp = 0; sp < splits; ++sp) u += part[(((long long)b * splits + sp) * C + c) * 2];
+      per_bc[(long long)b * ld + c] = f2bf(u);
+    }
+    return;
+  }
+  float u, v;
+  bool own;
+  const int c0 = ((int)blockIdx.x - nbc) * 64;
+  colsum64(part, B * splits, C, c0, u, v, own);
+  const int c = c0 + (threadIdx.x & 63);
+  if (own && c < c_store) {
+    if (per_c) per_c[c] = u;
+    if (per_c2) per_c2[c] = u;
   }
 }
 
@@ -234,7 +282,7 @@ __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
 
 int pick_splits(int B, int P) {
   int s = 1;
-  while (B * s < 512 && P / (s * 2) >= 16) s *= 2;
+  while (B * s < 256 && P / (s * 2) >= 32) s *= 2;
   return s;
 }
 
@@ -258,8 +306,7 @@ extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G,
   a.splits = pick_splits(B, P); a.part = ws;
   hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, a.splits), dim3(NT), 0, s, a);
   SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3((B * G + 255) / 256), dim3(256), 0, s, ws, B, a.splits, C, G, P,
-                     eps, mean, rstd);
+  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(B), dim3(256), 0, s, ws, B, a.splits, C, G, P, eps, mean, rstd);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -288,9 +335,8 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.mode = 1; r.splits = pick_splits(B, P); r.part = ws;
   hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, r.splits), dim3(NT), 0, s, r);
   SDMI_CHECK_LAUNCH();
-  int n = B * G > C ? B * G : C;
-  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ws, B, r.splits, C, G, gamma,
-                     coef_ws, dgamma, dbeta);
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(B + (dgamma ? (C + 63) / 64 : 0)), dim3(256), 0, s, ws, B, r.splits,
+                     C, G, gamma, coef_ws, dgamma, dbeta);
   SDMI_CHECK_LAUNCH();
   ApplyArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.dy = (const bf16_t*)dy; a.lddy = lddy; a.dx = (bf16_t*)dx; a.lddx = lddx;
@@ -313,9 +359,11 @@ extern "C" int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, floa
   r.splits = pick_splits(B, P); r.part = ws;
   hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, r.splits), dim3(NT), 0, s, r);
   SDMI_CHECK_LAUNCH();
-  int n = B * C;
-  hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ws, B, r.splits, C,
-                     (bf16_t*)per_bc, ld_bc, per_c, per_c2, c_store);
+  int nbc = per_bc ? (B * C + 255) / 256 : 0;
+  int ncol = (per_c || per_c2) ? (C + 63) / 64 : 0;
+  if (nbc + ncol == 0) return 0;
+  hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3(nbc + ncol), dim3(256), 0, s, ws, B, r.splits, C, (bf16_t*)per_bc,
+                     ld_bc, per_c, per_c2, c_store, nbc);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

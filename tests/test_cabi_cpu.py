@@ -1,0 +1,73 @@
+"""CPU-side checks of the C-ABI boundary: the in-tree libsdmi.so loads without a GPU and exports every
+entry point include/sdmi.h declares (no compute is launched here), and the host-side logic (flat
+store ordering, module state-dict surface, bucket watermarks) is consistent."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "sdmi.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|size_t)\s+(sdmi_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from sdmi import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libsdmi.so not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), f"{s} declared in sdmi.h but not exported"
+    # every declared symbol is bound with a signature in the ctypes layer
+    assert set(syms) <= set(_lib.SIGNATURES), set(syms) - set(_lib.SIGNATURES)
+
+
+def test_module_state_dict_matches_reference_layout():
+    from oracle import sd_oracle as O
+    from tests.golden.configs import SMALL_COND, SMALL_UNCOND, full_cond_config
+    import models.unet_cond_base as mc
+    import models.unet_base as mu
+    for cfg, mod, base in ((SMALL_COND, mc, "cond"), (SMALL_UNCOND, mu, "uncond"), (full_cond_config(), mc, "cond")):
+        m = mod.Unet(4, cfg)
+        shapes = O.unet_param_shapes(cfg, base=base)
+        sd = m.state_dict()
+        assert list(sd.keys()) == list(shapes.keys())
+        assert all(tuple(v.shape) == tuple(shapes[k]) for k, v in sd.items())
+
+
+def test_flat_store_order_and_contiguous_runs():
+    import torch
+    from oracle import sd_oracle as O
+    from tests.golden.configs import full_cond_config
+    from sdmi.store import FlatStore, param_label
+    from sdmi.unet_engine import layout, resnet_list, contiguous_run
+    cfg = full_cond_config()
+    shapes = O.unet_param_shapes(cfg)
+    st = FlatStore(shapes, cfg, "cpu")
+    assert st.numel == 118513466
+    res = resnet_list(layout(cfg))
+    tw = [f"{p}.t_emb_layers.{l}.1.weight" for (p, l, ci, co) in res]
+    v = contiguous_run(st.g, tw, (sum(co for (_, _, _, co) in res), 512))
+    assert v.shape[0] == sum(co for (_, _, _, co) in res)
+    # head parameters first, then up blocks (backward order)
+    assert param_label(st.order[0]) == "head"
+    assert st.order.index("ups.2.attentions.0.in_proj_weight") < st.order.index("downs.0.attentions.0.in_proj_weight")
+
+
+def test_scheduler_tables_host():
+    from scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    from oracle import sd_oracle as O
+    s = LinearNoiseScheduler(1000, 0.00085, 0.012)
+    o = O.SchedulerTables(1000, 0.00085, 0.012)
+    import torch
+    assert torch.equal(s.alpha_cum_prod, o.alpha_cum_prod)
+    with pytest.raises(RuntimeError):
+        s.add_noise(torch.zeros(1, 4, 8, 8), torch.zeros(1, 4, 8, 8), torch.zeros(1, dtype=torch.long))
