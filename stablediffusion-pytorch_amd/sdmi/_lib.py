@@ -88,6 +88,9 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libsdmi.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        # torch must bring in its HIP runtime first: libsdmi.so's libamdhip64.so.7 dependency then binds
+        # to that same (already loaded, same SONAME) runtime instead of loading a second copy.
+        import torch  # noqa: F401
         L = ctypes.CDLL(LIB_PATH)
         for name, (argt, rest) in SIGNATURES.items():
             fn = getattr(L, name)
