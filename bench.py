@@ -142,6 +142,8 @@ def main():
         prof, K.PROFILE = K.PROFILE, None
         by = {}
         for tag, fl, e0, e1, sp in prof:
+            if not tag.startswith("gemm"):
+                continue
             ms = e0.elapsed_time(e1)
             a = by.setdefault(tag, [0.0, 0.0, 0])
             a[0] += fl

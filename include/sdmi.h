@@ -78,6 +78,10 @@ typedef struct sdmi_gemm_desc {
   /* store limits (0 = m / n): rows >= m_store and columns >= n_store are computed but not stored,
    * and the bias is read only for stored columns (zero-padded output channels) */
   int m_store, n_store;
+  /* second A source (SDMI_A_CONV only): columns k >= k_split read a2[m*lda2 + (k - k_split)] (bf16, row-major,
+   * same pixel grid) -- fuses a 1x1 conv of another tensor into the same GEMM by K-concatenation */
+  const void* a2; int lda2; int k_split;
+  const float* bias2; /* second fp32 [n] bias added in the epilogue, or NULL */
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */
@@ -101,19 +105,20 @@ int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v,
  * GroupNorm (+ fused SiLU) on NHWC bf16 x[b][p][c] = x[(b*P + p)*ld + c]; fp32 statistics.
  * Replaces nn.GroupNorm -> nn.SiLU (models/blocks.py:45-47, 64-66; unet_cond_base.py:179-180) and the
  * attention pre-norms on the (B, C, HW) view (blocks.py:124-126, 137-139).  ws: sdmi_chan_reduce_workspace
- * bytes.  sdmi_gn_bwd: dx (+= addend if given), dgamma/dbeta (fp32, may be NULL), coef_ws fp32 [B*G*2].
+ * bytes.  sdmi_gn_bwd: dx (+= addend if given), dgamma/dbeta (fp32, may be NULL), table2_ws fp32 [B*C*4].
  * sdmi_chan_sum: per-(b,c) pixel sums (bf16, row stride ld_bc) and per-channel sums (fp32; c < c_store),
  * i.e. the bias and time-embedding-bias gradients of the convs at blocks.py:48-61, 102-107.
  * ------------------------------------------------------------------------------------------- */
 size_t sdmi_chan_reduce_workspace(int B, int P, int C);
-int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, float* ws, float* mean, float* rstd,
+/* table: fp32 float4 [B][C] = {a = rstd*gamma, s = beta - mean*a, mean, rstd} (per (b, c); the group
+ * statistics folded with the affine), produced by sdmi_gn_stats and consumed by apply / backward. */
+int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, const float* gamma, const float* beta,
+                  float* ws, float* table, sdmi_stream_t stream);
+int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* table, int B, int P, int C, int silu,
                   sdmi_stream_t stream);
-int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* mean, const float* rstd, const float* gamma,
-                  const float* beta, int B, int P, int C, int G, int silu, sdmi_stream_t stream);
-int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* mean,
-                const float* rstd, const float* gamma, const float* beta, int B, int P, int C, int G, int silu,
-                float* ws, float* coef_ws, float* dgamma, float* dbeta, const void* addend, int ldadd,
-                sdmi_stream_t stream);
+int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws, float* dgamma,
+                float* dbeta, const void* addend, int ldadd, sdmi_stream_t stream);
 int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, float* ws, void* per_bc, int ld_bc, float* per_c,
                   float* per_c2, int c_store, sdmi_stream_t stream);
 
@@ -154,6 +159,7 @@ typedef struct sdmi_pack_desc {
   void* dst;
   long long so, si, skh, skw;
   int O, I, Ipad, KH, KW, kh_off, kh_mul, kw_off, kw_mul;
+  int dst_ld; /* row stride of dst in elements (0 = KH*KW*Ipad): packs into a column slice of a wider matrix */
 } sdmi_pack_desc;
 int sdmi_pack_chunk(void);
 int sdmi_pack_weights(const sdmi_pack_desc* descs_dev, const void* bmap_dev, int nblocks, sdmi_stream_t stream);

@@ -9,58 +9,75 @@
 // Layout: Q/K/V/O are row-major [batch*len][ld] bf16 with head h at columns h*d .. h*d+d-1 (the
 // packed in-projection output is used in place: q, k, v are column offsets of one buffer).
 //
-// Forward  : per (b, h, 64-query tile), 4 waves x 16 queries, keys streamed through LDS in 64-key
-//            tiles. "Swapped" product S^T = K Q^T puts the query on the lane, so the softmax
-//            row statistics are per lane and P^T feeds the PV MFMA directly from the accumulator
-//            registers (keys permuted consistently in both operands; V read with ds_read_b64_tr_b16).
+// All three kernels share one structure: 4 waves x 32 rows (two 16-row groups per wave) = 128 rows
+// per workgroup stay on the MFMA lanes, the other operand is streamed through a double-buffered LDS
+// ring of 64-row tiles (next tile prefetched into registers while the current one is consumed, one
+// barrier per tile); every LDS fragment is read once and used by both row groups.
+//
+// Forward  : queries on lanes, "swapped" S^T = K Q^T so the softmax statistics are per lane and P^T
+//            feeds the PV MFMA straight from the accumulator registers (the key order inside a 32-key
+//            step is permuted identically in both operands; V is read with ds_read_b64_tr_b16).
 // Backward : two kernels, no atomics:
-//            dkv: per (b, h, 64-key tile), keys on the lane (S = Q K^T): dV^T += dO^T P, dK^T += Q^T dS
-//            dq : per (b, h, 64-query tile), queries on the lane (S^T = K Q^T): dQ^T += K^T dS^T
+//            dkv: keys on lanes (S = Q K^T): dV^T += dO^T P, dK^T += Q^T dS
+//            dq : queries on lanes (S^T = K Q^T): dQ^T += K^T dS^T
 //            with P recomputed from the forward's log-sum-exp and delta = rowsum(dO * O).
 #include "common.h"
 #include "../../include/sdmi.h"
 
 namespace {
 
-constexpr int TQ = 64, TK = 64, NT = 256;
+constexpr int NT = 256, ROWS = 128, TILE = 64;
 constexpr float LOG2E = 1.4426950408889634f;
 
 struct AttnArgs {
   const bf16_t* q; const bf16_t* k; const bf16_t* v; const bf16_t* o; const bf16_t* dout;
   bf16_t* out; bf16_t* dq; bf16_t* dk; bf16_t* dv;
-  float* lse;        // [B*H][N]  base-2 log-sum-exp of (score * scale * log2e)
-  const float* delta; // [B*H][N]
+  float* lse;          // [B*H][N]  base-2 log-sum-exp of (score * scale * log2e)
+  const float* delta;  // [B*H][N]
   int ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv;
   int B, H, N, S, d;
-  float scale;       // 1/sqrt(d)
+  float scale;  // 1/sqrt(d)
 };
 
-// LDS tile [64 rows][DP + 8] bf16 (row padded by 16 B)
 template <int DP> struct Tile {
-  static constexpr int LD = DP + 8;
-  static constexpr int BYTES = 64 * LD * 2;
+  static constexpr int LD = DP + 8;  // row padded by 16 B
+  static constexpr int ELEMS = 64 * LD;
+  static constexpr int CPT = 64 * DP / 8 / NT;  // 16-B chunks per thread per tile (1 or 2)
 };
 
-// load a 64-row x DP-col tile of head columns [col0, col0 + d) (zero outside rows < nrows, cols < d)
+// register prefetch of one 64-row x DP tile (zero outside rows < nrows, head columns < d)
 template <int DP>
-__device__ __forceinline__ void load_tile(bf16_t* t, const bf16_t* src, int ld, int row0, int nrows, int col0, int d) {
-  constexpr int CPR = DP / 8;  // 16-B chunks per row
-  for (int c = threadIdx.x; c < 64 * CPR; c += NT) {
-    int r = c / CPR, ch = c - r * CPR;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (row0 + r < nrows && ch * 8 < d) v = *(const uint4*)(src + (long long)(row0 + r) * ld + col0 + ch * 8);
-    *(uint4*)(t + r * Tile<DP>::LD + ch * 8) = v;
+__device__ __forceinline__ void tile_fetch(uint4 (&r)[Tile<DP>::CPT], const bf16_t* src, int ld, int row0, int nrows,
+                                           int col0, int d) {
+  constexpr int CPR = DP / 8;
+#pragma unroll
+  for (int j = 0; j < Tile<DP>::CPT; ++j) {
+    int c = threadIdx.x + j * NT;
+    int rr = c / CPR, ch = c - rr * CPR;
+    r[j] = make_uint4(0, 0, 0, 0);
+    if (row0 + rr < nrows && ch * 8 < d) r[j] = *(const uint4*)(src + (long long)(row0 + rr) * ld + col0 + ch * 8);
   }
 }
 
-// A/B fragment where the MFMA row index = tile row (16 rows from rbase), k = tile column (32 from kbase)
+template <int DP>
+__device__ __forceinline__ void tile_store(bf16_t* t, const uint4 (&r)[Tile<DP>::CPT]) {
+  constexpr int CPR = DP / 8;
+#pragma unroll
+  for (int j = 0; j < Tile<DP>::CPT; ++j) {
+    int c = threadIdx.x + j * NT;
+    int rr = c / CPR, ch = c - rr * CPR;
+    *(uint4*)(t + rr * Tile<DP>::LD + ch * 8) = r[j];
+  }
+}
+
+// fragment with MFMA row = tile row (rbase + lane&15), k = tile columns kbase + 8*(lane>>4) .. +7
 template <int DP>
 __device__ __forceinline__ s16x8 frag_rows(const bf16_t* t, int rbase, int kbase, int lane) {
   return *(const s16x8*)(t + (rbase + (lane & 15)) * Tile<DP>::LD + kbase + (lane >> 4) * 8);
 }
 
-// transposed fragment: MFMA row index = tile column (16 cols from cbase), k = tile rows
-// permuted as {rbase + 4g + j (j<4), rbase + 16 + 4g + j-4 (j>=4)} for lane group g = lane>>4.
+// transposed fragment: MFMA row = tile column (cbase + lane&15), k = tile rows permuted as
+// {rbase + 4g + j (j<4), rbase + 16 + 4g + j-4 (j>=4)} for lane group g = lane>>4
 template <int DP>
 __device__ __forceinline__ s16x8 frag_tr(const bf16_t* t, int rbase, int cbase, int lane) {
   int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -76,15 +93,18 @@ __device__ __forceinline__ s16x8 frag_tr(const bf16_t* t, int rbase, int cbase, 
 
 // B-operand fragment from two accumulator tiles (rows = k): elements j<4 from a[j], j>=4 from b[j-4]
 __device__ __forceinline__ s16x8 pack_acc(const f32x4& a, const f32x4& b) {
-  s16x8 r;
-  r[0] = (short)f2bf(a[0]); r[1] = (short)f2bf(a[1]); r[2] = (short)f2bf(a[2]); r[3] = (short)f2bf(a[3]);
-  r[4] = (short)f2bf(b[0]); r[5] = (short)f2bf(b[1]); r[6] = (short)f2bf(b[2]); r[7] = (short)f2bf(b[3]);
-  return r;
+  uint4 u;
+  u.x = pack2bf(a[0], a[1]);
+  u.y = pack2bf(a[2], a[3]);
+  u.z = pack2bf(b[0], b[1]);
+  u.w = pack2bf(b[2], b[3]);
+  return __builtin_bit_cast(s16x8, u);
 }
 
-// per-lane register fragment of one row (16-row block on lanes): row = row0 + (lane&15), d = 8*(lane>>4) + 32*ks
+// register fragment of one row (row on lane&15): d = 32*ks + 8*(lane>>4) .. +7
 template <int DP>
-__device__ __forceinline__ void row_frags(s16x8 (&f)[DP / 32], const bf16_t* src, int ld, int row, int nrows, int col0, int d, int lane) {
+__device__ __forceinline__ void row_frags(s16x8 (&f)[DP / 32], const bf16_t* src, int ld, int row, int nrows, int col0,
+                                          int d, int lane) {
 #pragma unroll
   for (int ks = 0; ks < DP / 32; ++ks) {
     int dd = ks * 32 + (lane >> 4) * 8;
@@ -94,99 +114,142 @@ __device__ __forceinline__ void row_frags(s16x8 (&f)[DP / 32], const bf16_t* src
   }
 }
 
+__device__ __forceinline__ f32x4 mfma(const s16x8& a, const s16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void store4(bf16_t* dst, const f32x4& v, float s) {
+  uint2 w;
+  w.x = pack2bf(v[0] * s, v[1] * s);
+  w.y = pack2bf(v[2] * s, v[3] * s);
+  *(uint2*)dst = w;
+}
+
 // =============================================================================================
 // forward
 // =============================================================================================
 template <int DP>
-__global__ __launch_bounds__(NT) void attn_fwd_kernel(AttnArgs a) {
-  constexpr int DT = DP / 16;  // max output row tiles (d <= DP)
-  __shared__ __attribute__((aligned(16))) bf16_t sK[64 * Tile<DP>::LD];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[64 * Tile<DP>::LD];
+__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int DT = DP / 16;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int q0 = blockIdx.x * TQ + wave * 16;
-  const int myq = q0 + (lane & 15);
   const int dt_n = (a.d + 15) / 16;
   const float c = a.scale * LOG2E;
-
   const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
   const bf16_t* K = a.k + (long long)b * a.S * a.ldk;
   const bf16_t* V = a.v + (long long)b * a.S * a.ldv;
-  s16x8 qf[DP / 32];
-  row_frags<DP>(qf, Q, a.ldq, myq, a.N, h * a.d, a.d, lane);
 
-  float m = -INFINITY, l = 0.f;
-  f32x4 o[DT];
+  int myq[2];
+  s16x8 qf[2][DP / 32];
+  float m[2], l[2];
+  f32x4 o[2][DT];
 #pragma unroll
-  for (int t = 0; t < DT; ++t) o[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < 2; ++g) {
+    myq[g] = blockIdx.x * ROWS + wave * 32 + g * 16 + (lane & 15);
+    row_frags<DP>(qf[g], Q, a.ldq, myq[g], a.N, h * a.d, a.d, lane);
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[g][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 
-  for (int k0 = 0; k0 < a.S; k0 += TK) {
-    __syncthreads();
-    load_tile<DP>(sK, K, a.ldk, k0, a.S, h * a.d, a.d);
-    load_tile<DP>(sV, V, a.ldv, k0, a.S, h * a.d, a.d);
-    __syncthreads();
-    f32x4 s[4];
+  uint4 rk[Tile<DP>::CPT], rv[Tile<DP>::CPT];
+  tile_fetch<DP>(rk, K, a.ldk, 0, a.S, h * a.d, a.d);
+  tile_fetch<DP>(rv, V, a.ldv, 0, a.S, h * a.d, a.d);
+  tile_store<DP>(smem, rk);
+  tile_store<DP>(smem + Tile<DP>::ELEMS, rv);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < a.S; k0 += TILE) {
+    const bool more = k0 + TILE < a.S;
+    if (more) {
+      tile_fetch<DP>(rk, K, a.ldk, k0 + TILE, a.S, h * a.d, a.d);
+      tile_fetch<DP>(rv, V, a.ldv, k0 + TILE, a.S, h * a.d, a.d);
+    }
+    const bf16_t* sK = smem + cur * 2 * Tile<DP>::ELEMS;
+    const bf16_t* sV = sK + Tile<DP>::ELEMS;
+    f32x4 s[2][4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      s[kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      s[0][kb] = s[1][kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < DP / 32; ++ks)
-        s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<DP>(sK, kb * 16, ks * 32, lane), qf[ks], s[kb], 0, 0, 0);
+      for (int ks = 0; ks < DP / 32; ++ks) {
+        s16x8 kf = frag_rows<DP>(sK, kb * 16, ks * 32, lane);
+        s[0][kb] = mfma(kf, qf[0][ks], s[0][kb]);
+        s[1][kb] = mfma(kf, qf[1][ks], s[1][kb]);
+      }
     }
-    float mx = -INFINITY;
+    if (k0 + TILE > a.S) {  // ragged last tile (cross-attention S = 77): mask keys >= S
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+      for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int key = k0 + kb * 16 + (lane >> 4) * 4 + i;
-        float v = key < a.S ? s[kb][i] * c : -INFINITY;
-        s[kb][i] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float mn = fmaxf(m, mx);
-    float alpha = exp2f(m - mn);
-    m = mn;
-    l *= alpha;
+        for (int i = 0; i < 4; ++i)
+          if (k0 + kb * 16 + (lane >> 4) * 4 + i >= a.S) s[0][kb][i] = s[1][kb][i] = -INFINITY;
+    }
+    s16x8 pf[2][2];
 #pragma unroll
-    for (int t = 0; t < DT; ++t) o[t] *= alpha;
+    for (int g = 0; g < 2; ++g) {
+      float mx = -INFINITY;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+      for (int kb = 0; kb < 4; ++kb)
+        mx = fmaxf(mx, fmaxf(fmaxf(s[g][kb][0], s[g][kb][1]), fmaxf(s[g][kb][2], s[g][kb][3])));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[g], mx * c);
+      const float alpha = exp2f(m[g] - mn);
+      m[g] = mn;
+      float ls = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float p = exp2f(s[kb][i] - mn);
-        s[kb][i] = p;
-        l += p;
-      }
+      for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      s16x8 pf = pack_acc(s[2 * s2], s[2 * s2 + 1]);
+        for (int i = 0; i < 4; ++i) {
+          float p = exp2f(fmaf(s[g][kb][i], c, -mn));
+          s[g][kb][i] = p;
+          ls += p;
+        }
+      l[g] = fmaf(l[g], alpha, ls);
+#pragma unroll
+      for (int t = 0; t < DT; ++t) o[g][t] *= alpha;
+      pf[g][0] = pack_acc(s[g][0], s[g][1]);
+      pf[g][1] = pack_acc(s[g][2], s[g][3]);
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int t = 0; t < DT; ++t)
-        if (t < dt_n) o[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<DP>(sV, 32 * s2, 16 * t, lane), pf, o[t], 0, 0, 0);
+        if (t < dt_n) {
+          s16x8 vf = frag_tr<DP>(sV, 32 * s2, 16 * t, lane);
+          o[0][t] = mfma(vf, pf[0][s2], o[0][t]);
+          o[1][t] = mfma(vf, pf[1][s2], o[1][t]);
+        }
+    if (more) {
+      bf16_t* nK = smem + (cur ^ 1) * 2 * Tile<DP>::ELEMS;
+      tile_store<DP>(nK, rk);
+      tile_store<DP>(nK + Tile<DP>::ELEMS, rv);
     }
+    __syncthreads();
+    cur ^= 1;
   }
-  l += __shfl_xor(l, 16, 64);
-  l += __shfl_xor(l, 32, 64);
-  if (myq < a.N) {
-    float inv = 1.f / l;
-    bf16_t* O = a.out + ((long long)b * a.N + myq) * a.ldo + h * a.d;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      int d0 = 16 * t + (lane >> 4) * 4;
-      if (t < dt_n && d0 < a.d) {
-        uint2 w;
-        w.x = pack2bf(o[t][0] * inv, o[t][1] * inv);
-        w.y = pack2bf(o[t][2] * inv, o[t][3] * inv);
-        *(uint2*)(O + d0) = w;
+  for (int g = 0; g < 2; ++g) {
+    float lt = l[g];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (myq[g] < a.N) {
+      const float inv = 1.f / lt;
+      bf16_t* O = a.out + ((long long)b * a.N + myq[g]) * a.ldo + h * a.d;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        int d0 = 16 * t + (lane >> 4) * 4;
+        if (t < dt_n && d0 < a.d) store4(O + d0, o[g][t], inv);
       }
+      if ((lane >> 4) == 0) a.lse[(long long)bh * a.N + myq[g]] = m[g] + __log2f(lt);
     }
-    if ((lane >> 4) == 0) a.lse[(long long)bh * a.N + myq] = m + __log2f(l);
   }
 }
 
-// delta[bh][q] = sum_d dO[q][h*d + .] * O[q][h*d + .]   (one wave per query row segment)
+// delta[bh][q] = sum_d dO[q][h*d + .] * O[q][h*d + .]
 __global__ void attn_delta_kernel(AttnArgs a) {
   long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (b, q, h)
   long long total = (long long)a.B * a.N * a.H;
@@ -209,159 +272,217 @@ __global__ void attn_delta_kernel(AttnArgs a) {
 }
 
 // =============================================================================================
-// backward: dK, dV (keys on lanes)
+// backward: dK, dV (keys on lanes, 128 keys per workgroup, query tiles streamed)
 // =============================================================================================
 template <int DP>
-__global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int DT = DP / 16;
-  __shared__ __attribute__((aligned(16))) bf16_t sQ[64 * Tile<DP>::LD];
-  __shared__ __attribute__((aligned(16))) bf16_t sO[64 * Tile<DP>::LD];  // dO tile
-  __shared__ float sL[64], sD[64];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][Q|dO]
+  __shared__ float sLD[2][2][64];                                            // [buf][lse|delta]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int kk0 = blockIdx.x * TK + wave * 16;
-  const int mykey = kk0 + (lane & 15);
   const int dt_n = (a.d + 15) / 16;
   const float c = a.scale * LOG2E;
-
   const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
   const bf16_t* dO = a.dout + (long long)b * a.N * a.lddo;
-  s16x8 kf[DP / 32], vf[DP / 32];
-  row_frags<DP>(kf, a.k + (long long)b * a.S * a.ldk, a.ldk, mykey, a.S, h * a.d, a.d, lane);
-  row_frags<DP>(vf, a.v + (long long)b * a.S * a.ldv, a.ldv, mykey, a.S, h * a.d, a.d, lane);
 
-  f32x4 dk[DT], dv[DT];
+  int mykey[2];
+  s16x8 kf[2][DP / 32], vf[2][DP / 32];
+  f32x4 dk[2][DT], dv[2][DT];
 #pragma unroll
-  for (int t = 0; t < DT; ++t) { dk[t] = (f32x4){0.f, 0.f, 0.f, 0.f}; dv[t] = dk[t]; }
+  for (int g = 0; g < 2; ++g) {
+    mykey[g] = blockIdx.x * ROWS + wave * 32 + g * 16 + (lane & 15);
+    row_frags<DP>(kf[g], a.k + (long long)b * a.S * a.ldk, a.ldk, mykey[g], a.S, h * a.d, a.d, lane);
+    row_frags<DP>(vf[g], a.v + (long long)b * a.S * a.ldv, a.ldv, mykey[g], a.S, h * a.d, a.d, lane);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) dk[g][t] = dv[g][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 
-  for (int q0 = 0; q0 < a.N; q0 += TQ) {
-    __syncthreads();
-    load_tile<DP>(sQ, Q, a.ldq, q0, a.N, h * a.d, a.d);
-    load_tile<DP>(sO, dO, a.lddo, q0, a.N, h * a.d, a.d);
+  uint4 rq[Tile<DP>::CPT], ro[Tile<DP>::CPT];
+  float rl = 0.f, rd = 0.f;
+  auto fetch = [&](int q0) __attribute__((always_inline)) {
+    tile_fetch<DP>(rq, Q, a.ldq, q0, a.N, h * a.d, a.d);
+    tile_fetch<DP>(ro, dO, a.lddo, q0, a.N, h * a.d, a.d);
     if (threadIdx.x < 64) {
       int q = q0 + threadIdx.x;
-      sL[threadIdx.x] = q < a.N ? a.lse[(long long)bh * a.N + q] : INFINITY;
-      sD[threadIdx.x] = q < a.N ? a.delta[(long long)bh * a.N + q] : 0.f;
+      rl = q < a.N ? a.lse[(long long)bh * a.N + q] : INFINITY;  // invalid rows: p = 0
+      rd = q < a.N ? a.delta[(long long)bh * a.N + q] : 0.f;
     }
-    __syncthreads();
-    f32x4 p[4], ds[4];
+  };
+  auto put = [&](int buf) __attribute__((always_inline)) {
+    tile_store<DP>(smem + buf * 2 * Tile<DP>::ELEMS, rq);
+    tile_store<DP>(smem + buf * 2 * Tile<DP>::ELEMS + Tile<DP>::ELEMS, ro);
+    if (threadIdx.x < 64) {
+      sLD[buf][0][threadIdx.x] = rl;
+      sLD[buf][1][threadIdx.x] = rd;
+    }
+  };
+  fetch(0);
+  put(0);
+  __syncthreads();
+  int cur = 0;
+  for (int q0 = 0; q0 < a.N; q0 += TILE) {
+    const bool more = q0 + TILE < a.N;
+    if (more) fetch(q0 + TILE);
+    const bf16_t* sQ = smem + cur * 2 * Tile<DP>::ELEMS;
+    const bf16_t* sO = sQ + Tile<DP>::ELEMS;
+    f32x4 p[2][4], ds[2][4];
 #pragma unroll
     for (int qb = 0; qb < 4; ++qb) {
-      f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = s;
+      p[0][qb] = p[1][qb] = ds[0][qb] = ds[1][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < DP / 32; ++ks) {
-        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<DP>(sQ, qb * 16, ks * 32, lane), kf[ks], s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<DP>(sO, qb * 16, ks * 32, lane), vf[ks], dp, 0, 0, 0);
+        s16x8 qa = frag_rows<DP>(sQ, qb * 16, ks * 32, lane);
+        s16x8 oa = frag_rows<DP>(sO, qb * 16, ks * 32, lane);
+        p[0][qb] = mfma(qa, kf[0][ks], p[0][qb]);
+        p[1][qb] = mfma(qa, kf[1][ks], p[1][qb]);
+        ds[0][qb] = mfma(oa, vf[0][ks], ds[0][qb]);
+        ds[1][qb] = mfma(oa, vf[1][ks], ds[1][qb]);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        int qi = qb * 16 + (lane >> 4) * 4 + i;  // row within tile; invalid rows have lse = +inf -> p = 0
-        float pv = exp2f(s[i] * c - sL[qi]);
-        p[qb][i] = pv;
-        ds[qb][i] = pv * (dp[i] - sD[qi]);
+        const int qi = qb * 16 + (lane >> 4) * 4 + i;
+        const float L = sLD[cur][0][qi], D = sLD[cur][1][qi];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          float pv = exp2f(fmaf(p[g][qb][i], c, -L));
+          p[g][qb][i] = pv;
+          ds[g][qb][i] = pv * (ds[g][qb][i] - D);
+        }
       }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      s16x8 pf = pack_acc(p[2 * s2], p[2 * s2 + 1]);
-      s16x8 df = pack_acc(ds[2 * s2], ds[2 * s2 + 1]);
+      s16x8 pf0 = pack_acc(p[0][2 * s2], p[0][2 * s2 + 1]), pf1 = pack_acc(p[1][2 * s2], p[1][2 * s2 + 1]);
+      s16x8 df0 = pack_acc(ds[0][2 * s2], ds[0][2 * s2 + 1]), df1 = pack_acc(ds[1][2 * s2], ds[1][2 * s2 + 1]);
 #pragma unroll
       for (int t = 0; t < DT; ++t)
         if (t < dt_n) {
-          dv[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<DP>(sO, 32 * s2, 16 * t, lane), pf, dv[t], 0, 0, 0);
-          dk[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<DP>(sQ, 32 * s2, 16 * t, lane), df, dk[t], 0, 0, 0);
+          s16x8 ot = frag_tr<DP>(sO, 32 * s2, 16 * t, lane);
+          dv[0][t] = mfma(ot, pf0, dv[0][t]);
+          dv[1][t] = mfma(ot, pf1, dv[1][t]);
+          s16x8 qt = frag_tr<DP>(sQ, 32 * s2, 16 * t, lane);
+          dk[0][t] = mfma(qt, df0, dk[0][t]);
+          dk[1][t] = mfma(qt, df1, dk[1][t]);
         }
     }
+    if (more) put(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
   }
-  if (mykey < a.S) {
-    bf16_t* DK = a.dk + ((long long)b * a.S + mykey) * a.lddk + h * a.d;
-    bf16_t* DV = a.dv + ((long long)b * a.S + mykey) * a.lddv + h * a.d;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      int d0 = 16 * t + (lane >> 4) * 4;
-      if (t < dt_n && d0 < a.d) {
-        uint2 w;
-        w.x = pack2bf(dk[t][0] * a.scale, dk[t][1] * a.scale);
-        w.y = pack2bf(dk[t][2] * a.scale, dk[t][3] * a.scale);
-        *(uint2*)(DK + d0) = w;
-        w.x = pack2bf(dv[t][0], dv[t][1]);
-        w.y = pack2bf(dv[t][2], dv[t][3]);
-        *(uint2*)(DV + d0) = w;
+  for (int g = 0; g < 2; ++g)
+    if (mykey[g] < a.S) {
+      bf16_t* DK = a.dk + ((long long)b * a.S + mykey[g]) * a.lddk + h * a.d;
+      bf16_t* DV = a.dv + ((long long)b * a.S + mykey[g]) * a.lddv + h * a.d;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        int d0 = 16 * t + (lane >> 4) * 4;
+        if (t < dt_n && d0 < a.d) {
+          store4(DK + d0, dk[g][t], a.scale);
+          store4(DV + d0, dv[g][t], 1.f);
+        }
       }
     }
-  }
 }
 
 // =============================================================================================
-// backward: dQ (queries on lanes)
+// backward: dQ (queries on lanes, 128 queries per workgroup, key tiles streamed)
 // =============================================================================================
 template <int DP>
-__global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int DT = DP / 16;
-  __shared__ __attribute__((aligned(16))) bf16_t sK[64 * Tile<DP>::LD];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[64 * Tile<DP>::LD];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int q0 = blockIdx.x * TQ + wave * 16;
-  const int myq = q0 + (lane & 15);
   const int dt_n = (a.d + 15) / 16;
   const float c = a.scale * LOG2E;
-
   const bf16_t* K = a.k + (long long)b * a.S * a.ldk;
   const bf16_t* V = a.v + (long long)b * a.S * a.ldv;
-  s16x8 qf[DP / 32], of[DP / 32];
-  row_frags<DP>(qf, a.q + (long long)b * a.N * a.ldq, a.ldq, myq, a.N, h * a.d, a.d, lane);
-  row_frags<DP>(of, a.dout + (long long)b * a.N * a.lddo, a.lddo, myq, a.N, h * a.d, a.d, lane);
-  const bool qok = myq < a.N;
-  const float lse = qok ? a.lse[(long long)bh * a.N + myq] : INFINITY;
-  const float dlt = qok ? a.delta[(long long)bh * a.N + myq] : 0.f;
 
-  f32x4 dq[DT];
+  int myq[2];
+  s16x8 qf[2][DP / 32], of[2][DP / 32];
+  float lse[2], dlt[2];
+  f32x4 dq[2][DT];
 #pragma unroll
-  for (int t = 0; t < DT; ++t) dq[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int g = 0; g < 2; ++g) {
+    myq[g] = blockIdx.x * ROWS + wave * 32 + g * 16 + (lane & 15);
+    row_frags<DP>(qf[g], a.q + (long long)b * a.N * a.ldq, a.ldq, myq[g], a.N, h * a.d, a.d, lane);
+    row_frags<DP>(of[g], a.dout + (long long)b * a.N * a.lddo, a.lddo, myq[g], a.N, h * a.d, a.d, lane);
+    const bool ok = myq[g] < a.N;
+    lse[g] = ok ? a.lse[(long long)bh * a.N + myq[g]] : INFINITY;
+    dlt[g] = ok ? a.delta[(long long)bh * a.N + myq[g]] : 0.f;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) dq[g][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 
-  for (int k0 = 0; k0 < a.S; k0 += TK) {
-    __syncthreads();
-    load_tile<DP>(sK, K, a.ldk, k0, a.S, h * a.d, a.d);
-    load_tile<DP>(sV, V, a.ldv, k0, a.S, h * a.d, a.d);
-    __syncthreads();
-    f32x4 ds[4];
+  uint4 rk[Tile<DP>::CPT], rv[Tile<DP>::CPT];
+  tile_fetch<DP>(rk, K, a.ldk, 0, a.S, h * a.d, a.d);
+  tile_fetch<DP>(rv, V, a.ldv, 0, a.S, h * a.d, a.d);
+  tile_store<DP>(smem, rk);
+  tile_store<DP>(smem + Tile<DP>::ELEMS, rv);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = 0; k0 < a.S; k0 += TILE) {
+    const bool more = k0 + TILE < a.S;
+    if (more) {
+      tile_fetch<DP>(rk, K, a.ldk, k0 + TILE, a.S, h * a.d, a.d);
+      tile_fetch<DP>(rv, V, a.ldv, k0 + TILE, a.S, h * a.d, a.d);
+    }
+    const bf16_t* sK = smem + cur * 2 * Tile<DP>::ELEMS;
+    const bf16_t* sV = sK + Tile<DP>::ELEMS;
+    const bool ragged = k0 + TILE > a.S;
+    f32x4 ds[2][4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f}, dp = s;
+      f32x4 s0 = (f32x4){0.f, 0.f, 0.f, 0.f}, s1 = s0, d0 = s0, d1 = s0;
 #pragma unroll
       for (int ks = 0; ks < DP / 32; ++ks) {
-        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<DP>(sK, kb * 16, ks * 32, lane), qf[ks], s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_rows<DP>(sV, kb * 16, ks * 32, lane), of[ks], dp, 0, 0, 0);
+        s16x8 ka = frag_rows<DP>(sK, kb * 16, ks * 32, lane);
+        s16x8 va = frag_rows<DP>(sV, kb * 16, ks * 32, lane);
+        s0 = mfma(ka, qf[0][ks], s0);
+        s1 = mfma(ka, qf[1][ks], s1);
+        d0 = mfma(va, of[0][ks], d0);
+        d1 = mfma(va, of[1][ks], d1);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        int key = k0 + kb * 16 + (lane >> 4) * 4 + i;
-        float pv = key < a.S ? exp2f(s[i] * c - lse) : 0.f;
-        ds[kb][i] = pv * (dp[i] - dlt);
+        const bool kok = !ragged || (k0 + kb * 16 + (lane >> 4) * 4 + i < a.S);
+        float p0 = kok ? exp2f(fmaf(s0[i], c, -lse[0])) : 0.f;
+        float p1 = kok ? exp2f(fmaf(s1[i], c, -lse[1])) : 0.f;
+        ds[0][kb][i] = p0 * (d0[i] - dlt[0]);
+        ds[1][kb][i] = p1 * (d1[i] - dlt[1]);
       }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      s16x8 df = pack_acc(ds[2 * s2], ds[2 * s2 + 1]);
+      s16x8 df0 = pack_acc(ds[0][2 * s2], ds[0][2 * s2 + 1]), df1 = pack_acc(ds[1][2 * s2], ds[1][2 * s2 + 1]);
 #pragma unroll
       for (int t = 0; t < DT; ++t)
-        if (t < dt_n) dq[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tr<DP>(sK, 32 * s2, 16 * t, lane), df, dq[t], 0, 0, 0);
+        if (t < dt_n) {
+          s16x8 kt = frag_tr<DP>(sK, 32 * s2, 16 * t, lane);
+          dq[0][t] = mfma(kt, df0, dq[0][t]);
+          dq[1][t] = mfma(kt, df1, dq[1][t]);
+        }
     }
+    if (more) {
+      bf16_t* nK = smem + (cur ^ 1) * 2 * Tile<DP>::ELEMS;
+      tile_store<DP>(nK, rk);
+      tile_store<DP>(nK + Tile<DP>::ELEMS, rv);
+    }
+    __syncthreads();
+    cur ^= 1;
   }
-  if (qok) {
-    bf16_t* DQ = a.dq + ((long long)b * a.N + myq) * a.lddq + h * a.d;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      int d0 = 16 * t + (lane >> 4) * 4;
-      if (t < dt_n && d0 < a.d) {
-        uint2 w;
-        w.x = pack2bf(dq[t][0] * a.scale, dq[t][1] * a.scale);
-        w.y = pack2bf(dq[t][2] * a.scale, dq[t][3] * a.scale);
-        *(uint2*)(DQ + d0) = w;
+  for (int g = 0; g < 2; ++g)
+    if (myq[g] < a.N) {
+      bf16_t* DQ = a.dq + ((long long)b * a.N + myq[g]) * a.lddq + h * a.d;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        int d0 = 16 * t + (lane >> 4) * 4;
+        if (t < dt_n && d0 < a.d) store4(DQ + d0, dq[g][t], a.scale);
       }
     }
-  }
 }
 
 int check_args(const AttnArgs& a) {
@@ -372,16 +493,15 @@ int check_args(const AttnArgs& a) {
 
 }  // namespace
 
-extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
-                             void* out, int ldo, float* lse, int B, int H, int N, int S, int d,
-                             sdmi_stream_t stream) {
+extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* out, int ldo,
+                             float* lse, int B, int H, int N, int S, int d, sdmi_stream_t stream) {
   AttnArgs a = {};
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.out = (bf16_t*)out; a.lse = lse;
   a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo;
   a.B = B; a.H = H; a.N = N; a.S = S; a.d = d; a.scale = 1.0f / sqrtf((float)d);
   int rc = check_args(a);
   if (rc) return rc;
-  dim3 grid((N + TQ - 1) / TQ, B * H);
+  dim3 grid((N + ROWS - 1) / ROWS, B * H);
   hipStream_t s = (hipStream_t)stream;
   if (d <= 32) hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(NT), 0, s, a);
   else hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(NT), 0, s, a);
@@ -389,10 +509,10 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
   return 0;
 }
 
-extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
-                             const void* o, int ldo, const void* dout, int lddo, const float* lse,
-                             float* delta_ws, void* dq, int lddq, void* dk, int lddk, void* dv, int lddv,
-                             int B, int H, int N, int S, int d, sdmi_stream_t stream) {
+extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, const void* o,
+                             int ldo, const void* dout, int lddo, const float* lse, float* delta_ws, void* dq, int lddq,
+                             void* dk, int lddk, void* dv, int lddv, int B, int H, int N, int S, int d,
+                             sdmi_stream_t stream) {
   AttnArgs a = {};
   a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (const bf16_t*)o;
   a.dout = (const bf16_t*)dout; a.lse = (float*)lse; a.delta = delta_ws;
@@ -405,7 +525,7 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
   long long rows = (long long)B * N * H;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, a);
   SDMI_CHECK_LAUNCH();
-  dim3 gk((S + TK - 1) / TK, B * H), gq((N + TQ - 1) / TQ, B * H);
+  dim3 gk((S + ROWS - 1) / ROWS, B * H), gq((N + ROWS - 1) / ROWS, B * H);
   if (d <= 32) {
     hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, gk, dim3(NT), 0, s, a);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, gq, dim3(NT), 0, s, a);

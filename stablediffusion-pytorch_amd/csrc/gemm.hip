@@ -34,15 +34,22 @@ struct Args {
   // gather geometry
   int ih, iw, cin, ldx, kw, ohl, owl, sy, sx, oy0, ox0;
   int ktiles_per_split, nsplit;
-  // epilogue
+  const bf16_t* A2; int lda2; int k_split;
+};
+
+// epilogue parameters (a separate kernel argument keeps both structs small enough to stay in SGPRs)
+struct EpiArgs {
+  int M, N;
   void* C; int ldc; int c_f32; long long split_stride;
-  const float* bias; const bf16_t* rowbias; int rb_ld, rb_shift;
+  const float* bias; const float* bias2; const bf16_t* rowbias; int rb_ld, rb_shift;
   const bf16_t* resid; int ldr;
   float alpha; int act;
   int remap, r_ghl, r_gwl, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
   int perm, p_cin, p_taps, p_cvalid;
   int m_store, n_store;
   int raw;  // 1: write raw fp32 partials (split-K), epilogue applied by the reducer
+  int nsplit;
+  const float* ws;  // reducer input slabs
 };
 
 __device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
@@ -50,7 +57,30 @@ __device__ __forceinline__ int tr_swz(int r) { return ((r & 3) | ((r >> 1) & 4))
 __device__ __forceinline__ int tr_off(int r, int c) { return r * 256 + ((c ^ tr_swz(r)) << 4); }
 
 struct Epi {
-  __device__ __forceinline__ static void store(const Args& g, int row, int col, float acc, int z) {
+  // v already holds alpha*acc + bias + bias2
+  __device__ __forceinline__ static void finish(const EpiArgs& g, int row, int col, float v) {
+    if (g.rowbias) v += bf2f(g.rowbias[(long long)(row >> g.rb_shift) * g.rb_ld + col]);
+    long long orow = row;
+    if (g.remap) {
+      int b = row >> (g.r_ghl + g.r_gwl);
+      int oy = (row >> g.r_gwl) & ((1 << g.r_ghl) - 1);
+      int ox = row & ((1 << g.r_gwl) - 1);
+      orow = ((long long)b * g.r_oh + oy * g.r_sy + g.r_oy) * g.r_ow + ox * g.r_sx + g.r_ox;
+    }
+    if (g.resid) v += bf2f(g.resid[orow * g.ldr + col]);
+    if (g.act == 1) v = silu_f(v);
+    long long ocol = col;
+    if (g.perm) {
+      int tap = col / g.p_cin;
+      int c = col - tap * g.p_cin;
+      if (c >= g.p_cvalid) return;
+      ocol = (long long)c * g.p_taps + tap;
+    }
+    if (g.c_f32) ((float*)g.C)[orow * g.ldc + ocol] = v;
+    else ((bf16_t*)g.C)[orow * g.ldc + ocol] = f2bf(v);
+  }
+
+  __device__ __forceinline__ static void store(const EpiArgs& g, int row, int col, float acc, int z) {
     if (row >= g.M || col >= g.N) return;
     if (g.raw) {
       ((float*)g.C)[(long long)z * g.split_stride + (long long)row * g.N + col] = acc;
@@ -59,6 +89,7 @@ struct Epi {
     if (row >= g.m_store || col >= g.n_store) return;
     float v = g.alpha * acc;
     if (g.bias) v += g.bias[col];
+    if (g.bias2) v += g.bias2[col];
     if (g.rowbias) v += bf2f(g.rowbias[(long long)(row >> g.rb_shift) * g.rb_ld + col]);
     long long orow = row;
     if (g.remap) {
@@ -82,7 +113,7 @@ struct Epi {
 };
 
 template <int AM, int BMODE>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g) {
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs e) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   // buffer b: A tile at smem + 2*b*TILE_BYTES, B tile right after it
 #define SA(b) (smem + (b) * 2 * TILE_BYTES)
@@ -131,6 +162,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g) {
   // ragged tiles and k >= K are zero-filled without a select on a pointer.
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsA2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.A2 ? g.A2 : g.A), (short)0, 0x7fffffff, 0x00020000);
   constexpr int OOB = (int)0x80000000;
 #define BUF_LD(rs, off) __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128((rs), (off), 0, 0))
 
@@ -147,17 +180,27 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g) {
       }
     } else if (AM == SDMI_A_CONV) {
       int k = k0 + (tid & 7) * 8;
-      int tap = k / g.cin;
-      int ci = k - tap * g.cin;
-      int ty = tap / g.kw;
-      int tx = tap - ty * g.kw;
-      bool kok = k < g.K;
+      if (k >= g.k_split) {  // K-concatenated second source: plain row-major rows (fused 1x1 conv)
+        int kk = k - g.k_split;
+        bool kok = k < g.K;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int iy = a_iy[i] + ty, ix = a_ix[i] + tx;
-        bool ok = kok && a_ok[i] && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
-        int off = ok ? (((a_pb[i] + iy) * g.iw + ix) * g.ldx + ci) * 2 : OOB;
-        ra[i] = BUF_LD(rsA, off);
+        for (int i = 0; i < 4; ++i) {
+          int m = m0 + (tid >> 3) + 32 * i;
+          int off = (kok && a_ok[i]) ? (m * g.lda2 + kk) * 2 : OOB;
+          ra[i] = BUF_LD(rsA2, off);
+        }
+      } else {
+        int tap = k / g.cin;
+        int ci = k - tap * g.cin;
+        int ty = tap / g.kw;
+        int tx = tap - ty * g.kw;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int iy = a_iy[i] + ty, ix = a_ix[i] + tx;
+          bool ok = a_ok[i] && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
+          int off = ok ? (((a_pb[i] + iy) * g.iw + ix) * g.ldx + ci) * 2 : OOB;
+          ra[i] = BUF_LD(rsA, off);
+        }
       }
     } else {  // col-major A: A[k*lda + m]
       int m = m0 + (tid & 15) * 8;
@@ -275,25 +318,50 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g) {
   }
 
   // ---------------- epilogue ----------------
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
+  if (e.raw) {  // split-K slab: raw fp32 partials, the reducer applies the epilogue
+    float* slab = (float*)e.C + (long long)z * e.split_stride;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      int col = n0 + wn + 16 * j + (lane & 15);
+      const int col = n0 + wn + 16 * j + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
-        Epi::store(g, row, col, acc[i][j][r], z);
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 v = acc[i][j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+          if (row < e.M && col < e.N) slab[(long long)row * e.N + col] = v[r];
+        }
       }
     }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn + 16 * j + (lane & 15);
+      const bool cok = col < e.n_store;
+      float bsum = 0.f;
+      if (cok) {
+        if (e.bias) bsum += e.bias[col];
+        if (e.bias2) bsum += e.bias2[col];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 v = acc[i][j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+          if (cok && row < e.m_store) Epi::finish(e, row, col, e.alpha * v[r] + bsum);
+        }
+      }
+    }
+  }
 }
 
 // Sum split-K slabs and apply the epilogue.
-__global__ void splitk_reduce_kernel(Args g) {
+__global__ void splitk_reduce_kernel(const EpiArgs g) {
   long long total = (long long)g.M * g.N;
   long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long stride = (long long)gridDim.x * blockDim.x;
-  const float* ws = (const float*)g.A;  // the launcher passes the slab workspace through A
+  const float* ws = g.ws;
   for (; idx < total; idx += stride) {
     float s = 0.f;
     for (int zz = 0; zz < g.nsplit; ++zz) s += ws[(long long)zz * g.split_stride + idx];
@@ -303,12 +371,12 @@ __global__ void splitk_reduce_kernel(Args g) {
 }
 
 template <int AM, int BMODE>
-hipError_t launch_t(const Args& a, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a);
+hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
   return hipGetLastError();
 }
 
-int fill_args(const sdmi_gemm_desc* d, Args& a) {
+int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   if (!d || d->m <= 0 || d->n <= 0 || d->k <= 0) return -1;
   // K is the contiguous (16-B chunked) dimension of row-major / conv A and of [n][k] B only
   if ((d->a_mode != SDMI_A_COLMAJOR || d->b_mode == SDMI_B_NK) && (d->k % 8)) return -2;
@@ -318,23 +386,29 @@ int fill_args(const sdmi_gemm_desc* d, Args& a) {
     const sdmi_conv_geom& q = d->geom;
     if (q.cin <= 0 || q.cin % 8 || q.kw <= 0 || q.ldx % 8) return -5;
   }
+  if (d->a2 && (d->k_split % 8 || d->lda2 % 8)) return -7;
   memset(&a, 0, sizeof(a));
+  memset(&e, 0, sizeof(e));
   a.M = d->m; a.N = d->n; a.K = d->k;
   a.A = (const bf16_t*)d->a; a.lda = d->lda;
   a.B = (const bf16_t*)d->b; a.ldb = d->ldb;
   a.ih = d->geom.ih; a.iw = d->geom.iw; a.cin = d->geom.cin; a.ldx = d->geom.ldx; a.kw = d->geom.kw;
   a.ohl = d->geom.oh_log2; a.owl = d->geom.ow_log2;
   a.sy = d->geom.sy; a.sx = d->geom.sx; a.oy0 = d->geom.oy0; a.ox0 = d->geom.ox0;
-  a.C = d->c; a.ldc = d->ldc; a.c_f32 = d->c_f32;
-  a.bias = d->bias; a.rowbias = (const bf16_t*)d->rowbias; a.rb_ld = d->rb_ld; a.rb_shift = d->rb_shift;
-  a.resid = (const bf16_t*)d->resid; a.ldr = d->ldr;
-  a.alpha = d->alpha; a.act = d->act;
-  a.remap = d->remap; a.r_ghl = d->r_gh_log2; a.r_gwl = d->r_gw_log2; a.r_oh = d->r_oh; a.r_ow = d->r_ow;
-  a.r_sy = d->r_sy; a.r_sx = d->r_sx; a.r_oy = d->r_oy; a.r_ox = d->r_ox;
-  a.perm = d->perm; a.p_cin = d->p_cin; a.p_taps = d->p_taps;
-  a.p_cvalid = d->p_cvalid > 0 ? d->p_cvalid : d->p_cin;
-  a.m_store = d->m_store > 0 ? d->m_store : d->m;
-  a.n_store = d->n_store > 0 ? d->n_store : d->n;
+  a.A2 = (const bf16_t*)d->a2; a.lda2 = d->lda2;
+  a.k_split = (d->a_mode == SDMI_A_CONV && d->a2) ? d->k_split : d->k;
+  e.M = d->m; e.N = d->n;
+  e.C = d->c; e.ldc = d->ldc; e.c_f32 = d->c_f32;
+  e.bias = d->bias; e.bias2 = d->bias2;
+  e.rowbias = (const bf16_t*)d->rowbias; e.rb_ld = d->rb_ld; e.rb_shift = d->rb_shift;
+  e.resid = (const bf16_t*)d->resid; e.ldr = d->ldr;
+  e.alpha = d->alpha; e.act = d->act;
+  e.remap = d->remap; e.r_ghl = d->r_gh_log2; e.r_gwl = d->r_gw_log2; e.r_oh = d->r_oh; e.r_ow = d->r_ow;
+  e.r_sy = d->r_sy; e.r_sx = d->r_sx; e.r_oy = d->r_oy; e.r_ox = d->r_ox;
+  e.perm = d->perm; e.p_cin = d->p_cin; e.p_taps = d->p_taps;
+  e.p_cvalid = d->p_cvalid > 0 ? d->p_cvalid : d->p_cin;
+  e.m_store = d->m_store > 0 ? d->m_store : d->m;
+  e.n_store = d->n_store > 0 ? d->n_store : d->n;
   return 0;
 }
 
@@ -351,7 +425,8 @@ int plan_splits(const sdmi_gemm_desc* d) {
 
 extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) {
   Args a;
-  int rc = fill_args(d, a);
+  EpiArgs e;
+  int rc = fill_args(d, a, e);
   if (rc) return rc;
   int s = plan_splits(d);
   if (splits) *splits = s;
@@ -361,7 +436,8 @@ extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) 
 
 extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_bytes, sdmi_stream_t stream) {
   Args a;
-  int rc = fill_args(d, a);
+  EpiArgs e;
+  int rc = fill_args(d, a, e);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   int splits = plan_splits(d);
@@ -370,36 +446,35 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
   a.ktiles_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + a.ktiles_per_split - 1) / a.ktiles_per_split;
   a.nsplit = splits;
-  Args run = a;
+  EpiArgs run = e;
   if (splits > 1) {
     run.raw = 1;
     run.C = workspace;
     run.split_stride = (long long)d->m * d->n;
   }
   dim3 grid((d->n + BN - 1) / BN, (d->m + BM - 1) / BM, splits);
-  hipError_t e;
+  hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
   switch (key) {
-    case SDMI_A_ROWMAJOR * 3 + SDMI_B_NK: e = launch_t<SDMI_A_ROWMAJOR, SDMI_B_NK>(run, grid, s); break;
-    case SDMI_A_ROWMAJOR * 3 + SDMI_B_KN: e = launch_t<SDMI_A_ROWMAJOR, SDMI_B_KN>(run, grid, s); break;
-    case SDMI_A_CONV * 3 + SDMI_B_NK: e = launch_t<SDMI_A_CONV, SDMI_B_NK>(run, grid, s); break;
-    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN: e = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN>(run, grid, s); break;
-    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN_CONV: e = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN_CONV>(run, grid, s); break;
+    case SDMI_A_ROWMAJOR * 3 + SDMI_B_NK: err = launch_t<SDMI_A_ROWMAJOR, SDMI_B_NK>(a, run, grid, s); break;
+    case SDMI_A_ROWMAJOR * 3 + SDMI_B_KN: err = launch_t<SDMI_A_ROWMAJOR, SDMI_B_KN>(a, run, grid, s); break;
+    case SDMI_A_CONV * 3 + SDMI_B_NK: err = launch_t<SDMI_A_CONV, SDMI_B_NK>(a, run, grid, s); break;
+    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN: err = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN>(a, run, grid, s); break;
+    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN_CONV: err = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN_CONV>(a, run, grid, s); break;
     default: return -6;
   }
-  if (e != hipSuccess) return (int)e;
+  if (err != hipSuccess) return (int)err;
   if (splits > 1) {
-    Args red = a;
+    EpiArgs red = e;
     red.raw = 0;
-    // reducer reads slabs from workspace and writes the real output
+    red.nsplit = splits;
     red.split_stride = (long long)d->m * d->n;
+    red.ws = (const float*)workspace;
     long long total = (long long)d->m * d->n;
     int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-    // pass the workspace through A (unused by the reducer)
-    red.A = (const bf16_t*)workspace;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, red);
-    e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
+    err = hipGetLastError();
+    if (err != hipSuccess) return (int)err;
   }
   return 0;
 }

@@ -223,7 +223,9 @@ __global__ void pack_kernel(const sdmi_pack_desc* descs, const int2* bmap) {
       int kh = d.kh_off + d.kh_mul * a, kw = d.kw_off + d.kw_mul * b;
       v = d.src[o * d.so + i * d.si + kh * d.skh + kw * d.skw];
     }
-    ((bf16_t*)d.dst)[r] = f2bf(v);
+    long long dr = d.dst_ld ? (r / ((long long)d.KH * d.KW * d.Ipad)) * d.dst_ld + r % ((long long)d.KH * d.KW * d.Ipad)
+                            : r;
+    ((bf16_t*)d.dst)[dr] = f2bf(v);
   }
 }
 }  // namespace

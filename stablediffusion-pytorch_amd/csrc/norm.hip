@@ -21,7 +21,7 @@ constexpr int NT = 256;
 struct RedArgs {
   const bf16_t* x; int ldx;   // GN input
   const bf16_t* dy; int ldy;  // upstream grad (modes 1, 2)
-  const float* mean; const float* rstd; const float* gamma; const float* beta;
+  const float4* tab;          // mode 1: per-(b,c) {a = rstd*gamma, s = beta - mean*a, mean, rstd}
   int B, P, C, G, silu, mode, splits;
   float* part;  // [B][splits][C][2]
 };
@@ -41,17 +41,12 @@ __global__ __launch_bounds__(NT) void chan_reduce_kernel(RedArgs a) {
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-  float mu[8], rs[8], ga[8], be[8];
+  float4 tb[8];
   if (a.mode == 1) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      int g = (c0 + e) / Cg;
-      mu[e] = a.mean[b * a.G + g];
-      rs[e] = a.rstd[b * a.G + g];
-      ga[e] = a.gamma[c0 + e];
-      be[e] = a.beta[c0 + e];
-    }
+    for (int e = 0; e < 8; ++e) tb[e] = a.tab[(long long)b * a.C + c0 + e];
   }
+  (void)Cg;
   if (active) {
     for (int p = p0 + r; p < p1; p += rows) {
       long long pix = (long long)b * a.P + p;
@@ -65,9 +60,9 @@ __global__ __launch_bounds__(NT) void chan_reduce_kernel(RedArgs a) {
         unpack8(*(const uint4*)(a.dy + pix * a.ldy + c0), gv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float xh = (xv[e] - mu[e]) * rs[e];
+          float xh = (xv[e] - tb[e].z) * tb[e].w;
           float dz = gv[e];
-          if (a.silu) dz *= silu_grad_f(xh * ga[e] + be[e]);
+          if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb[e].x, tb[e].y));
           s1[e] += dz;
           s2[e] += dz * xh;
         }
@@ -144,8 +139,10 @@ __device__ __forceinline__ void batch_totals(const float* part, int b, int split
 
 // mean/rstd per (b, g): one block per b
 __global__ __launch_bounds__(256) void gn_stats_finalize_kernel(const float* part, int B, int splits, int C, int G,
-                                                                int P, float eps, float* mean, float* rstd) {
+                                                                int P, float eps, const float* gamma,
+                                                                const float* beta, float4* tab) {
   __shared__ float2 tot[2048];
+  __shared__ float2 grp[2048];
   const int b = blockIdx.x;
   batch_totals(part, b, splits, C, tot);
   const int Cg = C / G;
@@ -159,29 +156,44 @@ __global__ __launch_bounds__(256) void gn_stats_finalize_kernel(const float* par
     double mu = s1 / n;
     double var = s2 / n - mu * mu;
     if (var < 0) var = 0;
-    mean[b * G + g] = (float)mu;
-    rstd[b * G + g] = (float)(1.0 / sqrt(var + (double)eps));
+    grp[g] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)eps)));
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float2 mr = grp[c / Cg];
+    float a = mr.y * gamma[c];
+    tab[(long long)b * C + c] = make_float4(a, beta[c] - mr.x * a, mr.x, mr.y);
   }
 }
 
 // GN backward: blocks [0, B): coef[b][g] = (sum_c gamma_c S1[b,c], sum_c gamma_c S2[b,c]);
 // blocks [B, B + ceil(C/64)): dbeta[c] = sum_b S1, dgamma[c] = sum_b S2.
+// dx = rstd*(dz*gamma - A/n - xhat*Bc/n) = a*dz + q*x + o with q = -rstd^2 Bc/n, o = rstd^2 mean Bc/n - rstd A/n
 __global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(const float* part, int B, int splits, int C, int G,
-                                                              const float* gamma, float* coef, float* dgamma,
-                                                              float* dbeta) {
+                                                              int P, const float* gamma, const float4* tab,
+                                                              float4* tab2, float* dgamma, float* dbeta) {
   if ((int)blockIdx.x < B) {
     __shared__ float2 tot[2048];
+    __shared__ float2 grp[2048];
     const int b = blockIdx.x;
     batch_totals(part, b, splits, C, tot);
     const int Cg = C / G;
+    const float inv_n = 1.0f / ((float)P * Cg);
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
       float A = 0.f, Bc = 0.f;
       for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
         A += gamma[c] * tot[c].x;
         Bc += gamma[c] * tot[c].y;
       }
-      coef[(b * G + g) * 2] = A;
-      coef[(b * G + g) * 2 + 1] = Bc;
+      float4 t = tab[(long long)b * C + g * Cg];
+      float r = t.w, mu = t.z;
+      grp[g] = make_float2(-r * r * Bc * inv_n, r * r * mu * Bc * inv_n - r * A * inv_n);
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float4 t = tab[(long long)b * C + c];
+      float2 qo = grp[c / Cg];
+      tab2[(long long)b * C + c] = make_float4(t.x, t.y, qo.x, qo.y);
     }
     return;
   }
@@ -226,41 +238,41 @@ struct ApplyArgs {
   bf16_t* y; int ldy;
   const bf16_t* dy; int lddy;
   bf16_t* dx; int lddx;
-  const float* mean; const float* rstd; const float* gamma; const float* beta; const float* coef;
+  const float4* tab;  // apply: {a, s, -, -}; backward: {a, s, q, o}
   const bf16_t* add; int ldadd;
-  int B, P, C, G, silu;
+  int B, P, C, silu;
 };
 
+// y = act(x*a + s)
 __global__ __launch_bounds__(NT) void gn_apply_kernel(ApplyArgs a) {
   const int C8 = a.C >> 3;
   long long total = (long long)a.B * a.P * C8;
-  const int Cg = a.C / a.G;
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
     long long pix = i / C8;
     int c0 = (int)(i - pix * C8) * 8;
     int b = (int)(pix / a.P);
+    const float4* t = a.tab + (long long)b * a.C + c0;
     float xv[8], yv[8];
     unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      int g = (c0 + e) / Cg;
-      float z = (xv[e] - a.mean[b * a.G + g]) * a.rstd[b * a.G + g] * a.gamma[c0 + e] + a.beta[c0 + e];
+      float4 te = t[e];
+      float z = fmaf(xv[e], te.x, te.y);
       yv[e] = a.silu ? silu_f(z) : z;
     }
     *(uint4*)(a.y + pix * a.ldy + c0) = pack8(yv);
   }
 }
 
-// dx = rstd * (dz*gamma - A/n - xhat*Bc/n)
+// dx = a*dz + q*x + o (+ addend), dz = dy [* silu'(x*a + s)]
 __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
   const int C8 = a.C >> 3;
   long long total = (long long)a.B * a.P * C8;
-  const int Cg = a.C / a.G;
-  const float inv_n = 1.0f / ((float)a.P * Cg);
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
     long long pix = i / C8;
     int c0 = (int)(i - pix * C8) * 8;
     int b = (int)(pix / a.P);
+    const float4* t = a.tab + (long long)b * a.C + c0;
     float xv[8], gv[8], ov[8], av[8];
     unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
     unpack8(*(const uint4*)(a.dy + pix * a.lddy + c0), gv);
@@ -268,13 +280,10 @@ __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
     else for (int e = 0; e < 8; ++e) av[e] = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      int g = (c0 + e) / Cg;
-      int bg = b * a.G + g;
-      float rs = a.rstd[bg];
-      float xh = (xv[e] - a.mean[bg]) * rs;
+      float4 te = t[e];
       float dz = gv[e];
-      if (a.silu) dz *= silu_grad_f(xh * a.gamma[c0 + e] + a.beta[c0 + e]);
-      ov[e] = av[e] + rs * (dz * a.gamma[c0 + e] - a.coef[bg * 2] * inv_n - xh * a.coef[bg * 2 + 1] * inv_n);
+      if (a.silu) dz *= silu_grad_f(fmaf(xv[e], te.x, te.y));
+      ov[e] = av[e] + fmaf(te.x, dz, fmaf(te.z, xv[e], te.w));
     }
     *(uint4*)(a.dx + pix * a.lddx + c0) = pack8(ov);
   }
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
 
 int pick_splits(int B, int P) {
   int s = 1;
-  while (B * s < 256 && P / (s * 2) >= 32) s *= 2;
+  while (B * s < 1024 && P / (s * 2) >= 16) s *= 2;
   return s;
 }
 
@@ -297,8 +306,9 @@ extern "C" size_t sdmi_chan_reduce_workspace(int B, int P, int C) {
   return (size_t)B * pick_splits(B, P) * C * 2 * sizeof(float);
 }
 
-extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, float* ws, float* mean,
-                             float* rstd, sdmi_stream_t stream) {
+// stats -> per-(b,c) table {a = rstd*gamma, s = beta - mean*a, mean, rstd} (fp32 float4 [B][C])
+extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, const float* gamma,
+                             const float* beta, float* ws, float* table, sdmi_stream_t stream) {
   if (C % 8 || C > 8 * NT || G <= 0 || C % G) return -1;
   hipStream_t s = (hipStream_t)stream;
   RedArgs a = {};
@@ -306,43 +316,41 @@ extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G,
   a.splits = pick_splits(B, P); a.part = ws;
   hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, a.splits), dim3(NT), 0, s, a);
   SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(B), dim3(256), 0, s, ws, B, a.splits, C, G, P, eps, mean, rstd);
+  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(B), dim3(256), 0, s, ws, B, a.splits, C, G, P, eps, gamma, beta,
+                     (float4*)table);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* mean, const float* rstd,
-                             const float* gamma, const float* beta, int B, int P, int C, int G, int silu,
-                             sdmi_stream_t stream) {
-  if (C % 8 || C % G) return -1;
+extern "C" int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* table, int B, int P, int C,
+                             int silu, sdmi_stream_t stream) {
+  if (C % 8) return -1;
   ApplyArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.y = (bf16_t*)y; a.ldy = ldy;
-  a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.B = B; a.P = P; a.C = C; a.G = G; a.silu = silu;
+  a.tab = (const float4*)table; a.B = B; a.P = P; a.C = C; a.silu = silu;
   hipLaunchKernelGGL(gn_apply_kernel, dim3(grid_for((long long)B * P * C / 8)), dim3(NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* mean,
-                           const float* rstd, const float* gamma, const float* beta, int B, int P, int C, int G,
-                           int silu, float* ws, float* coef_ws, float* dgamma, float* dbeta, const void* addend,
-                           int ldadd, sdmi_stream_t stream) {
+// table: forward table from sdmi_gn_stats; table2_ws: float4 [B][C] scratch
+extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                           const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws,
+                           float* dgamma, float* dbeta, const void* addend, int ldadd, sdmi_stream_t stream) {
   if (C % 8 || C > 8 * NT || C % G) return -1;
   hipStream_t s = (hipStream_t)stream;
   RedArgs r = {};
-  r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy;
-  r.mean = mean; r.rstd = rstd; r.gamma = gamma; r.beta = beta;
+  r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy; r.tab = (const float4*)table;
   r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.mode = 1; r.splits = pick_splits(B, P); r.part = ws;
   hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, r.splits), dim3(NT), 0, s, r);
   SDMI_CHECK_LAUNCH();
   hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(B + (dgamma ? (C + 63) / 64 : 0)), dim3(256), 0, s, ws, B, r.splits,
-                     C, G, gamma, coef_ws, dgamma, dbeta);
+                     C, G, P, gamma, (const float4*)table, (float4*)table2_ws, dgamma, dbeta);
   SDMI_CHECK_LAUNCH();
   ApplyArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.dy = (const bf16_t*)dy; a.lddy = lddy; a.dx = (bf16_t*)dx; a.lddx = lddx;
-  a.mean = mean; a.rstd = rstd; a.gamma = gamma; a.beta = beta; a.coef = coef_ws;
-  a.add = (const bf16_t*)addend; a.ldadd = ldadd;
-  a.B = B; a.P = P; a.C = C; a.G = G; a.silu = silu;
+  a.tab = (const float4*)table2_ws; a.add = (const bf16_t*)addend; a.ldadd = ldadd;
+  a.B = B; a.P = P; a.C = C; a.silu = silu;
   hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3(grid_for((long long)B * P * C / 8)), dim3(NT), 0, s, a);
   SDMI_CHECK_LAUNCH();
   return 0;

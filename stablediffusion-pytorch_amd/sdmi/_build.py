@@ -35,16 +35,28 @@ def build(force=False, verbose=False):
     for src in sources():
         obj = os.path.join("/tmp", "sdmi_" + os.path.basename(src) + f".{os.getpid()}.o")
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
-               "-I", os.path.join(REPO, "include")]
+               "-I", os.path.join(REPO, "include"), "-Rpass-analysis=kernel-resource-usage"]
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), src, cmd))
         objs.append(obj)
+    spills = []
     for p, src, cmd in procs:
         out, _ = p.communicate()
+        txt = out.decode(errors="replace")
         if p.returncode != 0:
-            sys.stderr.write(out.decode())
+            sys.stderr.write(txt)
             raise RuntimeError(f"hipcc failed on {src}")
-        if verbose and out:
-            sys.stderr.write(out.decode())
+        fn = None
+        for line in txt.splitlines():  # guard: no kernel may spill to scratch (silent 3x slowdowns)
+            if "Function Name:" in line:
+                fn = line.split("Function Name:")[1].split("[")[0].strip()
+            elif "ScratchSize [bytes/lane]:" in line:
+                n = int(line.split("ScratchSize [bytes/lane]:")[1].split("[")[0])
+                if n > 0:
+                    spills.append((os.path.basename(src), fn, n))
+        if verbose:
+            sys.stderr.write("\n".join(l for l in txt.splitlines() if "remark" not in l))
+    if spills:
+        raise RuntimeError(f"kernels use scratch memory (register spill / dynamic indexing): {spills}")
     tmp = LIB + f".tmp{os.getpid()}"
     subprocess.check_call(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
     os.replace(tmp, LIB)

@@ -36,6 +36,8 @@ class GemmDesc(ctypes.Structure):
         ("r_oy", ctypes.c_int), ("r_ox", ctypes.c_int),
         ("perm", ctypes.c_int), ("p_cin", ctypes.c_int), ("p_taps", ctypes.c_int), ("p_cvalid", ctypes.c_int),
         ("m_store", ctypes.c_int), ("n_store", ctypes.c_int),
+        ("a2", ctypes.c_void_p), ("lda2", ctypes.c_int), ("k_split", ctypes.c_int),
+        ("bias2", ctypes.c_void_p),
     ]
 
 
@@ -50,7 +52,8 @@ class PackDesc(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p),
                 ("so", ctypes.c_longlong), ("si", ctypes.c_longlong), ("skh", ctypes.c_longlong),
                 ("skw", ctypes.c_longlong)] + [(n, ctypes.c_int) for n in
-                                                ("O", "I", "Ipad", "KH", "KW", "kh_off", "kh_mul", "kw_off", "kw_mul")]
+                                                ("O", "I", "Ipad", "KH", "KW", "kh_off", "kh_mul", "kw_off", "kw_mul",
+                                                 "dst_ld")]
 
 
 SIGNATURES = {
@@ -60,9 +63,9 @@ SIGNATURES = {
     "sdmi_attn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I,
                        _I, _I, _I, _I, _I, _P], _I),
     "sdmi_chan_reduce_workspace": ([_I, _I, _I], _SZ),
-    "sdmi_gn_stats": ([_P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P], _I),
-    "sdmi_gn_apply": ([_P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P], _I),
-    "sdmi_gn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P], _I),
+    "sdmi_gn_stats": ([_P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
+    "sdmi_gn_apply": ([_P, _I, _P, _I, _P, _I, _I, _I, _I, _P], _I),
+    "sdmi_gn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P], _I),
     "sdmi_chan_sum": ([_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _I, _P], _I),
     "sdmi_prep_input": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),
     "sdmi_cond_wgrad": ([_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P], _I),

@@ -27,12 +27,32 @@ def _log2(v):
     return l
 
 
-# optional per-launch timing hook (bench.py): list of (tag, flops, start_event, end_event)
+# optional per-launch timing hook (bench.py): list of (tag, flops, start_event, end_event, info)
 PROFILE = None
 
 
+class _Prof:
+    """Context manager recording HIP events around a launch group when PROFILE is enabled."""
+
+    def __init__(self, tag, flops, info=""):
+        self.tag, self.flops, self.info = tag, flops, info
+
+    def __enter__(self):
+        if PROFILE is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e1 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *a):
+        if PROFILE is not None:
+            self.e1.record()
+            PROFILE.append((self.tag, self.flops, self.e0, self.e1, self.info))
+
+
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
-         rb_ld=0, rb_shift=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0):
+         rb_ld=0, rb_shift=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0,
+         a2=None, lda2=0, k_split=0, bias2=None):
     """C[m][n] = epi(sum_k A[m][k] B[k][n]).  a/b/c/resid/rowbias are tensors (pointer = data_ptr,
     offsets already applied by slicing); see include/sdmi.h for the operand modes."""
     L = _lib.lib()
@@ -61,21 +81,18 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
         d.p_cin, d.p_taps = perm[0], perm[1]
         d.p_cvalid = perm[2] if len(perm) > 2 else 0
     d.m_store, d.n_store = m_store, n_store
+    if a2 is not None:
+        d.a2, d.lda2, d.k_split = a2.data_ptr(), lda2, k_split
+    d.bias2 = bias2.data_ptr() if bias2 is not None else None
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
     ws = None
     if ws_bytes.value:
         ws = torch.empty(ws_bytes.value // 4, dtype=torch.float32, device=c.device)
-    if PROFILE is not None:
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record()
-    check(L.sdmi_gemm(ctypes.byref(d), ws.data_ptr() if ws is not None else None, ws_bytes.value, _stream()),
-          "sdmi_gemm")
-    if PROFILE is not None:
-        ev1.record()
-        PROFILE.append((f"gemm_a{a_mode}b{b_mode}", 2.0 * m * n * k, ev0, ev1, splits.value))
+    with _Prof(f"gemm_a{a_mode}b{b_mode}", 2.0 * m * n * k, f"M={m} N={n} K={k} splits={splits.value}"):
+        check(L.sdmi_gemm(ctypes.byref(d), ws.data_ptr() if ws is not None else None, ws_bytes.value, _stream()),
+              "sdmi_gemm")
     return c
 
 
@@ -89,16 +106,20 @@ def conv_geom(ih, iw, cin, ldx, kh, kw, oh, ow, sy, sx, oy0, ox0):
 
 
 def conv_fwd(x, B, H, W, cin, ldx, wpk, cout, kh, kw, stride, pad, out, ldo, *, bias=None, rowbias=None,
-             rb_ld=0, resid=None, ldr=0, act=0, n_store=0):
+             rb_ld=0, resid=None, ldr=0, act=0, n_store=0, x2=None, cin2=0, bias2=None, ldw=0):
     """y[b,oy,ox,co] = sum_{ty,tx,ci} x[b, oy*s+ty-pad, ox*s+tx-pad, ci] * wpk[co, (ty*kw+tx)*cin + ci].
     x: NHWC bf16 buffer (row stride ldx), wpk: bf16 [cout][kh*kw*cin]."""
     OH = (H + 2 * pad - kh) // stride + 1
     OW = (W + 2 * pad - kw) // stride + 1
     g = conv_geom(H, W, cin, ldx, kh, kw, OH, OW, stride, stride, -pad, -pad)
     rb_shift = _log2(OH * OW)
-    return gemm(B * OH * OW, cout, kh * kw * cin, x, _lib.A_CONV, 0, wpk, _lib.B_NK, kh * kw * cin, out, ldo,
+    K1 = kh * kw * cin
+    if x2 is not None:  # fused 1x1 conv of x2 (same pixel grid) by K-concatenation: wpk = [W | W2]
+        assert stride == 1 and OH == H and OW == W
+    return gemm(B * OH * OW, cout, K1 + cin2, x, _lib.A_CONV, 0, wpk, _lib.B_NK, ldw or (K1 + cin2), out, ldo,
                 geom=g, bias=bias, rowbias=rowbias, rb_ld=(rb_ld or cout) if rowbias is not None else 0,
-                rb_shift=rb_shift, resid=resid, ldr=ldr, act=act, n_store=n_store)
+                rb_shift=rb_shift, resid=resid, ldr=ldr, act=act, n_store=n_store,
+                a2=x2, lda2=ld_of(x2) if x2 is not None else 0, k_split=K1, bias2=bias2)
 
 
 def conv_wgrad(dy, ldy, x, B, H, W, cin, ldx, cout, kh, kw, stride, pad, out, OH, OW, *, perm=True, cvalid=0,
@@ -154,7 +175,7 @@ def linear_dgrad(dy, w, out, *, resid=None):
     """out[m][k] = sum_n dy[m][n] w[n][k] (+ resid);  w [N,K] bf16 used as B[k=n][n=k] (row-major)."""
     M, N = dy.shape
     K = w.shape[1]
-    return gemm(M, K, N, dy, _lib.A_ROWMAJOR, ld_of(dy), w, _lib.B_KN, K, out, ld_of(out), resid=resid,
+    return gemm(M, K, N, dy, _lib.A_ROWMAJOR, ld_of(dy), w, _lib.B_KN, w.stride(0), out, ld_of(out), resid=resid,
                 ldr=ld_of(resid) if resid is not None else 0)
 
 
@@ -165,28 +186,32 @@ def linear_wgrad(dy, x, out):
     return gemm(N, K, M, dy, _lib.A_COLMAJOR, ld_of(dy), x, _lib.B_KN, ld_of(x), out, out.stride(0))
 
 
-def gn_stats(x, B, P, C, G, eps=1e-5):
+def gn_stats(x, B, P, C, G, gamma, beta, eps=1e-5):
+    """GroupNorm statistics -> per-(b,c) table {rstd*gamma, beta - mean*rstd*gamma, mean, rstd} fp32 [B*C*4]."""
     L = _lib.lib()
     ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=x.device)
-    mean = torch.empty(B * G, dtype=torch.float32, device=x.device)
-    rstd = torch.empty_like(mean)
-    check(L.sdmi_gn_stats(_p(x), ld_of(x), B, P, C, G, eps, _p(ws), _p(mean), _p(rstd), _stream()), "sdmi_gn_stats")
-    return mean, rstd
+    tab = torch.empty(B * C * 4, dtype=torch.float32, device=x.device)
+    with _Prof("gn_stats", 0, f"B={B} P={P} C={C}"):
+        check(L.sdmi_gn_stats(_p(x), ld_of(x), B, P, C, G, eps, _p(gamma), _p(beta), _p(ws), _p(tab), _stream()),
+              "sdmi_gn_stats")
+    return tab
 
 
-def gn_apply(x, mean, rstd, gamma, beta, B, P, C, G, silu, out):
-    check(_lib.lib().sdmi_gn_apply(_p(x), ld_of(x), _p(out), ld_of(out), _p(mean), _p(rstd), _p(gamma), _p(beta),
-                                   B, P, C, G, 1 if silu else 0, _stream()), "sdmi_gn_apply")
+def gn_apply(x, tab, B, P, C, silu, out):
+    with _Prof("gn_apply", 0, f"B={B} P={P} C={C}"):
+        check(_lib.lib().sdmi_gn_apply(_p(x), ld_of(x), _p(out), ld_of(out), _p(tab), B, P, C, 1 if silu else 0,
+                                       _stream()), "sdmi_gn_apply")
     return out
 
 
-def gn_bwd(x, dy, dx, mean, rstd, gamma, beta, B, P, C, G, silu, dgamma, dbeta, addend=None):
+def gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, silu, dgamma, dbeta, addend=None):
     L = _lib.lib()
     ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=x.device)
-    coef = torch.empty(B * G * 2, dtype=torch.float32, device=x.device)
-    check(L.sdmi_gn_bwd(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(mean), _p(rstd), _p(gamma),
-                        _p(beta), B, P, C, G, 1 if silu else 0, _p(ws), _p(coef), _p(dgamma), _p(dbeta),
-                        _p(addend), ld_of(addend) if addend is not None else 0, _stream()), "sdmi_gn_bwd")
+    tab2 = torch.empty(B * C * 4, dtype=torch.float32, device=x.device)
+    with _Prof("gn_bwd", 0, f"B={B} P={P} C={C}"):
+        check(L.sdmi_gn_bwd(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma), B, P, C, G,
+                            1 if silu else 0, _p(ws), _p(tab2), _p(dgamma), _p(dbeta), _p(addend),
+                            ld_of(addend) if addend is not None else 0, _stream()), "sdmi_gn_bwd")
     return dx
 
 
@@ -202,20 +227,23 @@ def chan_sum(dy, B, P, C, *, per_bc=None, per_c=None, per_c2=None, c_store=0):
         return
     L = _lib.lib()
     ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=dy.device)
-    check(L.sdmi_chan_sum(_p(dy), ld_of(dy), B, P, C, _p(ws), _p(per_bc), ld_of(per_bc) if per_bc is not None else 0,
+    with _Prof("chan_sum", 0, f"B={B} P={P} C={C}"):
+      check(L.sdmi_chan_sum(_p(dy), ld_of(dy), B, P, C, _p(ws), _p(per_bc), ld_of(per_bc) if per_bc is not None else 0,
                           _p(per_c), _p(per_c2), c_store, _stream()), "sdmi_chan_sum")
 
 
 def attn_fwd(q, k, v, out, B, H, N, S, d):
     lse = torch.empty(B * H * N, dtype=torch.float32, device=q.device)
-    check(_lib.lib().sdmi_attn_fwd(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(out), ld_of(out), _p(lse),
+    with _Prof("attn_fwd", 4.0 * B * H * N * S * d, f"B={B} H={H} N={N} S={S} d={d}"):
+      check(_lib.lib().sdmi_attn_fwd(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(out), ld_of(out), _p(lse),
                                    B, H, N, S, d, _stream()), "sdmi_attn_fwd")
     return lse
 
 
 def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, B, H, N, S, d):
     delta = torch.empty(B * H * N, dtype=torch.float32, device=q.device)
-    check(_lib.lib().sdmi_attn_bwd(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(o), ld_of(o), _p(dout),
+    with _Prof("attn_bwd", 10.0 * B * H * N * S * d, f"B={B} H={H} N={N} S={S} d={d}"):
+      check(_lib.lib().sdmi_attn_bwd(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(o), ld_of(o), _p(dout),
                                    ld_of(dout), _p(lse), _p(delta), _p(dq), ld_of(dq), _p(dk), ld_of(dk), _p(dv),
                                    ld_of(dv), B, H, N, S, d, _stream()), "sdmi_attn_bwd")
 

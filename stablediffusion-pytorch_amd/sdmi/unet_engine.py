@@ -77,9 +77,11 @@ class PackPlan:
         self.views = {}
 
     def add(self, name, src, O, I, Ipad, KH, KW, so, si, skh, skw, kh_off=0, kh_mul=1, kw_off=0, kw_mul=1,
-            rows=None, into=None, row0=0):
-        """Pack dst[o][a][b][i] = src[o*so + i*si + (kh_off+kh_mul*a)*skh + (kw_off+kw_mul*b)*skw]."""
+            rows=None, into=None, row0=0, col0=0):
+        """Pack dst[o][a][b][i] = src[o*so + i*si + (kh_off+kh_mul*a)*skh + (kw_off+kw_mul*b)*skw]
+        (into a reserved matrix at row row0 / column col0 when `into` is given)."""
         n = (rows or O) * KH * KW * Ipad
+        dst_ld = 0
         if into is None:
             off = self.total
             self.total += (n + 63) // 64 * 64
@@ -87,9 +89,10 @@ class PackPlan:
             dst_off = off
         else:
             base, _, width = self.views[into]
-            dst_off = base + row0 * width
+            dst_off = base + row0 * width + col0
+            dst_ld = width if width != KH * KW * Ipad else 0
         self.items.append(dict(src=src, dst_off=dst_off, O=O, I=I, Ipad=Ipad, KH=KH, KW=KW, so=so, si=si, skh=skh,
-                               skw=skw, kh_off=kh_off, kh_mul=kh_mul, kw_off=kw_off, kw_mul=kw_mul))
+                               skw=skw, kh_off=kh_off, kh_mul=kh_mul, kw_off=kw_off, kw_mul=kw_mul, dst_ld=dst_ld))
 
     def reserve(self, name, rows, width):
         off = self.total
@@ -106,7 +109,7 @@ class PackPlan:
             d.src = it["src"].data_ptr()
             d.dst = self.buf.data_ptr() + 2 * it["dst_off"]
             d.so, d.si, d.skh, d.skw = it["so"], it["si"], it["skh"], it["skw"]
-            for f in ("O", "I", "Ipad", "KH", "KW", "kh_off", "kh_mul", "kw_off", "kw_mul"):
+            for f in ("O", "I", "Ipad", "KH", "KW", "kh_off", "kh_mul", "kw_off", "kw_mul", "dst_ld"):
                 setattr(d, f, it[f])
             n = it["O"] * it["KH"] * it["KW"] * it["Ipad"]
             bmap += [(j, c) for c in range((n + chunk - 1) // chunk)]
@@ -233,8 +236,14 @@ class UNetEngine:
             pk.add(None, w, cout, L["T"], L["T"], 1, 1, L["T"], 1, 0, 0, into="temb_all", row0=self.temb_off[(p, l)])
         for (p, l, cin, cout) in self.resnets:
             conv(f"{p}.resnet_conv_first.{l}.2")
-            conv(f"{p}.resnet_conv_second.{l}.2")
-            conv(f"{p}.residual_input_conv.{l}", dgrad=False)
+            conv(f"{p}.resnet_conv_second.{l}.2", fwd=False)
+            # second conv and the 1x1 residual conv as one K-concatenated weight [cout][9*cout + cin]
+            w2 = P[f"{p}.resnet_conv_second.{l}.2.weight"]
+            wr = P[f"{p}.residual_input_conv.{l}.weight"]
+            cat = f"{p}.res{l}#cat"
+            pk.reserve(cat, cout, 9 * cout + cin)
+            pk.add(None, w2, cout, cout, cout, 3, 3, cout * 9, 9, 3, 1, into=cat)
+            pk.add(None, wr, cout, cin, cin, 1, 1, cin, 1, 0, 0, into=cat, col0=9 * cout)
         nd = len(L["down"]) - 1
         for i in range(nd):
             p = f"downs.{i}"
@@ -452,13 +461,13 @@ class UNetEngine:
         tape.label = "head"
         C = L["conv_out"]
         Pn = H * W
-        mean, rstd = K.gn_stats(cur, B, Pn, C, G)
+        tab = K.gn_stats(cur, B, Pn, C, G, P["norm_out.weight"], P["norm_out.bias"])
         hs = self._new(B * Pn, C)
-        K.gn_apply(cur, mean, rstd, P["norm_out.weight"], P["norm_out.bias"], B, Pn, C, G, True, hs)
+        K.gn_apply(cur, tab, B, Pn, C, True, hs)
         pred = self._new(B * Pn, 8, torch.float32)
         K.conv_fwd(hs, B, H, W, C, C, self.W("conv_out#f"), 8, 3, 3, 1, 1, pred, 8, bias=P["conv_out.bias"],
                    n_store=self.im_channels)
-        tape.append((self._bwd_head, dict(x=cur, xn=cur_name, mean=mean, rstd=rstd, hs=hs, B=B, H=H, W=W)))
+        tape.append((self._bwd_head, dict(x=cur, xn=cur_name, tab=tab, hs=hs, B=B, H=H, W=W)))
         return pred, dict(tape=tape, st=st, grads=grads) if need_backward else None
 
     # ------------------------------------------------------------------------------------------
@@ -489,24 +498,23 @@ class UNetEngine:
         P, G = self.P, self.L["G"]
         Pn = h * w
         a, b = f"{p}.resnet_conv_first.{l}", f"{p}.resnet_conv_second.{l}"
-        m1, r1 = K.gn_stats(x, B, Pn, cin, G)
+        t1 = K.gn_stats(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"])
         h0 = self._new(B * Pn, cin)
-        K.gn_apply(x, m1, r1, P[a + ".0.weight"], P[a + ".0.bias"], B, Pn, cin, G, True, h0)
+        K.gn_apply(x, t1, B, Pn, cin, True, h0)
         h1 = self._new(B * Pn, cout)
         off = self.temb_off[(p, l)]
         K.conv_fwd(h0, B, h, w, cin, cin, self.W(a + ".2#f"), cout, 3, 3, 1, 1, h1, cout, bias=P[a + ".2.bias"],
                    rowbias=st["temb_all"][:, off:], rb_ld=self.temb_total)
-        m2, r2 = K.gn_stats(h1, B, Pn, cout, G)
+        t2 = K.gn_stats(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"])
         h2 = self._new(B * Pn, cout)
-        K.gn_apply(h1, m2, r2, P[b + ".0.weight"], P[b + ".0.bias"], B, Pn, cout, G, True, h2)
+        K.gn_apply(h1, t2, B, Pn, cout, True, h2)
         rc = f"{p}.residual_input_conv.{l}"
-        r = self._new(B * Pn, cout)
-        K.linear(x, self.W(rc + "#f"), r, bias=P[rc + ".bias"])
         y = out if out is not None else self._new(B * Pn, cout)
-        K.conv_fwd(h2, B, h, w, cout, cout, self.W(b + ".2#f"), cout, 3, 3, 1, 1, y, K.ld_of(y), bias=P[b + ".2.bias"],
-                   resid=r, ldr=cout)
+        # conv2(h2) + residual 1x1(x) in ONE GEMM: A = [im2col(h2) | x], B = [W2 | Wr]
+        K.conv_fwd(h2, B, h, w, cout, cout, self.W(f"{p}.res{l}#cat"), cout, 3, 3, 1, 1, y, K.ld_of(y),
+                   bias=P[b + ".2.bias"], x2=x, cin2=cin, bias2=P[rc + ".bias"])
         tape.append((self._resnet_bwd, dict(p=p, l=l, cin=cin, cout=cout, x=x, xn=xname, yn=oname, h0=h0, h1=h1, h2=h2,
-                                            m1=m1, r1=r1, m2=m2, r2=r2, B=B, h=h, w=w)))
+                                            t1=t1, t2=t2, B=B, h=h, w=w)))
         return y
 
     def _resnet_bwd(self, c, grads):
@@ -523,8 +531,8 @@ class UNetEngine:
         K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout)
         K.linear_wgrad(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
         dx, fresh = grads.get(c["xn"])
-        K.linear_dgrad(dy, self.W(rc + "#f"), dx, resid=None if fresh else dx)
-        K.gn_bwd(c["h1"], dh2, dh2, c["m2"], c["r2"], P[b + ".0.weight"], P[b + ".0.bias"], B, Pn, cout, G, True,
+        K.linear_dgrad(dy, self.W(f"{p}.res{l}#cat")[:, 9 * cout:], dx, resid=None if fresh else dx)
+        K.gn_bwd(c["h1"], dh2, dh2, c["t2"], P[b + ".0.weight"], B, Pn, cout, G, True,
                  self.g(b + ".0.weight"), self.g(b + ".0.bias"))
         off = self.temb_off[(p, l)]
         K.chan_sum(dh2, B, Pn, cout, per_bc=self.dtemb_all[:, off:off + cout], per_c=self.g(a + ".2.bias"),
@@ -532,7 +540,7 @@ class UNetEngine:
         K.conv_wgrad(dh2, cout, c["h0"], B, h, w, cin, cin, cout, 3, 3, 1, 1, self.g(a + ".2.weight"), h, w)
         dh0 = self._new(B * Pn, cin)
         K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin)
-        K.gn_bwd(c["x"], dh0, dx, c["m1"], c["r1"], P[a + ".0.weight"], P[a + ".0.bias"], B, Pn, cin, G, True,
+        K.gn_bwd(c["x"], dh0, dx, c["t1"], P[a + ".0.weight"], B, Pn, cin, G, True,
                  self.g(a + ".0.weight"), self.g(a + ".0.bias"), addend=dx)
 
     # ---- self / cross attention --------------------------------------------------------------------
@@ -541,15 +549,14 @@ class UNetEngine:
         N = h * w
         nk = f"{p}.cross_attention_norms.{l}" if cross else f"{p}.attention_norms.{l}"
         mk = f"{p}.cross_attentions.{l}" if cross else f"{p}.attentions.{l}"
-        mean, rstd = K.gn_stats(x, B, N, C, G)
+        tab = K.gn_stats(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"])
         a = self._new(B * N, C)
-        K.gn_apply(x, mean, rstd, P[nk + ".weight"], P[nk + ".bias"], B, N, C, G, False, a)
+        K.gn_apply(x, tab, B, N, C, False, a)
         Win = self.W(mk + ".in_proj_weight#f")
         bin_ = P[mk + ".in_proj_bias"]
         d = C // Hh
         o = self._new(B * N, C)
-        c = dict(p=p, l=l, C=C, x=x, xn=xname, yn=oname, a=a, mean=mean, rstd=rstd, o=o, B=B, N=N, cross=cross, nk=nk,
-                 mk=mk)
+        c = dict(p=p, l=l, C=C, x=x, xn=xname, yn=oname, a=a, tab=tab, o=o, B=B, N=N, cross=cross, nk=nk, mk=mk)
         if not cross:
             qkv = self._new(B * N, 3 * C)
             K.linear(a, Win, qkv, bias=bin_)
@@ -620,7 +627,7 @@ class UNetEngine:
                 addend = dx
             else:
                 addend = dy
-        K.gn_bwd(c["x"], da, dx, c["mean"], c["rstd"], P[nk + ".weight"], P[nk + ".bias"], B, N, C, G, False,
+        K.gn_bwd(c["x"], da, dx, c["tab"], P[nk + ".weight"], B, N, C, G, False,
                  self.g(nk + ".weight"), self.g(nk + ".bias"), addend=addend)
 
     # ---- down / up sampling convs --------------------------------------------------------------------
@@ -683,7 +690,7 @@ class UNetEngine:
         dhs = self._new(B * Pn, C)
         K.conv_fwd(dpred, B, H, W, 8, 8, self.W("conv_out#d"), C, 3, 3, 1, 1, dhs, C)
         dx, fresh = grads.get(c["xn"])
-        K.gn_bwd(c["x"], dhs, dx, c["mean"], c["rstd"], P["norm_out.weight"], P["norm_out.bias"], B, Pn, C, G, True,
+        K.gn_bwd(c["x"], dhs, dx, c["tab"], P["norm_out.weight"], B, Pn, C, G, True,
                  self.g("norm_out.weight"), self.g("norm_out.bias"), addend=None if fresh else dx)
 
     def _bwd_input(self, c, grads):
