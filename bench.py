@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-gemm", action="store_true", default=True)
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture (default: capture when N == 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,13 +104,21 @@ def main():
     x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
     gen = torch.Generator(device=device).manual_seed(1111 + rank)
 
-    def one_step():
+    def eager_step():
         noise = torch.randn(x0.shape, device=device, generator=gen)
         t = torch.randint(0, 1000, (B,), device=device, generator=gen)
         drop_t = torch.rand(B, device=device, generator=gen) < 0.1       # diffusion_utils.py:21-28
         txt = torch.where(drop_t[:, None, None], empty, text)
         keep = (torch.rand(B, device=device, generator=gen) > 0.1).float()  # diffusion_utils.py:31-37
         trainer.step(x0, noise, t, txt, mask, mask_keep=keep)
+
+    use_graph = not args.eager and world == 1
+    if use_graph:
+        from sdmi.graph import CapturedTrainStep
+        cap = CapturedTrainStep(trainer, x0, text, empty, mask, B, generator=gen)
+        one_step = cap.step
+    else:
+        one_step = eager_step
 
     for _ in range(args.warmup):
         one_step()
@@ -137,7 +146,7 @@ def main():
     roof = None
     if args.profile_gemm:
         K.PROFILE = []
-        one_step()
+        eager_step()
         torch.cuda.synchronize()
         prof, K.PROFILE = K.PROFILE, None
         by = {}
@@ -171,6 +180,7 @@ def main():
         "per_gpu_steps_per_s": steps_per_s, "samples_per_s": steps_per_s * B * world,
         "model_flops_utilization": FLOP_PER_STEP * steps_per_s / PEAK_BF16,
         "last_loss": state[S_LOSS], "last_grad_norm": state[S_NORM], "last_step_skipped": bool(state[S_SKIP]),
+        "hip_graph": use_graph,
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -50,6 +50,7 @@ struct EpiArgs {
   int raw;  // 1: write raw fp32 partials (split-K), epilogue applied by the reducer
   int nsplit;
   const float* ws;  // reducer input slabs
+  int vec;          // LDS-staged 16-B row stores (no column permute, 8-aligned columns/strides)
 };
 
 __device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
@@ -78,6 +79,50 @@ struct Epi {
     }
     if (g.c_f32) ((float*)g.C)[orow * g.ldc + ocol] = v;
     else ((bf16_t*)g.C)[orow * g.ldc + ocol] = f2bf(v);
+  }
+
+  // 8 consecutive columns [col, col+8) of one row, acc values in v (alpha/bias not yet applied)
+  __device__ __forceinline__ static void finish8(const EpiArgs& g, int row, int col, float* v) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= g.alpha;
+    if (g.bias) {
+      const float4 b0 = *(const float4*)(g.bias + col), b1 = *(const float4*)(g.bias + col + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    }
+    if (g.bias2) {
+      const float4 b0 = *(const float4*)(g.bias2 + col), b1 = *(const float4*)(g.bias2 + col + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    }
+    if (g.rowbias) {
+      float t[8];
+      unpack8(*(const uint4*)(g.rowbias + (long long)(row >> g.rb_shift) * g.rb_ld + col), t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    long long orow = row;
+    if (g.remap) {
+      int b = row >> (g.r_ghl + g.r_gwl);
+      int oy = (row >> g.r_gwl) & ((1 << g.r_ghl) - 1);
+      int ox = row & ((1 << g.r_gwl) - 1);
+      orow = ((long long)b * g.r_oh + oy * g.r_sy + g.r_oy) * g.r_ow + ox * g.r_sx + g.r_ox;
+    }
+    if (g.resid) {
+      float t[8];
+      unpack8(*(const uint4*)(g.resid + orow * g.ldr + col), t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += t[e];
+    }
+    if (g.act == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
+    }
+    if (g.c_f32) {
+      float* d = (float*)g.C + orow * g.ldc + col;
+      *(float4*)d = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      *(uint4*)((bf16_t*)g.C + orow * g.ldc + col) = pack8(v);
+    }
   }
 
   __device__ __forceinline__ static void store(const EpiArgs& g, int row, int col, float acc, int z) {
@@ -318,6 +363,46 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   }
 
   // ---------------- epilogue ----------------
+  if (e.vec) {
+    // Stage the fp32 tile through LDS in two 64-row halves and write whole rows with 16-B stores
+    // (8 bf16 or 4 fp32 per lane) instead of 64 scattered 2-byte stores per lane.
+    float* st = (float*)smem;  // [64][SROW] fp32, 33 KB
+    constexpr int SROW = 132;  // +4 floats: lanes of one ds_write hit distinct banks
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (wm == half * 64) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cl = wn + 16 * j + (lane & 15);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) st[(16 * i + 4 * (lane >> 4) + r) * SROW + cl] = acc[i][j][r];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {  // 64 rows x 16 chunks of 8 columns
+        const int ch = threadIdx.x + it * NT;
+        const int rl = ch >> 4, c8 = (ch & 15) * 8;
+        const int row = m0 + half * 64 + rl, col = n0 + c8;
+        float v[8];
+        const float4 lo = *(const float4*)(st + rl * SROW + c8), hi = *(const float4*)(st + rl * SROW + c8 + 4);
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+        if (e.raw) {
+          if (row < e.M && col < e.N) {
+            float* dst = (float*)e.C + (long long)z * e.split_stride + (long long)row * e.N + col;
+            *(float4*)dst = lo;
+            *(float4*)(dst + 4) = hi;
+          }
+        } else if (row < e.m_store && col < e.n_store) {
+          Epi::finish8(e, row, col, v);
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
   if (e.raw) {  // split-K slab: raw fp32 partials, the reducer applies the epilogue
     float* slab = (float*)e.C + (long long)z * e.split_stride;
 #pragma unroll
@@ -356,13 +441,27 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   }
 }
 
-// Sum split-K slabs and apply the epilogue.
+// Sum split-K slabs and apply the epilogue (8 columns per thread on the vector path).
 __global__ void splitk_reduce_kernel(const EpiArgs g) {
-  long long total = (long long)g.M * g.N;
-  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long stride = (long long)gridDim.x * blockDim.x;
   const float* ws = g.ws;
-  for (; idx < total; idx += stride) {
+  long long stride = (long long)gridDim.x * blockDim.x;
+  if (g.vec) {
+    const int N8 = g.N >> 3;
+    long long total = (long long)g.M * N8;
+    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
+      int row = (int)(idx / N8), col = (int)(idx - (long long)row * N8) * 8;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int zz = 0; zz < g.nsplit; ++zz) {
+        const float* p = ws + (long long)zz * g.split_stride + (long long)row * g.N + col;
+        const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      if (row < g.m_store && col < g.n_store) Epi::finish8(g, row, col, v);
+    }
+    return;
+  }
+  long long total = (long long)g.M * g.N;
+  for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
     float s = 0.f;
     for (int zz = 0; zz < g.nsplit; ++zz) s += ws[(long long)zz * g.split_stride + idx];
     int row = (int)(idx / g.N), col = (int)(idx - (long long)row * g.N);
@@ -409,6 +508,11 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   e.p_cvalid = d->p_cvalid > 0 ? d->p_cvalid : d->p_cin;
   e.m_store = d->m_store > 0 ? d->m_store : d->m;
   e.n_store = d->n_store > 0 ? d->n_store : d->n;
+  e.vec = !d->perm && d->n % 8 == 0 && e.n_store % 8 == 0 && d->ldc % 8 == 0 &&
+          (!d->resid || d->ldr % 8 == 0) && (!d->rowbias || d->rb_ld % 8 == 0) &&
+          ((uintptr_t)d->c % 16 == 0) && (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
+          (!d->bias2 || (uintptr_t)d->bias2 % 16 == 0) && (!d->resid || (uintptr_t)d->resid % 16 == 0) &&
+          (!d->rowbias || (uintptr_t)d->rowbias % 16 == 0);
   return 0;
 }
 
@@ -470,7 +574,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     red.nsplit = splits;
     red.split_stride = (long long)d->m * d->n;
     red.ws = (const float*)workspace;
-    long long total = (long long)d->m * d->n;
+    long long total = (long long)d->m * d->n / (red.vec ? 8 : 1);
     int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, red);
     err = hipGetLastError();

@@ -67,7 +67,7 @@ class FlatStore:
             for s in shapes[k]:
                 n *= s
             self.offsets[k] = (off, n)
-            off += n
+            off += (n + 3) // 4 * 4  # 16-B aligned starts (vector epilogue loads of biases)
         self.numel = off
         self.params = torch.zeros(off, dtype=torch.float32, device=device)
         self.grads = torch.zeros(off, dtype=torch.float32, device=device) if with_grads else None

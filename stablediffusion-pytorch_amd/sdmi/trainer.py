@@ -47,6 +47,7 @@ class DDPMTrainer:
         self.hp = dict(lr=lr, b1=betas[0], b2=betas[1], eps=eps, clip=max_grad_norm, ema=ema_decay,
                        growth=growth_interval)
         self.engine = UNetEngine(cfg, self.store.p, self.store.g, base=base)
+        self.num_timesteps = sched[0]
         sa, s1a = scheduler_tables(*sched)
         self.sqrt_abar, self.sqrt_1m_abar = sa.to(self.device), s1a.to(self.device)
         self.group = group

@@ -52,7 +52,8 @@ def test_flat_store_order_and_contiguous_runs():
     cfg = full_cond_config()
     shapes = O.unet_param_shapes(cfg)
     st = FlatStore(shapes, cfg, "cpu")
-    assert st.numel == 118513466
+    assert sum(n for _, n in st.offsets.values()) == 118513466
+    assert all(off % 4 == 0 for off, _ in st.offsets.values())
     res = resnet_list(layout(cfg))
     tw = [f"{p}.t_emb_layers.{l}.1.weight" for (p, l, ci, co) in res]
     v = contiguous_run(st.g, tw, (sum(co for (_, _, _, co) in res), 512))
