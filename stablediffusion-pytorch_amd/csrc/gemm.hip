@@ -21,6 +21,7 @@
 #include "../../include/sdmi.h"
 #include <string.h>
 #include <algorithm>
+#include <stdlib.h>
 
 namespace {
 
@@ -156,6 +157,89 @@ struct Epi {
     else ((bf16_t*)g.C)[orow * g.ldc + ocol] = f2bf(v);
   }
 };
+
+// Shared epilogue of the GEMM kernels: acc = this wave's 64x64 sub-tile (4x4 MFMA tiles), smem >= 34 KB
+// of LDS that no wave reads any more (the caller synchronises before).
+__device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][4], char* smem, int m0, int n0,
+                                              int wm, int wn, int lane, int z) {
+  // ---------------- epilogue ----------------
+  if (e.vec) {
+    // Stage the fp32 tile through LDS in two 64-row halves and write whole rows with 16-B stores
+    // (8 bf16 or 4 fp32 per lane) instead of 64 scattered 2-byte stores per lane.
+    float* st = (float*)smem;  // [64][SROW] fp32, 33 KB
+    constexpr int SROW = 132;  // +4 floats: lanes of one ds_write hit distinct banks
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (wm == half * 64) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cl = wn + 16 * j + (lane & 15);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) st[(16 * i + 4 * (lane >> 4) + r) * SROW + cl] = acc[i][j][r];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {  // 64 rows x 16 chunks of 8 columns
+        const int ch = threadIdx.x + it * NT;
+        const int rl = ch >> 4, c8 = (ch & 15) * 8;
+        const int row = m0 + half * 64 + rl, col = n0 + c8;
+        float v[8];
+        const float4 lo = *(const float4*)(st + rl * SROW + c8), hi = *(const float4*)(st + rl * SROW + c8 + 4);
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+        if (e.raw) {
+          if (row < e.M && col < e.N) {
+            float* dst = (float*)e.C + (long long)z * e.split_stride + (long long)row * e.N + col;
+            *(float4*)dst = lo;
+            *(float4*)(dst + 4) = hi;
+          }
+        } else if (row < e.m_store && col < e.n_store) {
+          Epi::finish8(e, row, col, v);
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  if (e.raw) {  // split-K slab: raw fp32 partials, the reducer applies the epilogue
+    float* slab = (float*)e.C + (long long)z * e.split_stride;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn + 16 * j + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 v = acc[i][j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+          if (row < e.M && col < e.N) slab[(long long)row * e.N + col] = v[r];
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wn + 16 * j + (lane & 15);
+      const bool cok = col < e.n_store;
+      float bsum = 0.f;
+      if (cok) {
+        if (e.bias) bsum += e.bias[col];
+        if (e.bias2) bsum += e.bias2[col];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 v = acc[i][j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+          if (cok && row < e.m_store) Epi::finish(e, row, col, e.alpha * v[r] + bsum);
+        }
+      }
+    }
+  }
+}
 
 template <int AM, int BMODE>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs e) {
@@ -362,83 +446,227 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
     }
   }
 
-  // ---------------- epilogue ----------------
-  if (e.vec) {
-    // Stage the fp32 tile through LDS in two 64-row halves and write whole rows with 16-B stores
-    // (8 bf16 or 4 fp32 per lane) instead of 64 scattered 2-byte stores per lane.
-    float* st = (float*)smem;  // [64][SROW] fp32, 33 KB
-    constexpr int SROW = 132;  // +4 floats: lanes of one ds_write hit distinct banks
+  gemm_epilogue(e, acc, smem, m0, n0, wm, wn, lane, z);
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA pipelined variant: operands go global -> LDS with buffer_load ... lds (no VGPR staging, no
+// ds_write), STAGES-deep ring, one barrier per 64-deep K tile. The LDS destination of a DMA
+// wave-instruction is lane-linear (1 KiB per instruction), so the XOR swizzles of the LDS images are
+// applied to the per-lane SOURCE addresses (logical chunk = physical slot ^ swizzle(row)); the
+// fragment reads are unchanged. Out-of-range lanes (conv padding, ragged tiles) use an offset beyond
+// the buffer record and the hardware writes zeros.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ s16x8 frag_kc(const char* tile, int rbase, int ks, int lane) {
+  int r = rbase + (lane & 15);
+  int c = ks * 4 + (lane >> 4);
+  return *(const s16x8*)(tile + kc_off(r, c));
+}
+
+__device__ __forceinline__ s16x8 frag_tr(const char* tile, int cbase, int ks, int lane) {
+  int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  int r1 = ks * 32 + gq * 8 + q;
+  int c = (cbase >> 3) + (p >> 1);
+  int o1 = tr_off(r1, c) + (p & 1) * 8;
+  int o2 = tr_off(r1 + 4, c) + (p & 1) * 8;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SDMI_LDS s16x4*)(tile + o1));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SDMI_LDS s16x4*)(tile + o2));
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, int off) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (SDMI_LDS void*)lds_wave_base, 16, off, 0, 0, 0);
+}
+
+template <int AM, int BMODE, int STAGES>
+__global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(const Args g, const EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // STAGES x (A 16 KiB | B 16 KiB)
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int z = blockIdx.z;
+  const int nkt_total = (g.K + BK - 1) / BK;
+  const int kt0 = z * g.ktiles_per_split;
+  const int kt1 = min(nkt_total, kt0 + g.ktiles_per_split);
+  constexpr int OOB = (int)0x80000000;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsA2 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.A2 ? g.A2 : g.A), (short)0, 0x7fffffff, 0x00020000);
+
+  // ---- per-lane, per-instruction (j = 0..3) coordinates, fixed over the K loop ----
+  // K-contiguous image: instruction j of wave w fills rows (w*4+j)*8 .. +8, lane -> row +lane>>3, slot lane&7
+  // MN-contiguous image: fills k-rows (w*4+j)*4 .. +4, lane -> k-row +lane>>4, slot lane&15
+  int a_base[4], b_base[4];   // element offsets (without the k / pixel part)
+  int a_kk[4], b_kk[4];       // k offset inside the tile (KC: chunk*8) or k-row (MN)
+  bool a_ok[4], b_ok[4];
+  int a_iy[4], a_ix[4], a_pb[4], a_pix[4];
+  int b_ty[4], b_tx[4];
+  const bool cin64 = AM == SDMI_A_CONV && (g.cin & 63) == 0;  // k tile lies inside one tap
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (wm == half * 64) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int cl = wn + 16 * j + (lane & 15);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) st[(16 * i + 4 * (lane >> 4) + r) * SROW + cl] = acc[i][j][r];
-        }
+  for (int j = 0; j < 4; ++j) {
+    if (AM == SDMI_A_COLMAJOR) {
+      int kr = (wave * 4 + j) * 4 + (lane >> 4);
+      int c = (lane & 15) ^ tr_swz(kr);
+      int m = m0 + c * 8;
+      a_ok[j] = m < g.M;
+      a_base[j] = m;
+      a_kk[j] = kr;
+    } else {
+      int r = (wave * 4 + j) * 8 + (lane >> 3);
+      int c = (lane & 7) ^ (r & 7);
+      int m = m0 + r;
+      a_ok[j] = m < g.M;
+      a_kk[j] = c * 8;
+      if (AM == SDMI_A_ROWMAJOR) {
+        a_base[j] = m * g.lda;
+      } else {
+        int b = m >> (g.ohl + g.owl);
+        int oy = (m >> g.owl) & ((1 << g.ohl) - 1);
+        int ox = m & ((1 << g.owl) - 1);
+        a_pb[j] = b * g.ih;
+        a_iy[j] = oy * g.sy + g.oy0;
+        a_ix[j] = ox * g.sx + g.ox0;
+        a_base[j] = m * g.lda2;  // second (K-concatenated) source row
+        a_pix[j] = ((a_pb[j] + a_iy[j]) * g.iw + a_ix[j]) * g.ldx;
       }
-      __syncthreads();
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {  // 64 rows x 16 chunks of 8 columns
-        const int ch = threadIdx.x + it * NT;
-        const int rl = ch >> 4, c8 = (ch & 15) * 8;
-        const int row = m0 + half * 64 + rl, col = n0 + c8;
-        float v[8];
-        const float4 lo = *(const float4*)(st + rl * SROW + c8), hi = *(const float4*)(st + rl * SROW + c8 + 4);
-        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-        if (e.raw) {
-          if (row < e.M && col < e.N) {
-            float* dst = (float*)e.C + (long long)z * e.split_stride + (long long)row * e.N + col;
-            *(float4*)dst = lo;
-            *(float4*)(dst + 4) = hi;
-          }
-        } else if (row < e.m_store && col < e.n_store) {
-          Epi::finish8(e, row, col, v);
-        }
-      }
-      __syncthreads();
     }
-    return;
+    if (BMODE == SDMI_B_NK) {
+      int r = (wave * 4 + j) * 8 + (lane >> 3);
+      int c = (lane & 7) ^ (r & 7);
+      int n = n0 + r;
+      b_ok[j] = n < g.N;
+      b_base[j] = n * g.ldb;
+      b_kk[j] = c * 8;
+    } else {
+      int kr = (wave * 4 + j) * 4 + (lane >> 4);
+      int c = (lane & 15) ^ tr_swz(kr);
+      int n = n0 + c * 8;
+      b_ok[j] = n < g.N;
+      b_kk[j] = kr;
+      b_base[j] = n;
+      if (BMODE == SDMI_B_KN_CONV) {
+        int tap = n / g.cin;
+        int ci = n - tap * g.cin;
+        b_ty[j] = tap / g.kw;
+        b_tx[j] = tap - b_ty[j] * g.kw;
+        b_base[j] = ci;
+      }
+    }
   }
-  if (e.raw) {  // split-K slab: raw fp32 partials, the reducer applies the epilogue
-    float* slab = (float*)e.C + (long long)z * e.split_stride;
+
+  auto issue = [&](int kt, int stage) __attribute__((always_inline)) {
+    char* sa = smem + stage * 2 * TILE_BYTES;
+    char* sb = sa + TILE_BYTES;
+    const int k0 = kt * BK;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn + 16 * j + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const f32x4 v = acc[i][j];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
-          if (row < e.M && col < e.N) slab[(long long)row * e.N + col] = v[r];
+      char* dst = sa + (wave * 4 + j) * 1024;
+      int off;
+      if (AM == SDMI_A_ROWMAJOR) {
+        int k = k0 + a_kk[j];
+        off = (a_ok[j] && k < g.K) ? (a_base[j] + k) * 2 : OOB;
+        dma16(rsA, dst, off);
+      } else if (AM == SDMI_A_COLMAJOR) {
+        int k = k0 + a_kk[j];
+        off = (a_ok[j] && k < g.K) ? (k * g.lda + a_base[j]) * 2 : OOB;
+        dma16(rsA, dst, off);
+      } else {
+        int k = k0 + a_kk[j];
+        if (k0 >= g.k_split) {  // fused 1x1 second source, tile-uniform (k_split % 64 == 0 on this path)
+          off = (a_ok[j] && k < g.K) ? (a_base[j] + (k - g.k_split)) * 2 : OOB;
+          dma16(rsA2, dst, off);
+        } else if (cin64) {
+          // tap, and with it the (ty, tx) shift, is uniform over the tile: scalar math once per tile
+          const int tap = k0 / g.cin;
+          const int ty = tap / g.kw, tx = tap - ty * g.kw;
+          const int sh = (ty * g.iw + tx) * g.ldx + (k0 - tap * g.cin);
+          int iy = a_iy[j] + ty, ix = a_ix[j] + tx;
+          bool ok = a_ok[j] && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
+          off = ok ? (a_pix[j] + sh + a_kk[j]) * 2 : OOB;
+          dma16(rsA, dst, off);
+        } else {
+          int tap = k / g.cin;
+          int ci = k - tap * g.cin;
+          int ty = tap / g.kw, tx = tap - (tap / g.kw) * g.kw;
+          int iy = a_iy[j] + ty, ix = a_ix[j] + tx;
+          bool ok = a_ok[j] && k < g.k_split && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
+          off = ok ? (((a_pb[j] + iy) * g.iw + ix) * g.ldx + ci) * 2 : OOB;
+          dma16(rsA, dst, off);
         }
       }
     }
-  } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn + 16 * j + (lane & 15);
-      const bool cok = col < e.n_store;
-      float bsum = 0.f;
-      if (cok) {
-        if (e.bias) bsum += e.bias[col];
-        if (e.bias2) bsum += e.bias2[col];
+      char* dst = sb + (wave * 4 + j) * 1024;
+      int off;
+      if (BMODE == SDMI_B_NK) {
+        int k = k0 + b_kk[j];
+        off = (b_ok[j] && k < g.K) ? (b_base[j] + k) * 2 : OOB;
+      } else if (BMODE == SDMI_B_KN) {
+        int k = k0 + b_kk[j];
+        off = (b_ok[j] && k < g.K) ? (k * g.ldb + b_base[j]) * 2 : OOB;
+      } else {
+        int p = k0 + b_kk[j];
+        int b = p >> (g.ohl + g.owl);
+        int oy = (p >> g.owl) & ((1 << g.ohl) - 1);
+        int ox = p & ((1 << g.owl) - 1);
+        int iy = oy * g.sy + g.oy0 + b_ty[j], ix = ox * g.sx + g.ox0 + b_tx[j];
+        bool ok = b_ok[j] && p < g.K && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
+        off = ok ? (((b * g.ih + iy) * g.iw + ix) * g.ldx + b_base[j]) * 2 : OOB;
       }
+      dma16(rsB, dst, off);
+    }
+  };
+
+  f32x4 acc[4][4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const f32x4 v = acc[i][j];
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
-          if (cok && row < e.m_store) Epi::finish(e, row, col, e.alpha * v[r] + bsum);
-        }
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nt = kt1 - kt0;
+  if (nt > 0) {
+    // prologue: STAGES-1 tiles in flight
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < nt) issue(kt0 + s, s);
+    for (int t = 0; t < nt; ++t) {
+      // tile t landed for this thread: at most (tiles issued after t) x 8 DMA instructions outstanding
+      const int after = min(STAGES - 2, nt - 1 - t);
+      if (after >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's DMA for tile t done; every wave done with tile t-1
+      if (t + STAGES - 1 < nt) issue(kt0 + t + STAGES - 1, (t + STAGES - 1) % STAGES);
+      const char* ta = smem + (t % STAGES) * 2 * TILE_BYTES;
+      const char* tb = ta + TILE_BYTES;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        s16x8 fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          fa[i] = (AM == SDMI_A_COLMAJOR) ? frag_tr(ta, wm + 16 * i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          fb[j] = (BMODE == SDMI_B_NK) ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_tr(tb, wn + 16 * j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
       }
+      __builtin_amdgcn_s_setprio(0);
     }
   }
+  __syncthreads();
+  gemm_epilogue(e, acc, smem, m0, n0, wm, wn, lane, z);
 }
 
 // Sum split-K slabs and apply the epilogue (8 columns per thread on the vector path).
@@ -469,9 +697,32 @@ __global__ void splitk_reduce_kernel(const EpiArgs g) {
   }
 }
 
+// Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged, 2 / 3 LDS-DMA ring
+// with that many stages, -1 (default) per mode: the DMA ring where it measured faster on the step's
+// shapes (row-major and implicit-conv A), register staging for the col-major (weight-gradient) A.
+int gemm_variant() {
+  static int v = -2;
+  if (v == -2) {
+    const char* s = getenv("SDMI_GEMM_VARIANT");
+    v = s ? atoi(s) : -1;
+    if (v != 0 && v != 2 && v != 3) v = -1;
+  }
+  return v;
+}
+
 template <int AM, int BMODE>
 hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
+  int v = gemm_variant();
+  if (v < 0) v = AM == SDMI_A_COLMAJOR ? 0 : 2;
+  // the DMA path needs a tile-uniform second source (k_split % BK == 0)
+  const bool dma_ok = AM != SDMI_A_CONV || !a.A2 || a.k_split % BK == 0;
+  if (v == 0 || !dma_ok) {
+    hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
+  } else if (v == 2) {
+    hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2>), grid, dim3(NT), 2 * 2 * TILE_BYTES, s, a, e);
+  } else {
+    hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 3>), grid, dim3(NT), 3 * 2 * TILE_BYTES, s, a, e);
+  }
   return hipGetLastError();
 }
 
