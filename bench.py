@@ -79,7 +79,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-gemm", action="store_true", default=True)
-    ap.add_argument("--eager", action="store_true", help="no hipGraph capture (default: capture when N == 1)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one captured hipGraph (N == 1; default off: eager issue with the "
+                         "weight-gradient stream overlapped measured faster than the captured graph)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,7 +114,7 @@ def main():
         keep = (torch.rand(B, device=device, generator=gen) > 0.1).float()  # diffusion_utils.py:31-37
         trainer.step(x0, noise, t, txt, mask, mask_keep=keep)
 
-    use_graph = not args.eager and world == 1
+    use_graph = args.graph and world == 1
     if use_graph:
         from sdmi.graph import CapturedTrainStep
         cap = CapturedTrainStep(trainer, x0, text, empty, mask, B, generator=gen)

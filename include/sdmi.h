@@ -161,6 +161,8 @@ typedef struct sdmi_pack_desc {
   int O, I, Ipad, KH, KW, kh_off, kh_mul, kw_off, kw_mul;
   int dst_ld; /* row stride of dst in elements (0 = KH*KW*Ipad): packs into a column slice of a wider matrix */
 } sdmi_pack_desc;
+/* Work split: one workgroup packs max(1, sdmi_pack_chunk() / (KH*KW*Ipad)) consecutive destination rows;
+ * bmap_dev holds one int2 (descriptor index, first row) per workgroup. KH*KW*(Ipad+8) <= 16384. */
 int sdmi_pack_chunk(void);
 int sdmi_pack_weights(const sdmi_pack_desc* descs_dev, const void* bmap_dev, int nblocks, sdmi_stream_t stream);
 

@@ -15,6 +15,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--dump", default="", help="write every launch (in issue order) to this file")
     args = ap.parse_args()
     from sdmi.trainer import DDPMTrainer
     from sdmi import kernels as K
@@ -54,6 +55,10 @@ def main():
     for tag, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         tf = fl / (ms * 1e-3) / 1e12 if fl else 0
         print(f"{tag:14s} {n:5d} launches {ms:8.3f} ms  {tf:7.1f} TFLOP/s")
+    if args.dump:
+        with open(args.dump, "w") as f:
+            for tag, fl, ms, info in rows:
+                f.write(f"{ms * 1000:9.1f} us  {tag:12s} {info}\n")
     print("--- top launches ---")
     for tag, fl, ms, info in sorted(rows, key=lambda r: -r[2])[:args.top]:
         tf = fl / (ms * 1e-3) / 1e12 if fl else 0

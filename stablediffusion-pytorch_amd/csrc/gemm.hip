@@ -48,11 +48,16 @@ struct EpiArgs {
   int remap, r_ghl, r_gwl, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
   int perm, p_cin, p_taps, p_cvalid;
   int m_store, n_store;
-  int raw;  // 1: write raw fp32 partials (split-K), epilogue applied by the reducer
+  int raw;  // 1: write raw fp32 partials (split-K) to ws, epilogue applied by the reducer
   int nsplit;
-  const float* ws;  // reducer input slabs
+  const float* ws;  // split-K slabs [nsplit][M][N]
+  unsigned* counters;  // per-tile arrival counters: the last split of a tile reduces it (0: separate reducer)
   int vec;          // LDS-staged 16-B row stores (no column permute, 8-aligned columns/strides)
+  int n8;           // N % 8 == 0: split-K slabs are written / read as 16-B rows even when !vec
 };
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int CPOL_SC1 = 16;  // buffer cache policy: device (agent) scope coherence
 
 __device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
 __device__ __forceinline__ int tr_swz(int r) { return ((r & 3) | ((r >> 1) & 4)) << 1; }
@@ -129,9 +134,13 @@ struct Epi {
   __device__ __forceinline__ static void store(const EpiArgs& g, int row, int col, float acc, int z) {
     if (row >= g.M || col >= g.N) return;
     if (g.raw) {
-      ((float*)g.C)[(long long)z * g.split_stride + (long long)row * g.N + col] = acc;
+      ((float*)g.ws)[(long long)z * g.split_stride + (long long)row * g.N + col] = acc;
       return;
     }
+    store_final(g, row, col, acc);
+  }
+
+  __device__ __forceinline__ static void store_final(const EpiArgs& g, int row, int col, float acc) {
     if (row >= g.m_store || col >= g.n_store) return;
     float v = g.alpha * acc;
     if (g.bias) v += g.bias[col];
@@ -163,7 +172,7 @@ struct Epi {
 __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][4], char* smem, int m0, int n0,
                                               int wm, int wn, int lane, int z) {
   // ---------------- epilogue ----------------
-  if (e.vec) {
+  if (e.vec || (e.raw && e.n8)) {
     // Stage the fp32 tile through LDS in two 64-row halves and write whole rows with 16-B stores
     // (8 bf16 or 4 fp32 per lane) instead of 64 scattered 2-byte stores per lane.
     float* st = (float*)smem;  // [64][SROW] fp32, 33 KB
@@ -191,9 +200,11 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
         v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
         if (e.raw) {
           if (row < e.M && col < e.N) {
-            float* dst = (float*)e.C + (long long)z * e.split_stride + (long long)row * e.N + col;
-            *(float4*)dst = lo;
-            *(float4*)(dst + 4) = hi;
+            // device-coherent (sc1) stores: the tile's last split may run on another XCD
+            const int off = (int)(((long long)z * e.split_stride + (long long)row * e.N + col) * 4);
+            const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), rw, off, 0, CPOL_SC1);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), rw, off + 16, 0, CPOL_SC1);
           }
         } else if (row < e.m_store && col < e.n_store) {
           Epi::finish8(e, row, col, v);
@@ -204,7 +215,8 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
     return;
   }
   if (e.raw) {  // split-K slab: raw fp32 partials, the reducer applies the epilogue
-    float* slab = (float*)e.C + (long long)z * e.split_stride;
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
+    const long long zoff = (long long)z * e.split_stride;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = n0 + wn + 16 * j + (lane & 15);
@@ -214,7 +226,9 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
-          if (row < e.M && col < e.N) slab[(long long)row * e.N + col] = v[r];
+          if (row < e.M && col < e.N)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rw,
+                                                  (int)((zoff + (long long)row * e.N + col) * 4), 0, CPOL_SC1);
         }
       }
     }
@@ -238,6 +252,62 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
         }
       }
     }
+  }
+}
+
+// Split-K without a second launch: every split of a tile publishes its slab and bumps the tile's
+// arrival counter; the split that arrives last sums the slabs in fixed z order (deterministic) and
+// applies the epilogue, then re-arms the counter for the next launch (graph replays included).
+__device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0, int n0) {
+  // Slabs were written with device-coherent (sc1) stores, so no L2 write-back fence is needed: wait
+  // for this block's stores to complete, then count the arrival with a relaxed device-scope atomic.
+  int* flag = (int*)smem;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* ctr = e.counters + blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(e.nsplit - 1);
+    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
+  const int zstride = (int)(e.split_stride * 4);
+  if (e.n8) {
+    // 2048 chunks of 8 columns, 8 per thread; 4 splits (8 loads) in flight per thread
+#pragma unroll 1
+    for (int ch = threadIdx.x; ch < BM * (BN / 8); ch += NT) {
+      const int row = m0 + (ch >> 4), col = n0 + (ch & 15) * 8;
+      if (e.vec ? (row >= e.m_store || col >= e.n_store) : (row >= e.M || col >= e.N)) continue;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const int off = (row * e.N + col) * 4;
+#pragma unroll 4
+      for (int zz = 0; zz < e.nsplit; ++zz) {  // sc1 loads: read past a stale local L2
+        const int o = off + zz * zstride;
+        const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, o, 0, CPOL_SC1));
+        const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, o + 16, 0, CPOL_SC1));
+        v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3]; v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
+      }
+      if (e.vec) {
+        Epi::finish8(e, row, col, v);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) Epi::store_final(e, row, col + q, v[q]);
+      }
+    }
+    return;
+  }
+#pragma unroll 1
+  for (int idx = threadIdx.x; idx < BM * BN; idx += NT) {
+    const int row = m0 + idx / BN, col = n0 + idx % BN;
+    if (row >= e.M || col >= e.N) continue;
+    float acc = 0.f;
+    int off = (row * e.N + col) * 4;
+    for (int zz = 0; zz < e.nsplit; ++zz, off += zstride)
+      acc += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, off, 0, CPOL_SC1));
+    Epi::store_final(e, row, col, acc);
   }
 }
 
@@ -447,6 +517,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   }
 
   gemm_epilogue(e, acc, smem, m0, n0, wm, wn, lane, z);
+  if (e.raw && e.counters) splitk_tail(e, smem, m0, n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -667,6 +738,7 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
   }
   __syncthreads();
   gemm_epilogue(e, acc, smem, m0, n0, wm, wn, lane, z);
+  if (e.raw && e.counters) splitk_tail(e, smem, m0, n0);
 }
 
 // Sum split-K slabs and apply the epilogue (8 columns per thread on the vector path).
@@ -726,6 +798,27 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
   return hipGetLastError();
 }
 
+__device__ unsigned g_splitk_counters[1 << 16];  // zero at load; every tile re-arms its own counter
+
+// per-device address of the split-K arrival counters, or null when SDMI_SPLITK_FUSED=0
+unsigned* splitk_counters() {
+  static int fused = -1;
+  static unsigned* addr[64] = {};
+  if (fused < 0) {
+    const char* s = getenv("SDMI_SPLITK_FUSED");
+    fused = s ? atoi(s) != 0 : 0;  // measured slower than the separate reducer on the step's shapes
+  }
+  if (!fused) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!addr[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_splitk_counters)) != hipSuccess) return nullptr;
+    addr[dev] = (unsigned*)p;
+  }
+  return addr[dev];
+}
+
 int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   if (!d || d->m <= 0 || d->n <= 0 || d->k <= 0) return -1;
   // K is the contiguous (16-B chunked) dimension of row-major / conv A and of [n][k] B only
@@ -759,6 +852,7 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   e.p_cvalid = d->p_cvalid > 0 ? d->p_cvalid : d->p_cin;
   e.m_store = d->m_store > 0 ? d->m_store : d->m;
   e.n_store = d->n_store > 0 ? d->n_store : d->n;
+  e.n8 = d->n % 8 == 0;
   e.vec = !d->perm && d->n % 8 == 0 && e.n_store % 8 == 0 && d->ldc % 8 == 0 &&
           (!d->resid || d->ldr % 8 == 0) && (!d->rowbias || d->rb_ld % 8 == 0) &&
           ((uintptr_t)d->c % 16 == 0) && (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
@@ -771,8 +865,20 @@ int plan_splits(const sdmi_gemm_desc* d) {
   long long tiles = (long long)((d->m + BM - 1) / BM) * ((d->n + BN - 1) / BN);
   int nkt = (d->k + BK - 1) / BK;
   int s = 1;
-  // aim for >= ~2 waves of workgroups over 256 CUs, keep >= 8 k-tiles per slice
-  while (tiles * s < 384 && nkt / (s * 2) >= 8 && s < 16) s *= 2;
+  static int policy = -1;
+  if (policy < 0) {
+    const char* e = getenv("SDMI_SPLIT_POLICY");
+    policy = e ? atoi(e) : 1;
+  }
+  if (policy == 0) {  // shallow: >= 8 k-tiles per slice, at most 16 slices
+    while (tiles * s < 384 && nkt / (s * 2) >= 8 && s < 16) s *= 2;
+    return s;
+  }
+  // fill the 256 CUs: deep split-K for the small-output / long-K weight gradients (a 128 x 128 dW over
+  // 32768 pixels is ONE tile), keeping >= 4 k-tiles per slice and the slabs within 32-bit offsets
+  while (tiles * s < 256 && nkt / (s * 2) >= 4 && s < 128 &&
+         (long long)(s * 2) * d->m * d->n * 4 < (1LL << 31))
+    s *= 2;
   return s;
 }
 
@@ -797,17 +903,20 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
   hipStream_t s = (hipStream_t)stream;
   int splits = plan_splits(d);
   if (splits > 1 && (!workspace || ws_bytes < (size_t)splits * d->m * d->n * sizeof(float))) splits = 1;
+  if ((long long)splits * d->m * d->n * 4 >= (1LL << 31)) splits = 1;  // slab offsets are 32-bit
   int nkt = (d->k + BK - 1) / BK;
   a.ktiles_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + a.ktiles_per_split - 1) / a.ktiles_per_split;
   a.nsplit = splits;
   EpiArgs run = e;
+  dim3 grid((d->n + BN - 1) / BN, (d->m + BM - 1) / BM, splits);
   if (splits > 1) {
     run.raw = 1;
-    run.C = workspace;
+    run.ws = (const float*)workspace;
+    run.nsplit = splits;
     run.split_stride = (long long)d->m * d->n;
+    if ((long long)grid.x * grid.y <= (1 << 16)) run.counters = splitk_counters();
   }
-  dim3 grid((d->n + BN - 1) / BN, (d->m + BM - 1) / BM, splits);
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
   switch (key) {
@@ -819,7 +928,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     default: return -6;
   }
   if (err != hipSuccess) return (int)err;
-  if (splits > 1) {
+  if (splits > 1 && !run.counters) {
     EpiArgs red = e;
     red.raw = 0;
     red.nsplit = splits;

@@ -205,27 +205,58 @@ __global__ void copy_slice_kernel(const bf16_t* src, int lds, bf16_t* dst, int l
 
 
 namespace {
-constexpr int PACK_CHUNK = 4096;  // elements per workgroup; bmap[blk] = (descriptor, chunk)
+constexpr int PACK_CHUNK = 4096;   // target elements per workgroup; bmap[blk] = (descriptor, first row)
+constexpr int PACK_LDS_ELEMS = 16384;  // bf16 staging capacity (32 KiB, 4+ workgroups per CU): taps * (Ipad + 8)
+
+template <int TAPS>
+__device__ __forceinline__ void pack_gather(const sdmi_pack_desc& d, const float* src, bf16_t* st, int ld, int taps) {
+  const int T = TAPS > 0 ? TAPS : taps;
+  for (int idx = threadIdx.x; idx < T * d.I; idx += NT) {
+    const int i = idx / T, t = idx - i * T;
+    const int a = t / d.KW, b = t - a * d.KW;
+    const int kh = d.kh_off + d.kh_mul * a, kw = d.kw_off + d.kw_mul * b;
+    st[t * ld + i] = f2bf(src[(long long)i * d.si + (long long)kh * d.skh + (long long)kw * d.skw]);
+  }
+}
+
+// One workgroup packs whole destination rows o0 .. o0+rows-1 of one descriptor. Phase 1 gathers the
+// row's source elements in SOURCE order (tap fastest: contiguous [I][KH][KW] runs for conv weights)
+// into LDS as bf16, phase 2 writes the [tap][Ipad] row with 16-byte stores.
 __global__ void pack_kernel(const sdmi_pack_desc* descs, const int2* bmap) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t st[];
   const int2 bm = bmap[blockIdx.x];
   const sdmi_pack_desc& d = descs[bm.x];
-  const long long n = (long long)d.O * d.KH * d.KW * d.Ipad;
-  const long long r0 = (long long)bm.y * PACK_CHUNK;
-  for (long long r = r0 + threadIdx.x; r < n && r < r0 + PACK_CHUNK; r += NT) {
-    int i = (int)(r % d.Ipad);
-    long long r2 = r / d.Ipad;
-    int b = (int)(r2 % d.KW);
-    long long r3 = r2 / d.KW;
-    int a = (int)(r3 % d.KH);
-    int o = (int)(r3 / d.KH);
-    float v = 0.f;
-    if (i < d.I) {
-      int kh = d.kh_off + d.kh_mul * a, kw = d.kw_off + d.kw_mul * b;
-      v = d.src[o * d.so + i * d.si + kh * d.skh + kw * d.skw];
+  const int taps = d.KH * d.KW;
+  const int ld = d.Ipad + 8;  // staging row stride: 16-B aligned, shifts banks per tap
+  const int row = taps * d.Ipad;
+  const int rows = max(1, PACK_CHUNK / row);
+  const int o_end = min(d.O, bm.y + rows);
+#pragma unroll 1
+  for (int o = bm.y; o < o_end; ++o) {
+    const float* src = d.src + (long long)o * d.so;
+    switch (taps) {  // constant divisors for the common tap counts
+      case 1: pack_gather<1>(d, src, st, ld, taps); break;
+      case 4: pack_gather<4>(d, src, st, ld, taps); break;
+      case 9: pack_gather<9>(d, src, st, ld, taps); break;
+      case 16: pack_gather<16>(d, src, st, ld, taps); break;
+      default: pack_gather<0>(d, src, st, ld, taps); break;
     }
-    long long dr = d.dst_ld ? (r / ((long long)d.KH * d.KW * d.Ipad)) * d.dst_ld + r % ((long long)d.KH * d.KW * d.Ipad)
-                            : r;
-    ((bf16_t*)d.dst)[dr] = f2bf(v);
+    __syncthreads();
+    bf16_t* dst = (bf16_t*)d.dst + (d.dst_ld ? (long long)o * d.dst_ld : (long long)o * row);
+    for (int q = threadIdx.x; q < row / 8; q += NT) {
+      const int t = (q * 8) / d.Ipad, i0 = q * 8 - t * d.Ipad;
+      uint4 v;
+      if (i0 + 8 <= d.I) {
+        v = *(const uint4*)(st + t * ld + i0);
+      } else {  // zero padding columns I .. Ipad
+        bf16_t tmp[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tmp[e] = i0 + e < d.I ? st[t * ld + i0 + e] : (bf16_t)0;
+        v = *(const uint4*)tmp;
+      }
+      *(uint4*)(dst + q * 8) = v;
+    }
+    __syncthreads();
   }
 }
 }  // namespace
@@ -318,7 +349,8 @@ extern "C" int sdmi_pack_chunk(void) { return PACK_CHUNK; }
 // descs_dev: device array of descriptors; bmap_dev: device array of int2 (descriptor, chunk), one per workgroup
 extern "C" int sdmi_pack_weights(const sdmi_pack_desc* descs_dev, const void* bmap_dev, int nblocks, sdmi_stream_t stream) {
   if (nblocks <= 0) return 0;
-  hipLaunchKernelGGL(pack_kernel, dim3(nblocks), dim3(NT), 0, (hipStream_t)stream, descs_dev, (const int2*)bmap_dev);
+  hipLaunchKernelGGL(pack_kernel, dim3(nblocks), dim3(NT), PACK_LDS_ELEMS * sizeof(bf16_t), (hipStream_t)stream, descs_dev,
+                     (const int2*)bmap_dev);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -18,6 +18,7 @@ class BucketReducer:
         self.total = flat.numel()
         self.cuda = flat.is_cuda
         self.stream = torch.cuda.Stream(device=flat.device) if self.cuda else None
+        self.producers = []  # extra streams that write gradients (the engine's weight-gradient stream)
         self.reset()
 
     def reset(self):
@@ -27,10 +28,14 @@ class BucketReducer:
     def _launch(self, lo, hi):
         view = self.flat[lo:hi]
         if self.cuda:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.flat.device))
+            evs = []
+            for st in [torch.cuda.current_stream(self.flat.device)] + list(self.producers):
+                ev = torch.cuda.Event()
+                ev.record(st)
+                evs.append(ev)
             with torch.cuda.stream(self.stream):
-                self.stream.wait_event(ev)
+                for ev in evs:
+                    self.stream.wait_event(ev)
                 self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
         else:
             self.works.append(dist.all_reduce(view, group=self.group, async_op=True))

@@ -53,6 +53,8 @@ class DDPMTrainer:
         self.group = group
         self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
         self.reducer = BucketReducer(self.store.grads, group, bucket_bytes) if self.world > 1 else None
+        if self.reducer is not None and self.engine.side is not None:
+            self.reducer.producers.append(self.engine.side)
         self._progress = None
         self.engine.refresh_weights()
 

@@ -16,7 +16,9 @@ for MI355X:
     views (a flat buffer in the trainer), so no autograd graph or aten kernel runs per op.
 Parameters are referenced by the reference's state-dict keys.
 """
+import contextlib
 import math
+import os
 
 import torch
 
@@ -82,6 +84,8 @@ class PackPlan:
         (into a reserved matrix at row row0 / column col0 when `into` is given)."""
         n = (rows or O) * KH * KW * Ipad
         dst_ld = 0
+        assert Ipad % 8 == 0, "pack_kernel writes 8 bf16 (16 bytes) per thread"
+        assert KH * KW * (Ipad + 8) <= 16384, "pack_kernel stages one destination row in 32 KiB of LDS"
         if into is None:
             off = self.total
             self.total += (n + 63) // 64 * 64
@@ -91,6 +95,7 @@ class PackPlan:
             base, _, width = self.views[into]
             dst_off = base + row0 * width + col0
             dst_ld = width if width != KH * KW * Ipad else 0
+            assert width % 8 == 0 and (row0 * width + col0) % 8 == 0, "16-byte aligned pack destination"
         self.items.append(dict(src=src, dst_off=dst_off, O=O, I=I, Ipad=Ipad, KH=KH, KW=KW, so=so, si=si, skh=skh,
                                skw=skw, kh_off=kh_off, kh_mul=kh_mul, kw_off=kw_off, kw_mul=kw_mul, dst_ld=dst_ld))
 
@@ -111,8 +116,8 @@ class PackPlan:
             d.so, d.si, d.skh, d.skw = it["so"], it["si"], it["skh"], it["skw"]
             for f in ("O", "I", "Ipad", "KH", "KW", "kh_off", "kh_mul", "kw_off", "kw_mul", "dst_ld"):
                 setattr(d, f, it[f])
-            n = it["O"] * it["KH"] * it["KW"] * it["Ipad"]
-            bmap += [(j, c) for c in range((n + chunk - 1) // chunk)]
+            row = it["KH"] * it["KW"] * it["Ipad"]
+            bmap += [(j, o) for o in range(0, it["O"], max(1, chunk // row))]
         raw = bytes(descs)
         self.desc_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self.bmap_dev = torch.tensor(bmap, dtype=torch.int32).reshape(-1).to(self.device)
@@ -200,6 +205,11 @@ class UNetEngine:
             self.temb_off[(p, l)] = off
             off += cout
         self.temb_total = off
+        # weight-gradient work (wgrad GEMMs, bias sums) runs on a side stream, overlapped with the
+        # data-gradient chain of the backward on the current stream
+        use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
+        self.side = torch.cuda.Stream(device=self.device) if use_side else None
+        self._keep = []
         self._build_pack()
 
     # ------------------------------------------------------------------------------------------
@@ -525,19 +535,21 @@ class UNetEngine:
         rc = f"{p}.residual_input_conv.{l}"
         dy, _ = grads.get(c["yn"])
         ldy = K.ld_of(dy)
-        K.conv_wgrad(dy, ldy, c["h2"], B, h, w, cout, cout, cout, 3, 3, 1, 1, self.g(b + ".2.weight"), h, w)
-        K.chan_sum(dy, B, Pn, cout, per_c=self.g(b + ".2.bias"), per_c2=self.g(rc + ".bias"))
+        with self._wg(dy):
+            K.conv_wgrad(dy, ldy, c["h2"], B, h, w, cout, cout, cout, 3, 3, 1, 1, self.g(b + ".2.weight"), h, w)
+            K.chan_sum(dy, B, Pn, cout, per_c=self.g(b + ".2.bias"), per_c2=self.g(rc + ".bias"))
+            K.linear_wgrad(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
         dh2 = self._new(B * Pn, cout)
         K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout)
-        K.linear_wgrad(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
         dx, fresh = grads.get(c["xn"])
         K.linear_dgrad(dy, self.W(f"{p}.res{l}#cat")[:, 9 * cout:], dx, resid=None if fresh else dx)
         K.gn_bwd(c["h1"], dh2, dh2, c["t2"], P[b + ".0.weight"], B, Pn, cout, G, True,
                  self.g(b + ".0.weight"), self.g(b + ".0.bias"))
         off = self.temb_off[(p, l)]
-        K.chan_sum(dh2, B, Pn, cout, per_bc=self.dtemb_all[:, off:off + cout], per_c=self.g(a + ".2.bias"),
-                   per_c2=self.g(f"{p}.t_emb_layers.{l}.1.bias"))
-        K.conv_wgrad(dh2, cout, c["h0"], B, h, w, cin, cin, cout, 3, 3, 1, 1, self.g(a + ".2.weight"), h, w)
+        with self._wg(dh2):
+            K.chan_sum(dh2, B, Pn, cout, per_bc=self.dtemb_all[:, off:off + cout], per_c=self.g(a + ".2.bias"),
+                       per_c2=self.g(f"{p}.t_emb_layers.{l}.1.bias"))
+            K.conv_wgrad(dh2, cout, c["h0"], B, h, w, cin, cin, cout, 3, 3, 1, 1, self.g(a + ".2.weight"), h, w)
         dh0 = self._new(B * Pn, cin)
         K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin)
         K.gn_bwd(c["x"], dh0, dx, c["t1"], P[a + ".0.weight"], B, Pn, cin, G, True,
@@ -584,8 +596,10 @@ class UNetEngine:
         C, B, N, mk, nk = c["C"], c["B"], c["N"], c["mk"], c["nk"]
         d = C // Hh
         dy, _ = grads.get(c["yn"])
-        K.linear_wgrad(dy, c["o"], self.g(mk + ".out_proj.weight"))
-        K.chan_sum(dy, 1, B * N, C, per_c=self.g(mk + ".out_proj.bias"))
+        with self._wg(dy):
+            K.linear_wgrad(dy, c["o"], self.g(mk + ".out_proj.weight"))
+            K.chan_sum(dy, 1, B * N, C, per_c=self.g(mk + ".out_proj.bias"))
+        dy_read = self.wg_event if self.side is not None else None
         do = self._new(B * N, C)
         K.linear_dgrad(dy, self.W(mk + ".out_proj#f"), do)
         Win = self.W(mk + ".in_proj_weight#f")
@@ -597,22 +611,25 @@ class UNetEngine:
             dqkv = self._new(B * N, 3 * C)
             K.attn_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], c["o"], do, c["lse"], dqkv[:, :C],
                        dqkv[:, C:2 * C], dqkv[:, 2 * C:], B, Hh, N, N, d)
-            K.linear_wgrad(dqkv, c["a"], gW)
-            K.chan_sum(dqkv, 1, B * N, 3 * C, per_c=gb)
+            with self._wg(dqkv):
+                K.linear_wgrad(dqkv, c["a"], gW)
+                K.chan_sum(dqkv, 1, B * N, 3 * C, per_c=gb)
             K.linear_dgrad(dqkv, Win, da)
         else:
             S, kv = c["S"], c["kv"]
             dq = self._new(B * N, C)
             dkv = self._new(B * S, 2 * C)
             K.attn_bwd(c["q"], kv[:, :C], kv[:, C:], c["o"], do, c["lse"], dq, dkv[:, :C], dkv[:, C:], B, Hh, N, S, d)
-            K.linear_wgrad(dq, c["a"], gW[:C])
-            K.chan_sum(dq, 1, B * N, C, per_c=gb[:C])
-            K.linear_wgrad(dkv, c["cp"], gW[C:])
-            K.chan_sum(dkv, 1, B * S, 2 * C, per_c=gb[C:])
+            with self._wg(dq, dkv):
+                K.linear_wgrad(dq, c["a"], gW[:C])
+                K.chan_sum(dq, 1, B * N, C, per_c=gb[:C])
+                K.linear_wgrad(dkv, c["cp"], gW[C:])
+                K.chan_sum(dkv, 1, B * S, 2 * C, per_c=gb[C:])
             dcp = self._new(B * S, C)
             K.linear_dgrad(dkv, Win[C:], dcp)
-            K.linear_wgrad(dcp, c["ctx"], self.g(c["ck"] + ".weight"))
-            K.chan_sum(dcp, 1, B * S, C, per_c=self.g(c["ck"] + ".bias"))
+            with self._wg(dcp):
+                K.linear_wgrad(dcp, c["ctx"], self.g(c["ck"] + ".weight"))
+                K.chan_sum(dcp, 1, B * S, C, per_c=self.g(c["ck"] + ".bias"))
             K.linear_dgrad(dq, Win[:C], da)
         # x receives dy (residual) + GroupNorm-branch gradient
         key, off, _ = grads.groups[c["xn"]]
@@ -620,6 +637,8 @@ class UNetEngine:
                 grads.shapes.get(key, (0, 0))[1] == C:
             grads.alias(c["xn"], dy)
             dx, addend = dy, dy
+            if dy_read is not None:  # the GroupNorm backward below rewrites dy in place
+                torch.cuda.current_stream(self.device).wait_event(dy_read)
         else:
             dx, fresh = grads.get(c["xn"])
             if not fresh:
@@ -643,9 +662,10 @@ class UNetEngine:
         key, C, B, h, w = c["key"], c["C"], c["B"], c["h"], c["w"]
         dy, _ = grads.get(c["yn"])
         ldy = K.ld_of(dy)
-        K.conv_wgrad(dy, ldy, c["x"], B, h, w, C, K.ld_of(c["x"]), C, 4, 4, 2, 1, self.g(key + ".weight"), h // 2,
-                     w // 2)
-        K.chan_sum(dy, B, (h // 2) * (w // 2), C, per_c=self.g(key + ".bias"))
+        with self._wg(dy):
+            K.conv_wgrad(dy, ldy, c["x"], B, h, w, C, K.ld_of(c["x"]), C, 4, 4, 2, 1, self.g(key + ".weight"),
+                         h // 2, w // 2)
+            K.chan_sum(dy, B, (h // 2) * (w // 2), C, per_c=self.g(key + ".bias"))
         dx, fresh = grads.get(c["xn"])
         wph = [self.W(f"{key}#d{ph}{pw}") for ph in range(2) for pw in range(2)]
         K.conv_dgrad_phases(dy, B, h, w, C, ldy, wph, C, dx, K.ld_of(dx), resid=None if fresh else dx,
@@ -663,11 +683,12 @@ class UNetEngine:
         dy, _ = grads.get(c["yn"])  # (B, 2h, 2w, C) slice of the concat gradient
         ldy = K.ld_of(dy)
         x = c["x"]
-        K.chan_sum(dy, B, 4 * h * w, C, per_c=self.g(key + ".bias"))
-        # dW[ci][co][kh][kw] = sum_{pixels of x} x[p][ci] * dy[2*iy-1+kh, 2*ix-1+kw][co]
-        g = K.conv_geom(2 * h, 2 * w, C, ldy, 4, 4, h, w, 2, 2, -1, -1)
-        K.gemm(C, 16 * C, B * h * w, x, _lib.A_COLMAJOR, K.ld_of(x), dy, _lib.B_KN_CONV, 0, self.g(key + ".weight"),
-               16 * C, geom=g, perm=(C, 16))
+        with self._wg(dy):
+            K.chan_sum(dy, B, 4 * h * w, C, per_c=self.g(key + ".bias"))
+            # dW[ci][co][kh][kw] = sum_{pixels of x} x[p][ci] * dy[2*iy-1+kh, 2*ix-1+kw][co]
+            g = K.conv_geom(2 * h, 2 * w, C, ldy, 4, 4, h, w, 2, 2, -1, -1)
+            K.gemm(C, 16 * C, B * h * w, x, _lib.A_COLMAJOR, K.ld_of(x), dy, _lib.B_KN_CONV, 0,
+                   self.g(key + ".weight"), 16 * C, geom=g, perm=(C, 16))
         dx, fresh = grads.get(c["xn"])
         K.conv_fwd(dy, B, 2 * h, 2 * w, C, ldy, self.W(key + "#d"), C, 4, 4, 2, 1, dx, K.ld_of(dx),
                    resid=None if fresh else dx, ldr=K.ld_of(dx))
@@ -684,9 +705,10 @@ class UNetEngine:
         C = self.L["conv_out"]
         Pn = H * W
         dpred = self.dpred
-        K.conv_wgrad(dpred, 8, c["hs"], B, H, W, C, C, 8, 3, 3, 1, 1, self.g("conv_out.weight"), H, W,
-                     m_store=self.im_channels)
-        K.chan_sum(dpred, B, Pn, 8, per_c=self.g("conv_out.bias"), c_store=self.im_channels)
+        with self._wg(dpred):
+            K.conv_wgrad(dpred, 8, c["hs"], B, H, W, C, C, 8, 3, 3, 1, 1, self.g("conv_out.weight"), H, W,
+                         m_store=self.im_channels)
+            K.chan_sum(dpred, B, Pn, 8, per_c=self.g("conv_out.bias"), c_store=self.im_channels)
         dhs = self._new(B * Pn, C)
         K.conv_fwd(dpred, B, H, W, 8, 8, self.W("conv_out#d"), C, 3, 3, 1, 1, dhs, C)
         dx, fresh = grads.get(c["xn"])
@@ -700,9 +722,10 @@ class UNetEngine:
         ldy = K.ld_of(dy)
         C0 = L["down"][0]
         cin_real = self.im_channels + (L["im_out"] if L["image"] else 0)
-        K.conv_wgrad(dy, ldy, c["xin"], B, H, W, self.cin_pad, self.cin_pad, C0, 3, 3, 1, 1,
-                     self.g(self.first + ".weight"), H, W, cvalid=cin_real)
-        K.chan_sum(dy, B, H * W, C0, per_c=self.g(self.first + ".bias"))
+        with self._wg(dy):
+            K.conv_wgrad(dy, ldy, c["xin"], B, H, W, self.cin_pad, self.cin_pad, C0, 3, 3, 1, 1,
+                         self.g(self.first + ".weight"), H, W, cvalid=cin_real)
+            K.chan_sum(dy, B, H * W, C0, per_c=self.g(self.first + ".bias"))
         if L["image"]:
             dxin = self._new(B * H * W, self.cin_pad)
             K.conv_fwd(dy, B, H, W, C0, ldy, self.W(self.first + "#d"), self.cin_pad, 3, 3, 1, 1, dxin, self.cin_pad)
@@ -716,6 +739,7 @@ class UNetEngine:
     def _bwd_time(self, c, grads):
         P, L = self.P, self.L
         B, T = c["B"], L["T"]
+        self._join()  # dtemb_all is filled by the resnets' side-stream bias sums
         d_all = self.dtemb_all
         # t_emb_layers weights are contiguous in the gradient store: one GEMM for all of them
         K.linear_wgrad(d_all, c["stemb"], self.temb_grad_all)
@@ -732,6 +756,28 @@ class UNetEngine:
         _lib.check(lib.sdmi_silu(c["h1"].data_ptr(), ds1.data_ptr(), dh1.data_ptr(), B * T, K._stream()), "silu")
         K.linear_wgrad(dh1, c["e"], self.g("t_proj.0.weight"))
         K.chan_sum(dh1, 1, B, T, per_c=self.g("t_proj.0.bias"))
+
+    # ------------------------------------------------------------------------------------------
+    @contextlib.contextmanager
+    def _wg(self, *keep):
+        """Weight-gradient work: issued on the side stream after everything issued so far on the current
+        stream. `keep` pins the operand tensors until the backward's final join, so the caching
+        allocator cannot hand their memory to the current stream while the side stream still reads it.
+        The block's completion event is left in self.wg_event."""
+        if self.side is None:
+            yield
+            return
+        self._keep.extend(keep)
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            yield
+        self.wg_event = torch.cuda.Event()
+        self.wg_event.record(self.side)
+
+    def _join(self):
+        """The current stream waits for all weight-gradient work issued so far."""
+        if self.side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
 
     # ------------------------------------------------------------------------------------------
     def backward(self, ctx, dpred, grads=None, on_progress=None):
@@ -752,6 +798,8 @@ class UNetEngine:
             fn(c, grads)
             if on_progress is not None:
                 on_progress(tape, k)
+        self._join()
+        self._keep = []
         self.dpred = None
 
     def _temb_grad_view(self):
