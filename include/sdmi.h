@@ -105,7 +105,9 @@ int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v,
  * GroupNorm (+ fused SiLU) on NHWC bf16 x[b][p][c] = x[(b*P + p)*ld + c]; fp32 statistics.
  * Replaces nn.GroupNorm -> nn.SiLU (models/blocks.py:45-47, 64-66; unet_cond_base.py:179-180) and the
  * attention pre-norms on the (B, C, HW) view (blocks.py:124-126, 137-139).  ws: sdmi_chan_reduce_workspace
- * bytes.  sdmi_gn_bwd: dx (+= addend if given), dgamma/dbeta (fp32, may be NULL), table2_ws fp32 [B*C*4].
+ * bytes (unused by sdmi_gn_stats).  Each reduction is one launch; batch sums (dgamma/dbeta, per-c sums) are
+ * finished in-kernel by the last workgroup of each channel strip.
+ * sdmi_gn_bwd: dx (+= addend if given), dgamma/dbeta (fp32, both or neither), table2_ws fp32 [B*C*4].
  * sdmi_chan_sum: per-(b,c) pixel sums (bf16, row stride ld_bc) and per-channel sums (fp32; c < c_store),
  * i.e. the bias and time-embedding-bias gradients of the convs at blocks.py:48-61, 102-107.
  * ------------------------------------------------------------------------------------------- */

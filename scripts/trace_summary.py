@@ -28,6 +28,34 @@ def main():
     t1 = int(step[-1]["End_Timestamp"])
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in step)
     print(f"step span {(t1 - t0) / 1e6:.3f} ms, kernel busy {busy / 1e6:.3f} ms, {len(step)} dispatches")
+    per_stream = {}
+    for r in step:
+        k = r.get("Stream_Id", r.get("Queue_Id"))
+        a = per_stream.setdefault(k, [0, 0])
+        a[0] += 1
+        a[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    for k, (c, t) in sorted(per_stream.items(), key=lambda kv: -kv[1][1]):
+        print(f"  stream {k}: {c} dispatches, busy {t / 1e6:.3f} ms")
+    # union of busy intervals = time at least one kernel runs
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in step)
+    union, cs, ce = 0, iv[0][0], iv[0][1]
+    for s0, e0 in iv[1:]:
+        if s0 > ce:
+            union += ce - cs
+            cs, ce = s0, e0
+        else:
+            ce = max(ce, e0)
+    union += ce - cs
+    print(f"  GPU busy (any stream) {union / 1e6:.3f} ms")
+    # phases on the issuing stream: forward = before the loss kernel, backward, optimizer = from sumsq on
+    names = [r["Kernel_Name"] for r in step]
+    i_mse = next((i for i, n in enumerate(names) if "mse_kernel" in n), None)
+    i_opt = next((i for i, n in enumerate(names) if "sumsq_kernel" in n), None)
+    if i_mse is not None and i_opt is not None:
+        def span_busy(a, b):
+            return sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in step[a:b])
+        print(f"  phases (kernel busy): forward {span_busy(0, i_mse) / 1e6:.3f} ms, "
+              f"backward {span_busy(i_mse, i_opt) / 1e6:.3f} ms, optimizer+pack {span_busy(i_opt, len(step)) / 1e6:.3f} ms")
     groups = {}
     for r in step:
         wg = int(r["Workgroup_Size_X"])

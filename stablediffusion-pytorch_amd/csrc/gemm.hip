@@ -868,10 +868,15 @@ int plan_splits(const sdmi_gemm_desc* d) {
   static int policy = -1;
   if (policy < 0) {
     const char* e = getenv("SDMI_SPLIT_POLICY");
-    policy = e ? atoi(e) : 1;
+    policy = e ? atoi(e) : 0;
   }
   if (policy == 0) {  // shallow: >= 8 k-tiles per slice, at most 16 slices
     while (tiles * s < 384 && nkt / (s * 2) >= 8 && s < 16) s *= 2;
+    return s;
+  }
+  if (policy == 2) return 1;
+  if (policy == 3) {  // only for grids far below the CU count, >= 16 k-tiles per slice
+    while (tiles * s < 128 && nkt / (s * 2) >= 16 && s < 32) s *= 2;
     return s;
   }
   // fill the 256 CUs: deep split-K for the small-output / long-K weight gradients (a 128 x 128 dW over

@@ -2,235 +2,257 @@
 //
 // Replaces nn.GroupNorm(32, C) -> nn.SiLU() (models/blocks.py:45-47, 64-66 and the Mid/Up copies),
 // the attention pre-norms on the (B, C, HW) view (blocks.py:124-126, 137-139: same statistics as
-// 4-D) and unet_cond_base.py:179-180. Statistics are fp32 (partials) / fp64 (final merge), eps 1e-5.
+// 4-D) and unet_cond_base.py:179-180. Statistics: fp32 per-thread / per-channel sums, fp64 group merge,
+// eps 1e-5.
 //
 // All kernels see an activation as x[b][p][c] = x[(b*P + p)*ld + c], P = H*W pixels.
-//  1. sdmi_chan_reduce  : per (b, c) partial sums over a pixel slice (grid = B x splits):
-//        mode 0: (sum x, sum x^2)                                   -> GN statistics
-//        mode 1: (sum dz, sum dz*xhat), dz = dy [* silu'(z)]          -> GN backward
-//        mode 2: (sum dy, 0)                                         -> bias / time-embedding grads
-//  2. finalize kernels turn partials into mean/rstd, GN backward coefficients, dgamma/dbeta, bias grads.
-//  3. sdmi_gn_apply / sdmi_gn_bwd_apply : vectorised elementwise passes (8 channels per lane).
+// Reductions run as ONE launch each: a workgroup owns a channel strip of one batch row (for GroupNorm a
+// strip of whole groups) and reduces all of its pixels, so per-(b, c) and per-(b, g) results come out
+// of the workgroup directly. Sums over the batch (dgamma/dbeta, bias gradients) are finished by the
+// last-arriving workgroup of each strip: rows are published with device-coherent (sc1) stores and a
+// relaxed device-scope arrival counter, so no L2 write-back fence is needed.
+//   sdmi_gn_stats     : table {a = rstd*gamma, s = beta - mean*a, mean, rstd} per (b, c)
+//   sdmi_gn_bwd       : (sum dz, sum dz*xhat) -> table2 {a, s, q, o} + dgamma/dbeta, then the apply pass
+//   sdmi_chan_sum     : per-(b, c) and per-c sums of dy (bias / time-embedding gradients)
+//   sdmi_gn_apply / gn_bwd_apply : vectorised elementwise passes (8 channels per lane).
+#include <atomic>
+
 #include "common.h"
 #include "../../include/sdmi.h"
 
 namespace {
 
 constexpr int NT = 256;
+constexpr int NSLOTS = 4096;      // counter slots, one per launch, round-robin
+constexpr int SLOT_CTRS = 128;    // strips per launch
+__device__ unsigned g_norm_counters[NSLOTS * SLOT_CTRS];  // zero at load; the last arriver re-arms
 
-struct RedArgs {
-  const bf16_t* x; int ldx;   // GN input
-  const bf16_t* dy; int ldy;  // upstream grad (modes 1, 2)
-  const float4* tab;          // mode 1: per-(b,c) {a = rstd*gamma, s = beta - mean*a, mean, rstd}
-  int B, P, C, G, silu, mode, splits;
-  float* part;  // [B][splits][C][2]
+struct StripArgs {
+  const bf16_t* x; int ldx;   // GN input (modes 0, 1)
+  const bf16_t* dy; int ldy;  // upstream gradient (modes 1, 2)
+  const float4* tab;          // mode 1: forward table
+  int B, P, C, G, CW, silu;
+  float eps;
+  const float* gamma; const float* beta;
+  float4* out_tab;            // mode 0: table, mode 1: table2
+  float* rows;                // [nb][C][2] per-row sums for the batch tail (sc1 stores)
+  unsigned* ctr;              // [nchunks] arrival counters
+  float* sum1; float* sum2;   // batch tail outputs: mode 1 dbeta/dgamma, mode 2 per_c/per_c2
+  bf16_t* per_bc; int ld_bc;  // mode 2
+  int c_store;
+  long long seg;              // mode 2: rows per (virtual) batch row; 0 = P
+  int nb;                     // batch rows (virtual for mode 2)
 };
 
-__global__ __launch_bounds__(NT) void chan_reduce_kernel(RedArgs a) {
-  const int b = blockIdx.x, sp = blockIdx.y;
-  const int C8 = a.C >> 3;
-  const int rows = NT / C8;  // pixel rows processed per iteration
-  const int t = threadIdx.x;
-  const int col = t % C8, r = t / C8;
-  const bool active = r < rows;
-  const int p_per = (a.P + a.splits - 1) / a.splits;
-  const int p0 = sp * p_per, p1 = min(a.P, p0 + p_per);
-  const int c0 = col * 8;
-  const int Cg = a.C / a.G;
+__device__ __forceinline__ void st_coherent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_coherent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-  float s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-  float4 tb[8];
-  if (a.mode == 1) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) tb[e] = a.tab[(long long)b * a.C + c0 + e];
+// true in every thread of the workgroup that arrives last among n at *ctr (which it re-arms)
+__device__ __forceinline__ bool arrive_last(unsigned* ctr, int n) {
+  __shared__ int flag;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's coherent row stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (unsigned)(n - 1);
+    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag = last;
   }
-  (void)Cg;
-  if (active) {
-    for (int p = p0 + r; p < p1; p += rows) {
-      long long pix = (long long)b * a.P + p;
-      float xv[8], gv[8];
-      if (a.mode == 0) {
-        unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
+  __syncthreads();
+  return flag != 0;
+}
+
+// Per-channel sums over rows [row0, row0 + nrows) of the strip [c0, c0 + cw) -> s1[cw], s2[cw] in LDS.
+// mode 0: (x, x^2); mode 1: (dz, dz*xhat) with dz = dy [* silu'(x*a + s)]; mode 2: (dy, -).
+template <int MODE>
+__device__ __forceinline__ void strip_reduce(const StripArgs& a, int b, long long row0, long long nrows, int c0, int cw,
+                                             float* s1, float* s2) {
+  __shared__ float red[NT][17];
+  const int L = cw >> 3;            // lanes per pixel row
+  const int R = NT / L;             // pixel rows per iteration
+  const int t = threadIdx.x;
+  const int lane = t % L, r = t / L;
+  const int cc = c0 + lane * 8;
+  float u[8], v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { s1[e] += xv[e]; s2[e] += xv[e] * xv[e]; }
-      } else if (a.mode == 1) {
-        unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
-        unpack8(*(const uint4*)(a.dy + pix * a.ldy + c0), gv);
+  for (int e = 0; e < 8; ++e) { u[e] = 0.f; v[e] = 0.f; }
+  float4 tb[8];
+  if (MODE == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) tb[e] = r < R ? a.tab[(long long)b * a.C + cc + e] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (r < R) {
+#pragma unroll 2
+    for (long long p = r; p < nrows; p += R) {
+      const long long row = row0 + p;
+      float xv[8], gv[8];
+      if (MODE == 0) {
+        unpack8(*(const uint4*)(a.x + row * a.ldx + cc), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { u[e] += xv[e]; v[e] = fmaf(xv[e], xv[e], v[e]); }
+      } else if (MODE == 1) {
+        unpack8(*(const uint4*)(a.x + row * a.ldx + cc), xv);
+        unpack8(*(const uint4*)(a.dy + row * a.ldy + cc), gv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float xh = (xv[e] - tb[e].z) * tb[e].w;
           float dz = gv[e];
           if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb[e].x, tb[e].y));
-          s1[e] += dz;
-          s2[e] += dz * xh;
+          u[e] += dz;
+          v[e] = fmaf(dz, (xv[e] - tb[e].z) * tb[e].w, v[e]);
         }
       } else {
-        unpack8(*(const uint4*)(a.dy + pix * a.ldy + c0), gv);
+        unpack8(*(const uint4*)(a.dy + row * a.ldy + cc), gv);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s1[e] += gv[e];
+        for (int e = 0; e < 8; ++e) u[e] += gv[e];
       }
     }
   }
-  // reduce across the `rows` threads sharing a column
-  __shared__ float red[NT][17];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { red[t][e] = s1[e]; red[t][8 + e] = s2[e]; }
+  for (int e = 0; e < 8; ++e) { red[t][e] = u[e]; red[t][8 + e] = v[e]; }
   __syncthreads();
-  // thread j < C (channel) sums over rows
-  for (int ch = t; ch < a.C; ch += NT) {
-    int cc = ch >> 3, e = ch & 7;
-    float u = 0.f, v = 0.f;
-    for (int rr = 0; rr < rows; ++rr) {
-      u += red[rr * C8 + cc][e];
-      v += red[rr * C8 + cc][8 + e];
+  for (int ch = t; ch < cw; ch += NT) {
+    const int l = ch >> 3, e = ch & 7;
+    float x1 = 0.f, x2 = 0.f;
+    for (int rr = 0; rr < R; ++rr) {
+      x1 += red[rr * L + l][e];
+      x2 += red[rr * L + l][8 + e];
     }
-    float* o = a.part + (((long long)b * a.splits + sp) * a.C + ch) * 2;
-    o[0] = u;
-    o[1] = v;
-  }
-}
-
-// ---- finalize kernels: partials [B][splits][C][2] -> per-(b,c) / per-(b,g) / per-c results ----
-
-// column sums over all (b, split) rows for 64 channels [c0, c0+64): 256 threads = 64 channels x 4 row groups
-__device__ __forceinline__ void colsum64(const float* part, int rows, int C, int c0, float& u, float& v, bool& own) {
-  __shared__ float red[4][64][2];
-  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-  const int c = c0 + cx;
-  float a = 0.f, b = 0.f;
-  if (c < C) {
-    int r = ry;
-    for (; r + 28 < rows; r += 32) {  // 8 independent loads in flight per lane
-      float2 v2[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v2[j] = *(const float2*)(part + ((long long)(r + 4 * j) * C + c) * 2);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { a += v2[j].x; b += v2[j].y; }
-    }
-    for (; r < rows; r += 4) {
-      const float2 v2 = *(const float2*)(part + ((long long)r * C + c) * 2);
-      a += v2.x;
-      b += v2.y;
-    }
-  }
-  red[ry][cx][0] = a;
-  red[ry][cx][1] = b;
-  __syncthreads();
-  own = ry == 0 && c < C;
-  u = red[0][cx][0] + red[1][cx][0] + red[2][cx][0] + red[3][cx][0];
-  v = red[0][cx][1] + red[1][cx][1] + red[2][cx][1] + red[3][cx][1];
-}
-
-// per-channel totals of one batch row b over the splits, into LDS (C <= 2048)
-__device__ __forceinline__ void batch_totals(const float* part, int b, int splits, int C, float2* tot) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a = 0.f, d = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
-      const float2 v2 = *(const float2*)(part + (((long long)b * splits + sp) * C + c) * 2);
-      a += v2.x;
-      d += v2.y;
-    }
-    tot[c] = make_float2(a, d);
+    s1[ch] = x1;
+    s2[ch] = x2;
   }
   __syncthreads();
 }
 
-// mean/rstd per (b, g): one block per b
-__global__ __launch_bounds__(256) void gn_stats_finalize_kernel(const float* part, int B, int splits, int C, int G,
-                                                                int P, float eps, const float* gamma,
-                                                                const float* beta, float4* tab) {
-  __shared__ float2 tot[2048];
-  __shared__ float2 grp[2048];
-  const int b = blockIdx.x;
-  batch_totals(part, b, splits, C, tot);
-  const int Cg = C / G;
-  for (int g = threadIdx.x; g < G; g += blockDim.x) {
-    double s1 = 0, s2 = 0;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-      s1 += tot[c].x;
-      s2 += tot[c].y;
+// Last strip of a batch column: out1[c] = sum_b rows[b][c][0], out2[c] = sum_b rows[b][c][1] for the strip.
+__device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, float* o1, float* o2, int c_store,
+                                           bool dup = false) {
+  __shared__ float acc[NT][2];
+  const int t = threadIdx.x;
+  const int nbg = max(1, NT / cw);
+  const int ch = t % cw, bg = t / cw;
+  float x1 = 0.f, x2 = 0.f;
+  if (bg < nbg && t < nbg * cw) {
+#pragma unroll 4
+    for (int b = bg; b < a.nb; b += nbg) {
+      const float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
+      x1 += ld_coherent(rp);
+      x2 += ld_coherent(rp + 1);
     }
-    double n = (double)P * Cg;
-    double mu = s1 / n;
-    double var = s2 / n - mu * mu;
+  }
+  acc[t][0] = x1;
+  acc[t][1] = x2;
+  __syncthreads();
+  if (t < cw) {
+    float y1 = 0.f, y2 = 0.f;
+    for (int g = 0; g < nbg; ++g) {
+      y1 += acc[g * cw + t][0];
+      y2 += acc[g * cw + t][1];
+    }
+    const int c = c0 + t;
+    if (c < c_store) {
+      if (o1) o1[c] = y1;
+      if (o2) o2[c] = dup ? y1 : y2;
+    }
+  }
+}
+
+// grid (nchunks, B): GroupNorm statistics of whole groups -> forward table
+__global__ __launch_bounds__(NT) void gn_stats_kernel(StripArgs a) {
+  __shared__ float s1[NT], s2[NT];
+  __shared__ float2 grp[NT];
+  const int b = blockIdx.y;
+  const int c0 = blockIdx.x * a.CW;
+  const int cw = min(a.CW, a.C - c0);
+  const int Cg = a.C / a.G;
+  strip_reduce<0>(a, b, (long long)b * a.P, a.P, c0, cw, s1, s2);
+  const int ng = cw / Cg;
+  if ((int)threadIdx.x < ng) {
+    double m1 = 0, m2 = 0;
+    for (int c = threadIdx.x * Cg; c < (int)(threadIdx.x + 1) * Cg; ++c) {
+      m1 += s1[c];
+      m2 += s2[c];
+    }
+    const double n = (double)a.P * Cg;
+    const double mu = m1 / n;
+    double var = m2 / n - mu * mu;
     if (var < 0) var = 0;
-    grp[g] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)eps)));
+    grp[threadIdx.x] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)a.eps)));
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float2 mr = grp[c / Cg];
-    float a = mr.y * gamma[c];
-    tab[(long long)b * C + c] = make_float4(a, beta[c] - mr.x * a, mr.x, mr.y);
+  for (int ch = threadIdx.x; ch < cw; ch += NT) {
+    const int c = c0 + ch;
+    const float2 mr = grp[ch / Cg];
+    const float sc = mr.y * a.gamma[c];
+    a.out_tab[(long long)b * a.C + c] = make_float4(sc, a.beta[c] - mr.x * sc, mr.x, mr.y);
   }
 }
 
-// GN backward: blocks [0, B): coef[b][g] = (sum_c gamma_c S1[b,c], sum_c gamma_c S2[b,c]);
-// blocks [B, B + ceil(C/64)): dbeta[c] = sum_b S1, dgamma[c] = sum_b S2.
+// grid (nchunks, B): GroupNorm backward coefficients -> table2 {a, s, q, o}; dgamma/dbeta by the batch tail.
 // dx = rstd*(dz*gamma - A/n - xhat*Bc/n) = a*dz + q*x + o with q = -rstd^2 Bc/n, o = rstd^2 mean Bc/n - rstd A/n
-__global__ __launch_bounds__(256) void gn_bwd_finalize_kernel(const float* part, int B, int splits, int C, int G,
-                                                              int P, const float* gamma, const float4* tab,
-                                                              float4* tab2, float* dgamma, float* dbeta) {
-  if ((int)blockIdx.x < B) {
-    __shared__ float2 tot[2048];
-    __shared__ float2 grp[2048];
-    const int b = blockIdx.x;
-    batch_totals(part, b, splits, C, tot);
-    const int Cg = C / G;
-    const float inv_n = 1.0f / ((float)P * Cg);
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
-      float A = 0.f, Bc = 0.f;
-      for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
-        A += gamma[c] * tot[c].x;
-        Bc += gamma[c] * tot[c].y;
-      }
-      float4 t = tab[(long long)b * C + g * Cg];
-      float r = t.w, mu = t.z;
-      grp[g] = make_float2(-r * r * Bc * inv_n, r * r * mu * Bc * inv_n - r * A * inv_n);
+__global__ __launch_bounds__(NT) void gn_bwd_reduce_kernel(StripArgs a) {
+  __shared__ float s1[NT], s2[NT];
+  __shared__ float2 grp[NT];
+  const int b = blockIdx.y;
+  const int c0 = blockIdx.x * a.CW;
+  const int cw = min(a.CW, a.C - c0);
+  const int Cg = a.C / a.G;
+  strip_reduce<1>(a, b, (long long)b * a.P, a.P, c0, cw, s1, s2);
+  const int ng = cw / Cg;
+  const float inv_n = 1.0f / ((float)a.P * Cg);
+  if ((int)threadIdx.x < ng) {
+    float A = 0.f, Bc = 0.f;
+    for (int ch = threadIdx.x * Cg; ch < (int)(threadIdx.x + 1) * Cg; ++ch) {
+      A += a.gamma[c0 + ch] * s1[ch];
+      Bc += a.gamma[c0 + ch] * s2[ch];
     }
-    __syncthreads();
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      float4 t = tab[(long long)b * C + c];
-      float2 qo = grp[c / Cg];
-      tab2[(long long)b * C + c] = make_float4(t.x, t.y, qo.x, qo.y);
+    const float4 t = a.tab[(long long)b * a.C + c0 + threadIdx.x * Cg];
+    const float r = t.w, mu = t.z;
+    grp[threadIdx.x] = make_float2(-r * r * Bc * inv_n, r * r * mu * Bc * inv_n - r * A * inv_n);
+  }
+  __syncthreads();
+  for (int ch = threadIdx.x; ch < cw; ch += NT) {
+    const int c = c0 + ch;
+    const float4 t = a.tab[(long long)b * a.C + c];
+    const float2 qo = grp[ch / Cg];
+    a.out_tab[(long long)b * a.C + c] = make_float4(t.x, t.y, qo.x, qo.y);
+    if (a.sum1) {
+      float* rp = a.rows + ((long long)b * a.C + c) * 2;
+      st_coherent(rp, s1[ch]);
+      st_coherent(rp + 1, s2[ch]);
     }
-    return;
   }
-  float u, v;
-  bool own;
-  const int c0 = ((int)blockIdx.x - B) * 64;
-  colsum64(part, B * splits, C, c0, u, v, own);
-  if (own && dgamma) {
-    dbeta[c0 + (threadIdx.x & 63)] = u;
-    dgamma[c0 + (threadIdx.x & 63)] = v;
-  }
+  if (!a.sum1) return;
+  if (!arrive_last(a.ctr + blockIdx.x, a.nb)) return;
+  batch_tail(a, c0, cw, a.sum1, a.sum2, a.C);
 }
 
-// per-(b,c) sums (mode 2): blocks [0, nbc) write per_bc[b*ld + c] (bf16); blocks [nbc, nbc + ceil(C/64)) write
-// per_c[c] = per_c2[c] = sum_b for c < c_store (fp32)
-__global__ __launch_bounds__(256) void chan_sum_finalize_kernel(const float* part, int B, int splits, int C,
-                                                                bf16_t* per_bc, int ld, float* per_c, float* per_c2,
-                                                                int c_store, int nbc) {
-  if ((int)blockIdx.x < nbc) {
-    int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx < B * C) {
-      int b = idx / C, c = idx - b * C;
-      float u = 0.f;
-      for (int sp = 0; sp < splits; ++sp) u += part[(((long long)b * splits + sp) * C + c) * 2];
-      per_bc[(long long)b * ld + c] = f2bf(u);
+// grid (nchunks, nb): per-(row, c) sums of dy -> per_bc (bf16), per-c sums by the batch tail
+__global__ __launch_bounds__(NT) void chan_sum_kernel(StripArgs a) {
+  __shared__ float s1[NT], s2[NT];
+  const int b = blockIdx.y;
+  const int c0 = blockIdx.x * a.CW;
+  const int cw = min(a.CW, a.C - c0);
+  const long long total = (long long)a.B * a.P;
+  const long long row0 = (long long)b * a.seg;
+  const long long nrows = max(0LL, min(a.seg, total - row0));
+  strip_reduce<2>(a, b, row0, nrows, c0, cw, s1, s2);
+  const bool tail = a.sum1 || a.sum2;
+  for (int ch = threadIdx.x; ch < cw; ch += NT) {
+    const int c = c0 + ch;
+    if (a.per_bc) a.per_bc[(long long)b * a.ld_bc + c] = f2bf(s1[ch]);
+    if (tail) {
+      float* rp = a.rows + ((long long)b * a.C + c) * 2;
+      st_coherent(rp, s1[ch]);
+      st_coherent(rp + 1, 0.f);
     }
-    return;
   }
-  float u, v;
-  bool own;
-  const int c0 = ((int)blockIdx.x - nbc) * 64;
-  colsum64(part, B * splits, C, c0, u, v, own);
-  const int c = c0 + (threadIdx.x & 63);
-  if (own && c < c_store) {
-    if (per_c) per_c[c] = u;
-    if (per_c2) per_c2[c] = u;
-  }
+  if (!tail) return;
+  if (!arrive_last(a.ctr + blockIdx.x, a.nb)) return;
+  batch_tail(a, c0, cw, a.sum1, a.sum2, a.c_store, /*dup=*/true);  // per_c2: a second bias with the same gradient
 }
 
 struct ApplyArgs {
@@ -289,35 +311,51 @@ __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
   }
 }
 
-int pick_splits(int B, int P) {
-  int s = 1;
-  while (B * s < 1024 && P / (s * 2) >= 16) s *= 2;
-  return s;
-}
-
 int grid_for(long long work) {
   long long g = (work + NT - 1) / NT;
   return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
 }
 
+// Strip width: a multiple of `unit` (whole groups) and of 8 channels, at least 64 channels when C allows
+// (narrower strips measured slower: 16-byte row segments coalesce poorly).
+int strip_width(int C, int unit) {
+  int cw = unit;
+  while (cw % 8 || (cw < 64 && cw * 2 <= C)) cw += unit;
+  while ((C + cw - 1) / cw > SLOT_CTRS) cw += unit;
+  return cw;
+}
+
+unsigned* counter_slot() {
+  static std::atomic<unsigned> next{0};
+  static unsigned* base[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_norm_counters)) != hipSuccess) return nullptr;
+    base[dev] = (unsigned*)p;
+  }
+  return base[dev] + (size_t)(next.fetch_add(1) % NSLOTS) * SLOT_CTRS;
+}
+
 }  // namespace
 
 extern "C" size_t sdmi_chan_reduce_workspace(int B, int P, int C) {
-  return (size_t)B * pick_splits(B, P) * C * 2 * sizeof(float);
+  (void)P;
+  return (size_t)(B > 32 ? B : 32) * C * 2 * sizeof(float);
 }
 
 // stats -> per-(b,c) table {a = rstd*gamma, s = beta - mean*a, mean, rstd} (fp32 float4 [B][C])
 extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, const float* gamma,
                              const float* beta, float* ws, float* table, sdmi_stream_t stream) {
-  if (C % 8 || C > 8 * NT || G <= 0 || C % G) return -1;
-  hipStream_t s = (hipStream_t)stream;
-  RedArgs a = {};
-  a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.mode = 0;
-  a.splits = pick_splits(B, P); a.part = ws;
-  hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, a.splits), dim3(NT), 0, s, a);
-  SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gn_stats_finalize_kernel, dim3(B), dim3(256), 0, s, ws, B, a.splits, C, G, P, eps, gamma, beta,
-                     (float4*)table);
+  (void)ws;
+  if (C % 8 || G <= 0 || C % G) return -1;
+  StripArgs a = {};
+  a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.eps = eps;
+  a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table;
+  a.CW = strip_width(C, C / G);
+  if (a.CW > NT) return -2;
+  hipLaunchKernelGGL(gn_stats_kernel, dim3((C + a.CW - 1) / a.CW, B), dim3(NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -333,19 +371,22 @@ extern "C" int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const flo
   return 0;
 }
 
-// table: forward table from sdmi_gn_stats; table2_ws: float4 [B][C] scratch
+// table: forward table from sdmi_gn_stats; table2_ws: float4 [B][C] scratch; ws: sdmi_chan_reduce_workspace
 extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
                            const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws,
                            float* dgamma, float* dbeta, const void* addend, int ldadd, sdmi_stream_t stream) {
-  if (C % 8 || C > 8 * NT || C % G) return -1;
+  if (C % 8 || G <= 0 || C % G) return -1;
+  if ((dgamma == nullptr) != (dbeta == nullptr)) return -3;
   hipStream_t s = (hipStream_t)stream;
-  RedArgs r = {};
+  StripArgs r = {};
   r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy; r.tab = (const float4*)table;
-  r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.mode = 1; r.splits = pick_splits(B, P); r.part = ws;
-  hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, r.splits), dim3(NT), 0, s, r);
-  SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(B + (dgamma ? (C + 63) / 64 : 0)), dim3(256), 0, s, ws, B, r.splits,
-                     C, G, P, gamma, (const float4*)table, (float4*)table2_ws, dgamma, dbeta);
+  r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.gamma = gamma; r.out_tab = (float4*)table2_ws;
+  r.CW = strip_width(C, C / G);
+  const int nch = (C + r.CW - 1) / r.CW;
+  if (r.CW > NT || nch > SLOT_CTRS) return -2;
+  r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
+  if (dgamma && !(r.ctr = counter_slot())) return -4;
+  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(nch, B), dim3(NT), 0, s, r);
   SDMI_CHECK_LAUNCH();
   ApplyArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.dy = (const bf16_t*)dy; a.lddy = lddy; a.dx = (bf16_t*)dx; a.lddx = lddx;
@@ -360,18 +401,26 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
 extern "C" int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, float* ws, void* per_bc, int ld_bc,
                              float* per_c, float* per_c2, int c_store, sdmi_stream_t stream) {
   if (c_store <= 0 || c_store > C) c_store = C;
-  if (C % 8 || C > 8 * NT) return -1;
-  hipStream_t s = (hipStream_t)stream;
-  RedArgs r = {};
-  r.dy = (const bf16_t*)dy; r.ldy = lddy; r.B = B; r.P = P; r.C = C; r.G = 1; r.mode = 2;
-  r.splits = pick_splits(B, P); r.part = ws;
-  hipLaunchKernelGGL(chan_reduce_kernel, dim3(B, r.splits), dim3(NT), 0, s, r);
-  SDMI_CHECK_LAUNCH();
-  int nbc = per_bc ? (B * C + 255) / 256 : 0;
-  int ncol = (per_c || per_c2) ? (C + 63) / 64 : 0;
-  if (nbc + ncol == 0) return 0;
-  hipLaunchKernelGGL(chan_sum_finalize_kernel, dim3(nbc + ncol), dim3(256), 0, s, ws, B, r.splits, C, (bf16_t*)per_bc,
-                     ld_bc, per_c, per_c2, c_store, nbc);
+  if (C % 8 || B <= 0 || P <= 0) return -1;
+  StripArgs r = {};
+  r.dy = (const bf16_t*)dy; r.ldy = lddy; r.B = B; r.P = P; r.C = C;
+  r.per_bc = (bf16_t*)per_bc; r.ld_bc = ld_bc; r.c_store = c_store;
+  r.sum1 = per_c; r.sum2 = per_c2; r.rows = ws;
+  if (per_bc) {
+    r.nb = B;
+    r.seg = P;
+  } else {  // only batch totals: cut the B*P rows into <= 32 contiguous segments of >= 64 rows
+    const long long total = (long long)B * P;
+    long long nb = total / 64;
+    nb = nb < 1 ? 1 : (nb > 32 ? 32 : nb);
+    r.seg = (total + nb - 1) / nb;
+    r.nb = (int)((total + r.seg - 1) / r.seg);
+  }
+  r.CW = strip_width(C, 8);
+  const int nch = (C + r.CW - 1) / r.CW;
+  if (nch > SLOT_CTRS || r.CW > NT) return -2;
+  if ((per_c || per_c2) && !(r.ctr = counter_slot())) return -4;
+  hipLaunchKernelGGL(chan_sum_kernel, dim3(nch, r.nb), dim3(NT), 0, (hipStream_t)stream, r);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

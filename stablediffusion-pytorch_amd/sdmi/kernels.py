@@ -217,18 +217,10 @@ def gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, silu, dgamma, dbeta, addend=None):
 
 def chan_sum(dy, B, P, C, *, per_bc=None, per_c=None, per_c2=None, c_store=0):
     """per-(b,c) sums over pixels -> per_bc (bf16 2-D view [B, ld]) and per-channel sums (fp32)."""
-    if C > 1024:  # the reduction kernel covers <= 2048 channels per launch; split wide rows
-        for c0 in range(0, C, 1024):
-            c1 = min(C, c0 + 1024)
-            chan_sum(dy[:, c0:c1], B, P, c1 - c0,
-                     per_bc=per_bc[:, c0:c1] if per_bc is not None else None,
-                     per_c=per_c[c0:c1] if per_c is not None else None,
-                     per_c2=per_c2[c0:c1] if per_c2 is not None else None)
-        return
     L = _lib.lib()
     ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=dy.device)
     with _Prof("chan_sum", 0, f"B={B} P={P} C={C}"):
-      check(L.sdmi_chan_sum(_p(dy), ld_of(dy), B, P, C, _p(ws), _p(per_bc), ld_of(per_bc) if per_bc is not None else 0,
+        check(L.sdmi_chan_sum(_p(dy), ld_of(dy), B, P, C, _p(ws), _p(per_bc), ld_of(per_bc) if per_bc is not None else 0,
                           _p(per_c), _p(per_c2), c_store, _stream()), "sdmi_chan_sum")
 
 
