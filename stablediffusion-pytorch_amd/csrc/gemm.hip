@@ -745,7 +745,7 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
 __global__ void splitk_reduce_kernel(const EpiArgs g) {
   const float* ws = g.ws;
   long long stride = (long long)gridDim.x * blockDim.x;
-  if (g.vec) {
+  if (g.n8) {  // 16-B slab reads; permuted (weight-gradient) outputs store element-wise
     const int N8 = g.N >> 3;
     long long total = (long long)g.M * N8;
     for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
@@ -756,7 +756,12 @@ __global__ void splitk_reduce_kernel(const EpiArgs g) {
         const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
       }
-      if (row < g.m_store && col < g.n_store) Epi::finish8(g, row, col, v);
+      if (g.vec) {
+        if (row < g.m_store && col < g.n_store) Epi::finish8(g, row, col, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Epi::store_final(g, row, col + e, v[e]);
+      }
     }
     return;
   }
@@ -939,7 +944,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     red.nsplit = splits;
     red.split_stride = (long long)d->m * d->n;
     red.ws = (const float*)workspace;
-    long long total = (long long)d->m * d->n / (red.vec ? 8 : 1);
+    long long total = (long long)d->m * d->n / (red.n8 ? 8 : 1);
     int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, red);
     err = hipGetLastError();

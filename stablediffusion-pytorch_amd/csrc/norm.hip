@@ -23,8 +23,10 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int NSLOTS = 4096;      // counter slots, one per launch, round-robin
-constexpr int SLOT_CTRS = 128;    // strips per launch
+constexpr int NSLOTS = 2048;      // counter slots, one per launch, round-robin
+constexpr int SLOT_CTRS = 2048;   // [0, 1024): per (strip, b) pixel-split counters, [1024, 2048): per strip
+constexpr int BATCH_CTR = 1024;
+constexpr int PS_MAX = 8;         // pixel splits per (strip, b)
 __device__ unsigned g_norm_counters[NSLOTS * SLOT_CTRS];  // zero at load; the last arriver re-arms
 
 struct StripArgs {
@@ -36,6 +38,7 @@ struct StripArgs {
   const float* gamma; const float* beta;
   float4* out_tab;            // mode 0: table, mode 1: table2
   float* rows;                // [nb][C][2] per-row sums for the batch tail (sc1 stores)
+  float* part;                // [nb][psplit][C][2] pixel-split partials (sc1 stores)
   unsigned* ctr;              // [nchunks] arrival counters
   float* sum1; float* sum2;   // batch tail outputs: mode 1 dbeta/dgamma, mode 2 per_c/per_c2
   bf16_t* per_bc; int ld_bc;  // mode 2
@@ -160,6 +163,39 @@ __device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, f
   }
 }
 
+// Pixel-split combine: with gridDim.z > 1 every workgroup publishes its strip sums and the last of the
+// (strip, b) group continues with the complete sums in s1/s2; the others return false.
+__device__ __forceinline__ bool combine_psplits(const StripArgs& a, int b, int c0, int cw, float* s1, float* s2) {
+  const int nz = gridDim.z;
+  if (nz == 1) return true;
+  float* mine = a.part + (((long long)b * nz + blockIdx.z) * a.C + c0) * 2;
+  for (int ch = threadIdx.x; ch < cw; ch += NT) {
+    st_coherent(mine + 2 * ch, s1[ch]);
+    st_coherent(mine + 2 * ch + 1, s2[ch]);
+  }
+  if (!arrive_last(a.ctr + blockIdx.x * gridDim.y + b, nz)) return false;
+  for (int ch = threadIdx.x; ch < cw; ch += NT) {
+    float x1 = 0.f, x2 = 0.f;
+    const float* pp = a.part + ((long long)b * nz * a.C + c0 + ch) * 2;
+#pragma unroll 4
+    for (int z = 0; z < nz; ++z) {
+      x1 += ld_coherent(pp + (long long)z * a.C * 2);
+      x2 += ld_coherent(pp + (long long)z * a.C * 2 + 1);
+    }
+    s1[ch] = x1;
+    s2[ch] = x2;
+  }
+  __syncthreads();
+  return true;
+}
+
+__device__ __forceinline__ void pixel_range(long long n, long long& p0, long long& p1) {
+  const long long per = (n + gridDim.z - 1) / gridDim.z;
+  p0 = blockIdx.z * per;
+  p1 = min(n, p0 + per);
+  if (p1 < p0) p1 = p0;
+}
+
 // grid (nchunks, B): GroupNorm statistics of whole groups -> forward table
 __global__ __launch_bounds__(NT) void gn_stats_kernel(StripArgs a) {
   __shared__ float s1[NT], s2[NT];
@@ -168,7 +204,10 @@ __global__ __launch_bounds__(NT) void gn_stats_kernel(StripArgs a) {
   const int c0 = blockIdx.x * a.CW;
   const int cw = min(a.CW, a.C - c0);
   const int Cg = a.C / a.G;
-  strip_reduce<0>(a, b, (long long)b * a.P, a.P, c0, cw, s1, s2);
+  long long p0, p1;
+  pixel_range(a.P, p0, p1);
+  strip_reduce<0>(a, b, (long long)b * a.P + p0, p1 - p0, c0, cw, s1, s2);
+  if (!combine_psplits(a, b, c0, cw, s1, s2)) return;
   const int ng = cw / Cg;
   if ((int)threadIdx.x < ng) {
     double m1 = 0, m2 = 0;
@@ -200,7 +239,10 @@ __global__ __launch_bounds__(NT) void gn_bwd_reduce_kernel(StripArgs a) {
   const int c0 = blockIdx.x * a.CW;
   const int cw = min(a.CW, a.C - c0);
   const int Cg = a.C / a.G;
-  strip_reduce<1>(a, b, (long long)b * a.P, a.P, c0, cw, s1, s2);
+  long long p0, p1;
+  pixel_range(a.P, p0, p1);
+  strip_reduce<1>(a, b, (long long)b * a.P + p0, p1 - p0, c0, cw, s1, s2);
+  if (!combine_psplits(a, b, c0, cw, s1, s2)) return;
   const int ng = cw / Cg;
   const float inv_n = 1.0f / ((float)a.P * Cg);
   if ((int)threadIdx.x < ng) {
@@ -226,7 +268,7 @@ __global__ __launch_bounds__(NT) void gn_bwd_reduce_kernel(StripArgs a) {
     }
   }
   if (!a.sum1) return;
-  if (!arrive_last(a.ctr + blockIdx.x, a.nb)) return;
+  if (!arrive_last(a.ctr + BATCH_CTR + blockIdx.x, a.nb)) return;
   batch_tail(a, c0, cw, a.sum1, a.sum2, a.C);
 }
 
@@ -239,7 +281,10 @@ __global__ __launch_bounds__(NT) void chan_sum_kernel(StripArgs a) {
   const long long total = (long long)a.B * a.P;
   const long long row0 = (long long)b * a.seg;
   const long long nrows = max(0LL, min(a.seg, total - row0));
-  strip_reduce<2>(a, b, row0, nrows, c0, cw, s1, s2);
+  long long p0, p1;
+  pixel_range(nrows, p0, p1);
+  strip_reduce<2>(a, b, row0 + p0, p1 - p0, c0, cw, s1, s2);
+  if (!combine_psplits(a, b, c0, cw, s1, s2)) return;
   const bool tail = a.sum1 || a.sum2;
   for (int ch = threadIdx.x; ch < cw; ch += NT) {
     const int c = c0 + ch;
@@ -251,7 +296,7 @@ __global__ __launch_bounds__(NT) void chan_sum_kernel(StripArgs a) {
     }
   }
   if (!tail) return;
-  if (!arrive_last(a.ctr + blockIdx.x, a.nb)) return;
+  if (!arrive_last(a.ctr + BATCH_CTR + blockIdx.x, a.nb)) return;
   batch_tail(a, c0, cw, a.sum1, a.sum2, a.c_store, /*dup=*/true);  // per_c2: a second bias with the same gradient
 }
 
@@ -265,56 +310,90 @@ struct ApplyArgs {
   int B, P, C, silu;
 };
 
+// Elementwise passes: grid (C/64 strips, B, pixel splits); a thread owns 8 channels of one strip for
+// all of its pixels, so its table entries are loaded once and stay in registers.
+constexpr int APPLY_CW = 64;
+
+__device__ __forceinline__ void apply_coords(const ApplyArgs& a, int& cc, int& r, int& p0, int& p1, bool& on) {
+  const int lane = threadIdx.x & 7;
+  r = threadIdx.x >> 3;  // 32 pixel rows per iteration
+  cc = blockIdx.x * APPLY_CW + lane * 8;
+  const int per = (a.P + gridDim.z - 1) / gridDim.z;
+  p0 = blockIdx.z * per;
+  p1 = min(a.P, p0 + per);
+  on = cc < a.C;
+}
+
 // y = act(x*a + s)
 __global__ __launch_bounds__(NT) void gn_apply_kernel(ApplyArgs a) {
-  const int C8 = a.C >> 3;
-  long long total = (long long)a.B * a.P * C8;
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    long long pix = i / C8;
-    int c0 = (int)(i - pix * C8) * 8;
-    int b = (int)(pix / a.P);
-    const float4* t = a.tab + (long long)b * a.C + c0;
+  int cc, r, p0, p1;
+  bool on;
+  apply_coords(a, cc, r, p0, p1, on);
+  if (!on) return;
+  const int b = blockIdx.y;
+  float ta[8], ts[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float4 t = a.tab[(long long)b * a.C + cc + e];
+    ta[e] = t.x;
+    ts[e] = t.y;
+  }
+  const bf16_t* X = a.x + (long long)b * a.P * a.ldx + cc;
+  bf16_t* Y = a.y + (long long)b * a.P * a.ldy + cc;
+#pragma unroll 4
+  for (int p = p0 + r; p < p1; p += NT / 8) {
     float xv[8], yv[8];
-    unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
+    unpack8(*(const uint4*)(X + (long long)p * a.ldx), xv);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float4 te = t[e];
-      float z = fmaf(xv[e], te.x, te.y);
+      const float z = fmaf(xv[e], ta[e], ts[e]);
       yv[e] = a.silu ? silu_f(z) : z;
     }
-    *(uint4*)(a.y + pix * a.ldy + c0) = pack8(yv);
+    *(uint4*)(Y + (long long)p * a.ldy) = pack8(yv);
   }
 }
 
 // dx = a*dz + q*x + o (+ addend), dz = dy [* silu'(x*a + s)]
 __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
-  const int C8 = a.C >> 3;
-  long long total = (long long)a.B * a.P * C8;
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    long long pix = i / C8;
-    int c0 = (int)(i - pix * C8) * 8;
-    int b = (int)(pix / a.P);
-    const float4* t = a.tab + (long long)b * a.C + c0;
+  int cc, r, p0, p1;
+  bool on;
+  apply_coords(a, cc, r, p0, p1, on);
+  if (!on) return;
+  const int b = blockIdx.y;
+  float4 tb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) tb[e] = a.tab[(long long)b * a.C + cc + e];
+  const long long rb = (long long)b * a.P;
+#pragma unroll 2
+  for (int p = p0 + r; p < p1; p += NT / 8) {
+    const long long row = rb + p;
     float xv[8], gv[8], ov[8], av[8];
-    unpack8(*(const uint4*)(a.x + pix * a.ldx + c0), xv);
-    unpack8(*(const uint4*)(a.dy + pix * a.lddy + c0), gv);
-    if (a.add) unpack8(*(const uint4*)(a.add + pix * a.ldadd + c0), av);
-    else for (int e = 0; e < 8; ++e) av[e] = 0.f;
+    unpack8(*(const uint4*)(a.x + row * a.ldx + cc), xv);
+    unpack8(*(const uint4*)(a.dy + row * a.lddy + cc), gv);
+    if (a.add) {
+      unpack8(*(const uint4*)(a.add + row * a.ldadd + cc), av);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[e] = 0.f;
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float4 te = t[e];
       float dz = gv[e];
-      if (a.silu) dz *= silu_grad_f(fmaf(xv[e], te.x, te.y));
-      ov[e] = av[e] + fmaf(te.x, dz, fmaf(te.z, xv[e], te.w));
+      if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb[e].x, tb[e].y));
+      ov[e] = av[e] + fmaf(tb[e].x, dz, fmaf(tb[e].z, xv[e], tb[e].w));
     }
-    *(uint4*)(a.dx + pix * a.lddx + c0) = pack8(ov);
+    *(uint4*)(a.dx + row * a.lddx + cc) = pack8(ov);
   }
 }
 
-int grid_for(long long work) {
-  long long g = (work + NT - 1) / NT;
-  return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
+// grid of an elementwise pass: C/64 strips x B x pixel splits, >= ~2048 workgroups, >= 64 pixels each
+dim3 apply_grid(int B, int P, int C) {
+  const int strips = (C + APPLY_CW - 1) / APPLY_CW;
+  int ps = 1;
+  while ((long long)strips * B * ps < 2048 && P / (ps * 2) >= 64) ps *= 2;
+  return dim3(strips, B, ps);
 }
+
 
 // Strip width: a multiple of `unit` (whole groups) and of 8 channels, at least 64 channels when C allows
 // (narrower strips measured slower: 16-byte row segments coalesce poorly).
@@ -338,24 +417,40 @@ unsigned* counter_slot() {
   return base[dev] + (size_t)(next.fetch_add(1) % NSLOTS) * SLOT_CTRS;
 }
 
+// pixel splits per (strip, batch row): aim for >= 512 workgroups with >= 128 pixels each
+int pick_psplit(int nch, int nb, long long rows_per_b) {
+  int ps = 1;
+  if ((long long)nch * nb > BATCH_CTR) return 1;
+  while ((long long)nch * nb * ps < 512 && rows_per_b / (ps * 2) >= 128 && ps < PS_MAX) ps *= 2;
+  return ps;
+}
+
+float* part_base(float* ws, int nb, int C) { return ws + (size_t)(nb > 32 ? nb : 32) * C * 2; }
+
 }  // namespace
 
 extern "C" size_t sdmi_chan_reduce_workspace(int B, int P, int C) {
   (void)P;
-  return (size_t)(B > 32 ? B : 32) * C * 2 * sizeof(float);
+  const size_t nb = B > 32 ? B : 32;
+  return (nb + nb * PS_MAX) * C * 2 * sizeof(float);
 }
 
 // stats -> per-(b,c) table {a = rstd*gamma, s = beta - mean*a, mean, rstd} (fp32 float4 [B][C])
 extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, const float* gamma,
                              const float* beta, float* ws, float* table, sdmi_stream_t stream) {
-  (void)ws;
   if (C % 8 || G <= 0 || C % G) return -1;
   StripArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.eps = eps;
   a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table;
   a.CW = strip_width(C, C / G);
-  if (a.CW > NT) return -2;
-  hipLaunchKernelGGL(gn_stats_kernel, dim3((C + a.CW - 1) / a.CW, B), dim3(NT), 0, (hipStream_t)stream, a);
+  const int nch = (C + a.CW - 1) / a.CW;
+  if (a.CW > NT || nch > BATCH_CTR) return -2;
+  const int ps = pick_psplit(nch, B, P);
+  if (ps > 1) {
+    a.part = part_base(ws, B, C);
+    if (!(a.ctr = counter_slot())) return -4;
+  }
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(nch, B, ps), dim3(NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -366,7 +461,7 @@ extern "C" int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const flo
   ApplyArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.y = (bf16_t*)y; a.ldy = ldy;
   a.tab = (const float4*)table; a.B = B; a.P = P; a.C = C; a.silu = silu;
-  hipLaunchKernelGGL(gn_apply_kernel, dim3(grid_for((long long)B * P * C / 8)), dim3(NT), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(gn_apply_kernel, apply_grid(B, P, C), dim3(NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -383,16 +478,18 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.gamma = gamma; r.out_tab = (float4*)table2_ws;
   r.CW = strip_width(C, C / G);
   const int nch = (C + r.CW - 1) / r.CW;
-  if (r.CW > NT || nch > SLOT_CTRS) return -2;
+  if (r.CW > NT || nch > BATCH_CTR) return -2;
   r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
-  if (dgamma && !(r.ctr = counter_slot())) return -4;
-  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(nch, B), dim3(NT), 0, s, r);
+  const int ps = pick_psplit(nch, B, P);
+  r.part = part_base(ws, B, C);
+  if ((dgamma || ps > 1) && !(r.ctr = counter_slot())) return -4;
+  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(nch, B, ps), dim3(NT), 0, s, r);
   SDMI_CHECK_LAUNCH();
   ApplyArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.dy = (const bf16_t*)dy; a.lddy = lddy; a.dx = (bf16_t*)dx; a.lddx = lddx;
   a.tab = (const float4*)table2_ws; a.add = (const bf16_t*)addend; a.ldadd = ldadd;
   a.B = B; a.P = P; a.C = C; a.silu = silu;
-  hipLaunchKernelGGL(gn_bwd_apply_kernel, dim3(grid_for((long long)B * P * C / 8)), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(gn_bwd_apply_kernel, apply_grid(B, P, C), dim3(NT), 0, s, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -418,9 +515,11 @@ extern "C" int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, floa
   }
   r.CW = strip_width(C, 8);
   const int nch = (C + r.CW - 1) / r.CW;
-  if (nch > SLOT_CTRS || r.CW > NT) return -2;
-  if ((per_c || per_c2) && !(r.ctr = counter_slot())) return -4;
-  hipLaunchKernelGGL(chan_sum_kernel, dim3(nch, r.nb), dim3(NT), 0, (hipStream_t)stream, r);
+  if (nch > BATCH_CTR || r.CW > NT) return -2;
+  const int ps = pick_psplit(nch, r.nb, r.seg);
+  r.part = part_base(ws, r.nb, C);
+  if ((per_c || per_c2 || ps > 1) && !(r.ctr = counter_slot())) return -4;
+  hipLaunchKernelGGL(chan_sum_kernel, dim3(nch, r.nb, ps), dim3(NT), 0, (hipStream_t)stream, r);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
