@@ -41,3 +41,18 @@ def full_uncond_config():
 # scheduler configs: (num_timesteps, beta_start, beta_end)
 SCHED_COND = (1000, 0.00085, 0.012)     # config/celebhq_text_image_cond.py:31-33
 SCHED_UNCOND = (1000, 0.0015, 0.0195)   # config/celebhq.yaml diffusion_params
+
+
+# ---- DiT (models/transformer.py) ----
+def dit12l_config():
+    """Model_DiT_12L_config.py dit_model_config: hidden 288, patch 2, t-emb 192 (build_ldm_scaling(2.58)
+    of the UNet's 512), 12 layers, 9 heads x 32, image-only conditioning (ldm_condition_types=['image'])."""
+    return {"hidden_size": 288, "patch_size": 2, "timestep_emb_dim": 192, "num_layers": 12, "num_heads": 9,
+            "head_dim": 32, "condition_config": _cond(512, text=False, image=True)}
+
+
+# small DiT with text cross-attention (CustomMultiheadAttention path, Model_DiT_9L-style) and image cond
+SMALL_DIT = {"hidden_size": 96, "patch_size": 2, "timestep_emb_dim": 64, "num_layers": 2, "num_heads": 3,
+             "head_dim": 32, "condition_config": _cond(64, text=True, image=True)}
+SMALL_DIT_UNCOND = {"hidden_size": 64, "patch_size": 2, "timestep_emb_dim": 32, "num_layers": 2, "num_heads": 2,
+                    "head_dim": 32}

@@ -1,0 +1,139 @@
+"""Generates the DiT (and VQVAE) golden fixtures in tests/golden/ by importing the REFERENCE
+implementation (read-only at /root/reference) in THIS container. Only input/output tensors are
+committed (safetensors); weights regenerate from oracle.sd_oracle.deterministic_state.
+
+Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae]
+
+The reference DIT zero-initialises adaptive_norm_layer and proj_out (models/transformer.py:147-151,
+transformer_layer.py:70-71), so a freshly built reference model outputs exactly 0; the fixtures load
+the seeded non-zero state instead, after checking key order and shapes against the oracle's tables.
+"""
+import os
+import sys
+
+import torch
+from safetensors.torch import save_file
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+REF = os.environ.get("SDMI_REFERENCE", "/root/reference")
+if REF not in sys.path:
+    sys.path.insert(1, REF)
+
+from oracle import sd_oracle as O  # noqa: E402
+from oracle import dit_oracle as DO  # noqa: E402
+from tests.golden.configs import SMALL_DIT, SMALL_DIT_UNCOND, dit12l_config  # noqa: E402
+from tests.golden.make_golden import one_hot_mask  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def make_dit(cfg, seed):
+    import models.transformer as ref_dit
+    model = ref_dit.DIT(im_channels=4, model_config=cfg)
+    shapes = DO.dit_param_shapes(cfg)
+    ref_sd = model.state_dict()
+    assert list(ref_sd.keys()) == list(shapes.keys()), (list(ref_sd.keys())[:12], list(shapes.keys())[:12])
+    for k, v in ref_sd.items():
+        assert tuple(v.shape) == tuple(shapes[k]), (k, v.shape, shapes[k])
+    sd = O.deterministic_state(shapes, seed)
+    model.load_state_dict(sd)
+    return model, sd
+
+
+def dit_inputs(B, cfg, seed, mask_hw=64):
+    L = DO.dit_layout(cfg)
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, 4, 32, 32, generator=g)
+    t = torch.randint(0, 1000, (B,), generator=g)
+    f = {"x": x, "t": t}
+    cond = {}
+    if L["text"]:
+        f["text"] = torch.randn(B, 77, L["ctx_dim"], generator=g)
+        cond["text"] = f["text"]
+    if L["image"]:
+        f["classmap"] = torch.randint(0, 19, (B, mask_hw, mask_hw), generator=g).to(torch.uint8)
+        cond["image"] = one_hot_mask(f["classmap"])
+    return f, (cond or None)
+
+
+GRAD_KEYS_DIT = ("cond_conv_in.weight", "patch_embed_layer.patch_embed.0.weight", "t_proj.0.weight",
+                 "t_proj.2.bias", "transformer_layers.0.attn_block.qkv_proj.weight",
+                 "transformer_layers.1.attn_block.output_proj.0.bias", "transformer_layers.0.mlp_block.0.weight",
+                 "transformer_layers.1.mlp_block.2.weight", "transformer_layers.0.adaptive_norm_layer.1.weight",
+                 "transformer_layers.1.adaptive_norm_layer.1.bias", "transformer_layers.0.cross_attn_block.q_proj.weight",
+                 "transformer_layers.1.cross_attn_block.v_proj.bias", "transformer_layers.0.context_proj.weight",
+                 "adaptive_norm_layer.1.weight", "proj_out.weight", "proj_out.bias")
+
+
+def gen_dit():
+    # small text+image DiT: forward, loss, gradients
+    for name, cfg in (("dit_small", SMALL_DIT), ("dit_small_uncond", SMALL_DIT_UNCOND)):
+        model, sd = make_dit(cfg, seed=4)
+        f, cond = dit_inputs(2, cfg, seed=12)
+        noise = torch.randn(f["x"].shape, generator=torch.Generator().manual_seed(13))
+        f["noise"] = noise
+        model.zero_grad()
+        out = model(f["x"], f["t"], cond_input=cond) if cond else model(f["x"], f["t"])
+        loss = torch.nn.functional.mse_loss(out, noise)
+        loss.backward()
+        f["out"] = out.detach()
+        f["loss"] = loss.detach().reshape(1)
+        f["grad_norm"] = torch.norm(torch.stack([p.grad.norm() for p in model.parameters() if p.grad is not None])
+                                    ).reshape(1)
+        for k, p in model.named_parameters():
+            if k in GRAD_KEYS_DIT:
+                f["grad." + k] = p.grad.detach().reshape(-1)[:8192].clone()
+        save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, f"{name}.safetensors"))
+
+    # DiT-12L (Model_DiT_12L_config) forward at batch 2
+    model, sd = make_dit(dit12l_config(), seed=6)
+    f, cond = dit_inputs(2, dit12l_config(), seed=14, mask_hw=512)
+    with torch.no_grad():
+        f["out"] = model(f["x"], f["t"], cond_input=cond)
+    save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, "dit12l.safetensors"))
+
+    # two reference DiT training steps (Model_DiT_12L_train.py:300-375: Adam lr 1e-4, clip 1.0, no EMA)
+    import scheduler.linear_noise_scheduler as ref_sched
+    model, sd = make_dit(SMALL_DIT, seed=4)
+    sched = ref_sched.LinearNoiseScheduler(1000, 0.00085, 0.012)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    f = {}
+    for step in range(2):
+        inp, cond = dit_inputs(2, SMALL_DIT, seed=300 + step)
+        noise = torch.randn(inp["x"].shape, generator=torch.Generator().manual_seed(400 + step))
+        for k, v in inp.items():
+            f[f"s{step}.{k}"] = v
+        f[f"s{step}.noise"] = noise
+        opt.zero_grad(set_to_none=True)
+        xt = sched.add_noise(inp["x"], noise, inp["t"])
+        loss = torch.nn.functional.mse_loss(model(xt, inp["t"], cond_input=cond), noise)
+        loss.backward()
+        gn = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        f[f"s{step}.loss"] = loss.detach().reshape(1)
+        f[f"s{step}.grad_norm"] = gn.detach().reshape(1)
+    for k, p in model.named_parameters():
+        if k in GRAD_KEYS_DIT:
+            f["param." + k] = p.detach().reshape(-1)[:8192].clone()
+    save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, "dit_train_step.safetensors"))
+
+    # position embedding KAT
+    from models.patch_embed import get_patch_position_embedding
+    save_file({"pos_288_16x16": get_patch_position_embedding(288, (16, 16), "cpu").contiguous(),
+               "pos_96_16x8": get_patch_position_embedding(96, (16, 8), "cpu").contiguous()},
+              os.path.join(HERE, "dit_pos.safetensors"))
+
+
+def main():
+    what = sys.argv[1:] or ["dit", "vqvae"]
+    if "dit" in what:
+        gen_dit()
+    if "vqvae" in what and "gen_vqvae" in globals():
+        globals()["gen_vqvae"]()
+    print("fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
