@@ -68,12 +68,13 @@ typedef struct sdmi_gemm_desc {
   int rb_ld, rb_shift;
   const void* resid; int ldr; /* bf16 or NULL           */
   float alpha;
-  int act;                    /* 0 none, 1 SiLU         */
+  int act;                    /* 0 none, 1 SiLU, 2 ReLU, 3 ReLU-gradient mask (aux) */
   /* row remap (stride-2 sub-pixel phases of a transposed conv): m -> (b, oy, ox) on a
    * (2^r_gh_log2 x 2^r_gw_log2) grid, orow = (b*r_oh + oy*r_sy + r_oy)*r_ow + ox*r_sx + r_ox */
   int remap, r_gh_log2, r_gw_log2, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
-  /* column permute (weight-gradient layouts): n = tap*p_cin + c  ->  ocol = c*p_taps + tap, stored only
-   * for c < p_cvalid (0 = all): gradients of zero-padded input channels are dropped */
+  /* column permute (weight-gradient layouts): n = tap*p_cin + c  ->  ocol = c*p_taps + tap (perm 1, torch
+   * conv weight layout) or tap*p_cvalid + c (perm 2, tap-major Linear layout of a patch embedding), stored
+   * only for c < p_cvalid (0 = all): gradients of zero-padded input channels are dropped */
   int perm, p_cin, p_taps, p_cvalid;
   /* store limits (0 = m / n): rows >= m_store and columns >= n_store are computed but not stored,
    * and the bias is read only for stored columns (zero-padded output channels) */
@@ -82,6 +83,12 @@ typedef struct sdmi_gemm_desc {
    * same pixel grid) -- fuses a 1x1 conv of another tensor into the same GEMM by K-concatenation */
   const void* a2; int lda2; int k_split;
   const float* bias2; /* second fp32 [n] bias added in the epilogue, or NULL */
+  /* rowbias row index = (m >> rb_shift) % rb_mod when rb_mod > 0: a per-token table shared by every
+   * sample (the DiT patch position embedding, models/patch_embed.py:93-95) */
+  int rb_mod;
+  /* act 3 (ReLU backward, models/transformer_layer.py:38-42 / transformer.py:107-111): v is kept where
+   * aux[orow*ld_aux + n] > 0 (aux = the saved bf16 ReLU output), else 0 */
+  const void* aux; int ld_aux;
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */
@@ -152,6 +159,40 @@ int sdmi_time_embedding(const long long* t, int tstride, int B, int dim, void* o
 int sdmi_silu(const void* x, const void* dy, void* y, long long n, sdmi_stream_t stream);
 int sdmi_copy_slice(const void* src, int lds, void* dst, int ldd, long long P, int C, int accumulate,
                     sdmi_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * DiT row kernels (models/transformer.py:153-213, transformer_layer.py:80-106). Tokens are row-major bf16
+ * [B*N][ld] (N tokens per sample, C = hidden size, C % 8 == 0, C <= 512, 16-B aligned rows). The adaLN
+ * tables shift / scale / gate are bf16 [B][ld_mod] column slices of the one GEMM that evaluates every
+ * layer's adaptive_norm_layer.
+ *  sdmi_ln_mod_fwd : [xo = x + gate*v (gate NULL: ungated)] -> LayerNorm(no affine, eps) -> y = xhat*(1+scale)
+ *                    + shift (shift = scale = NULL: plain LayerNorm); mean / rstd fp32 [rows] saved.
+ *                    x_f32: the residual stream x / xo is fp32 (more precise than the reference's bf16
+ *                    autocast stream; v, gate, shift, scale, y stay bf16).
+ *  sdmi_ln_mod_bwd : dx = dres + LayerNorm'(dy*(1+scale)); partial dshift / dscale rows (fp32, one per
+ *                    (sample, token chunk of sdmi_ln_chunk_rows(N)), row stride ws_ld); with gate: the gate
+ *                    backward of the branch that produced x, dv = gate*dx and partial dgate = sum dx*v.
+ *                    x_f32: x, dres and dx are fp32; dx16 (optional) receives a bf16 copy of dx.
+ *  sdmi_mod_finalize: out[b][c] = bf16(sum over the chunk partial rows) -- fixed order, no atomics.
+ *  sdmi_tokens_to_nchw / sdmi_nchw_to_tokens_bf16 : '(nh nw) (ph pw c)' token layout <-> NCHW fp32
+ *                    (the reference's einops rearranges, transformer.py:209-212, patch_embed.py:88-89).
+ *  sdmi_mse_patch  : nn.MSELoss with pred in token layout, target NCHW (p = 1: NHWC pred, as sdmi_mse).
+ * ------------------------------------------------------------------------------------------- */
+int sdmi_ln_chunk_rows(int N);
+int sdmi_ln_mod_fwd(const void* x, int ldx, const void* v, int ldv, const void* gate, void* xo, int ldxo,
+                    const void* shift, const void* scale, int ld_mod, void* y, int ldy, float* mean, float* rstd,
+                    int rows, int C, int N, float eps, int x_f32, sdmi_stream_t stream);
+int sdmi_ln_mod_bwd(const void* x, int ldx, const float* mean, const float* rstd, const void* dy, int lddy,
+                    const void* scale, int ld_mod, const void* dres, int lddres, void* dx, int lddx, float* psh,
+                    float* psc, int ws_ld, const void* gate, const void* v, int ldv, void* dv, int lddv, float* pg,
+                    int rows, int C, int N, int x_f32, void* dx16, int ld16, sdmi_stream_t stream);
+int sdmi_mod_finalize(const float* ws, int B, int chunks, int ws_ld, int W, void* out, int ldo, sdmi_stream_t stream);
+int sdmi_tokens_to_nchw(const void* src, int src_f32, int ld, int B, int C, int H, int W, int p, float* dst,
+                        sdmi_stream_t stream);
+int sdmi_nchw_to_tokens_bf16(const float* src, int B, int C, int H, int W, int p, void* dst, int ld,
+                             sdmi_stream_t stream);
+int sdmi_mse_patch(const float* pred, int ld, const float* target, int B, int C, int H, int W, int p, float gscale,
+                   const float* gscale_dev, void* grad, float* ws, float* loss, sdmi_stream_t stream);
 
 /* bf16 GEMM-layout weight packing (the per-step fp32 -> bf16 cast that autocast performs,
  * train_ddpm_cond_celebhq_multi_gpu.py:281-283, fused with the layout change):

@@ -54,7 +54,14 @@ struct EpiArgs {
   unsigned* counters;  // per-tile arrival counters: the last split of a tile reduces it (0: separate reducer)
   int vec;          // LDS-staged 16-B row stores (no column permute, 8-aligned columns/strides)
   int n8;           // N % 8 == 0: split-K slabs are written / read as 16-B rows even when !vec
+  int rb_mod;       // rowbias row = (row >> rb_shift) % rb_mod when > 0 (per-token tables, e.g. position embedding)
+  const bf16_t* aux; int ld_aux;  // act 3: ReLU-gradient mask source (aux[orow*ld_aux + col] > 0)
 };
+
+__device__ __forceinline__ long long rb_row(const EpiArgs& g, int row) {
+  long long r = row >> g.rb_shift;
+  return g.rb_mod > 0 ? r % g.rb_mod : r;
+}
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int CPOL_SC1 = 16;  // buffer cache policy: device (agent) scope coherence
@@ -63,10 +70,18 @@ __device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + ((c ^ (r 
 __device__ __forceinline__ int tr_swz(int r) { return ((r & 3) | ((r >> 1) & 4)) << 1; }
 __device__ __forceinline__ int tr_off(int r, int c) { return r * 256 + ((c ^ tr_swz(r)) << 4); }
 
+// activation of the epilogue: 1 SiLU, 2 ReLU, 3 ReLU gradient (keep v where aux > 0)
+__device__ __forceinline__ float act1(const EpiArgs& g, float v, long long orow, int col) {
+  if (g.act == 1) return silu_f(v);
+  if (g.act == 2) return fmaxf(v, 0.f);
+  if (g.act == 3) return bf2f(g.aux[orow * g.ld_aux + col]) > 0.f ? v : 0.f;
+  return v;
+}
+
 struct Epi {
   // v already holds alpha*acc + bias + bias2
   __device__ __forceinline__ static void finish(const EpiArgs& g, int row, int col, float v) {
-    if (g.rowbias) v += bf2f(g.rowbias[(long long)(row >> g.rb_shift) * g.rb_ld + col]);
+    if (g.rowbias) v += bf2f(g.rowbias[rb_row(g, row) * g.rb_ld + col]);
     long long orow = row;
     if (g.remap) {
       int b = row >> (g.r_ghl + g.r_gwl);
@@ -75,13 +90,13 @@ struct Epi {
       orow = ((long long)b * g.r_oh + oy * g.r_sy + g.r_oy) * g.r_ow + ox * g.r_sx + g.r_ox;
     }
     if (g.resid) v += bf2f(g.resid[orow * g.ldr + col]);
-    if (g.act == 1) v = silu_f(v);
+    v = act1(g, v, orow, col);
     long long ocol = col;
     if (g.perm) {
       int tap = col / g.p_cin;
       int c = col - tap * g.p_cin;
       if (c >= g.p_cvalid) return;
-      ocol = (long long)c * g.p_taps + tap;
+      ocol = g.perm == 2 ? (long long)tap * g.p_cvalid + c : (long long)c * g.p_taps + tap;
     }
     if (g.c_f32) ((float*)g.C)[orow * g.ldc + ocol] = v;
     else ((bf16_t*)g.C)[orow * g.ldc + ocol] = f2bf(v);
@@ -101,7 +116,7 @@ struct Epi {
     }
     if (g.rowbias) {
       float t[8];
-      unpack8(*(const uint4*)(g.rowbias + (long long)(row >> g.rb_shift) * g.rb_ld + col), t);
+      unpack8(*(const uint4*)(g.rowbias + rb_row(g, row) * g.rb_ld + col), t);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += t[e];
     }
@@ -121,6 +136,14 @@ struct Epi {
     if (g.act == 1) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = silu_f(v[e]);
+    } else if (g.act == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if (g.act == 3) {
+      float t[8];
+      unpack8(*(const uint4*)(g.aux + orow * g.ld_aux + col), t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = t[e] > 0.f ? v[e] : 0.f;
     }
     if (g.c_f32) {
       float* d = (float*)g.C + orow * g.ldc + col;
@@ -145,7 +168,7 @@ struct Epi {
     float v = g.alpha * acc;
     if (g.bias) v += g.bias[col];
     if (g.bias2) v += g.bias2[col];
-    if (g.rowbias) v += bf2f(g.rowbias[(long long)(row >> g.rb_shift) * g.rb_ld + col]);
+    if (g.rowbias) v += bf2f(g.rowbias[rb_row(g, row) * g.rb_ld + col]);
     long long orow = row;
     if (g.remap) {
       int b = row >> (g.r_ghl + g.r_gwl);
@@ -154,13 +177,13 @@ struct Epi {
       orow = ((long long)b * g.r_oh + oy * g.r_sy + g.r_oy) * g.r_ow + ox * g.r_sx + g.r_ox;
     }
     if (g.resid) v += bf2f(g.resid[orow * g.ldr + col]);
-    if (g.act == 1) v = silu_f(v);
+    v = act1(g, v, orow, col);
     long long ocol = col;
     if (g.perm) {
       int tap = col / g.p_cin;
       int c = col - tap * g.p_cin;
       if (c >= g.p_cvalid) return;
-      ocol = (long long)c * g.p_taps + tap;
+      ocol = g.perm == 2 ? (long long)tap * g.p_cvalid + c : (long long)c * g.p_taps + tap;
     }
     if (g.c_f32) ((float*)g.C)[orow * g.ldc + ocol] = v;
     else ((bf16_t*)g.C)[orow * g.ldc + ocol] = f2bf(v);
@@ -858,11 +881,16 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   e.m_store = d->m_store > 0 ? d->m_store : d->m;
   e.n_store = d->n_store > 0 ? d->n_store : d->n;
   e.n8 = d->n % 8 == 0;
+  e.rb_mod = d->rb_mod;
+  e.aux = (const bf16_t*)d->aux; e.ld_aux = d->ld_aux;
+  if (d->act == 3 && !d->aux) return -8;
+  if (d->act < 0 || d->act > 3) return -9;
   e.vec = !d->perm && d->n % 8 == 0 && e.n_store % 8 == 0 && d->ldc % 8 == 0 &&
           (!d->resid || d->ldr % 8 == 0) && (!d->rowbias || d->rb_ld % 8 == 0) &&
           ((uintptr_t)d->c % 16 == 0) && (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
           (!d->bias2 || (uintptr_t)d->bias2 % 16 == 0) && (!d->resid || (uintptr_t)d->resid % 16 == 0) &&
-          (!d->rowbias || (uintptr_t)d->rowbias % 16 == 0);
+          (!d->rowbias || (uintptr_t)d->rowbias % 16 == 0) &&
+          (d->act != 3 || (d->ld_aux % 8 == 0 && (uintptr_t)d->aux % 16 == 0));
   return 0;
 }
 

@@ -38,6 +38,8 @@ class GemmDesc(ctypes.Structure):
         ("m_store", ctypes.c_int), ("n_store", ctypes.c_int),
         ("a2", ctypes.c_void_p), ("lda2", ctypes.c_int), ("k_split", ctypes.c_int),
         ("bias2", ctypes.c_void_p),
+        ("rb_mod", ctypes.c_int),
+        ("aux", ctypes.c_void_p), ("ld_aux", ctypes.c_int),
     ]
 
 
@@ -82,6 +84,14 @@ SIGNATURES = {
     "sdmi_optim_workspace": ([], _SZ),
     "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
     "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P], _I),
+    "sdmi_ln_chunk_rows": ([_I], _I),
+    "sdmi_ln_mod_fwd": ([_P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _I, _F, _I, _P], _I),
+    "sdmi_ln_mod_bwd": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P,
+                         _I, _I, _I, _I, _P, _I, _P], _I),
+    "sdmi_mod_finalize": ([_P, _I, _I, _I, _I, _P, _I, _P], _I),
+    "sdmi_tokens_to_nchw": ([_P, _I, _I, _I, _I, _I, _I, _I, _P, _P], _I),
+    "sdmi_nchw_to_tokens_bf16": ([_P, _I, _I, _I, _I, _I, _P, _I, _P], _I),
+    "sdmi_mse_patch": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
 }
 
 

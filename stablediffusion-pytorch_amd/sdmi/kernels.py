@@ -52,7 +52,7 @@ class _Prof:
 
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
          rb_ld=0, rb_shift=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0,
-         a2=None, lda2=0, k_split=0, bias2=None):
+         a2=None, lda2=0, k_split=0, bias2=None, rb_mod=0, aux=None, ld_aux=0):
     """C[m][n] = epi(sum_k A[m][k] B[k][n]).  a/b/c/resid/rowbias are tensors (pointer = data_ptr,
     offsets already applied by slicing); see include/sdmi.h for the operand modes."""
     L = _lib.lib()
@@ -77,13 +77,16 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
         (d.r_gh_log2, d.r_gw_log2, d.r_oh, d.r_ow, d.r_sy, d.r_sx, d.r_oy, d.r_ox) = remap
         d.remap = 1
     if perm is not None:
-        d.perm = 1
+        d.perm = perm[3] if len(perm) > 3 else 1
         d.p_cin, d.p_taps = perm[0], perm[1]
         d.p_cvalid = perm[2] if len(perm) > 2 else 0
     d.m_store, d.n_store = m_store, n_store
     if a2 is not None:
         d.a2, d.lda2, d.k_split = a2.data_ptr(), lda2, k_split
     d.bias2 = bias2.data_ptr() if bias2 is not None else None
+    d.rb_mod = rb_mod
+    if aux is not None:
+        d.aux, d.ld_aux = aux.data_ptr(), ld_aux or ld_of(aux)
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
@@ -125,11 +128,16 @@ def conv_fwd(x, B, H, W, cin, ldx, wpk, cout, kh, kw, stride, pad, out, ldo, *, 
 def conv_wgrad(dy, ldy, x, B, H, W, cin, ldx, cout, kh, kw, stride, pad, out, OH, OW, *, perm=True, cvalid=0,
                m_store=0):
     """dW[co][(ty,tx,ci)] = sum_pixels dy[p, co] * x[gather(p, ty, tx), ci]; written fp32 in torch
-    layout (co, ci, kh, kw) when perm (only ci < cvalid, co < m_store when given)."""
+    layout (co, ci, kh, kw) when perm is True (only ci < cvalid, co < m_store when given); perm may also be
+    an explicit (p_cin, p_taps, p_cvalid, mode) tuple (mode 2: tap-major (co, kh, kw, ci) Linear layout)."""
     g = conv_geom(H, W, cin, ldx, kh, kw, OH, OW, stride, stride, -pad, -pad)
     cv = cvalid or cin
+    if perm is True:
+        perm = (cin, kh * kw, cv)
+    elif isinstance(perm, tuple):
+        cv = perm[2]
     return gemm(cout, kh * kw * cin, B * OH * OW, dy, _lib.A_COLMAJOR, ldy, x, _lib.B_KN_CONV, 0, out,
-                kh * kw * cv, geom=g, perm=(cin, kh * kw, cv) if perm else None, m_store=m_store)
+                kh * kw * cv, geom=g, perm=perm or None, m_store=m_store)
 
 
 # stride-2, 4x4, pad-1 transposed convolution as four 2x2 sub-pixel convolutions.
@@ -163,20 +171,23 @@ def _p(t):
     return t.data_ptr() if t is not None else None
 
 
-def linear(x, w, out, *, bias=None, resid=None, act=0, alpha=1.0, n_store=0):
-    """out[m][n] = act(alpha * x[m] . w[n] + bias[n] + resid[m][n]);  x [M,K] bf16 view, w [N,K] bf16."""
+def linear(x, w, out, *, bias=None, resid=None, act=0, alpha=1.0, n_store=0, rowbias=None, rb_mod=0):
+    """out[m][n] = act(alpha * x[m] . w[n] + bias[n] + rowbias[m % rb_mod][n] + resid[m][n]);
+    x [M,K] bf16 view, w [N,K] bf16 (act: 0 none, 1 SiLU, 2 ReLU)."""
     M, K = x.shape
     N = w.shape[0]
-    return gemm(M, N, K, x, _lib.A_ROWMAJOR, ld_of(x), w, _lib.B_NK, K, out, ld_of(out), bias=bias, resid=resid,
-                ldr=ld_of(resid) if resid is not None else 0, act=act, alpha=alpha)
+    return gemm(M, N, K, x, _lib.A_ROWMAJOR, ld_of(x), w, _lib.B_NK, ld_of(w), out, ld_of(out), bias=bias,
+                resid=resid, ldr=ld_of(resid) if resid is not None else 0, act=act, alpha=alpha, n_store=n_store,
+                rowbias=rowbias, rb_ld=ld_of(rowbias) if rowbias is not None else 0, rb_mod=rb_mod)
 
 
-def linear_dgrad(dy, w, out, *, resid=None):
-    """out[m][k] = sum_n dy[m][n] w[n][k] (+ resid);  w [N,K] bf16 used as B[k=n][n=k] (row-major)."""
+def linear_dgrad(dy, w, out, *, resid=None, relu_of=None):
+    """out[m][k] = sum_n dy[m][n] w[n][k] (+ resid), times (relu_of[m][k] > 0) when relu_of (the saved ReLU
+    output) is given;  w [N,K] bf16 used as B[k=n][n=k] (row-major)."""
     M, N = dy.shape
     K = w.shape[1]
     return gemm(M, K, N, dy, _lib.A_ROWMAJOR, ld_of(dy), w, _lib.B_KN, w.stride(0), out, ld_of(out), resid=resid,
-                ldr=ld_of(resid) if resid is not None else 0)
+                ldr=ld_of(resid) if resid is not None else 0, act=3 if relu_of is not None else 0, aux=relu_of)
 
 
 def linear_wgrad(dy, x, out):

@@ -56,9 +56,10 @@ def flat_order(cfg, keys):
 
 
 class FlatStore:
-    def __init__(self, shapes, cfg, device, with_grads=True):
+    def __init__(self, shapes, cfg, device, with_grads=True, order=None):
         keys = list(shapes.keys())
-        self.order = flat_order(cfg, keys)
+        self.order = list(order) if order is not None else flat_order(cfg, keys)
+        assert sorted(self.order) == sorted(keys), "flat order must cover every parameter exactly once"
         self.shapes = dict(shapes)
         self.offsets = {}
         off = 0

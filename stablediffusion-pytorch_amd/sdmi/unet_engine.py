@@ -758,6 +758,28 @@ class UNetEngine:
         K.chan_sum(dh1, 1, B, T, per_c=self.g("t_proj.0.bias"))
 
     # ------------------------------------------------------------------------------------------
+    def loss(self, pred, noise, dpred, loss_out, gscale_dev=None, gscale=1.0):
+        """nn.MSELoss(pred, noise) with pred NHWC fp32 [B*H*W, 8]; dpred (bf16, same layout) = dL/dpred."""
+        B, C, H, W = noise.shape
+        K.mse(pred, 8, noise, B, C, H * W, gscale, dpred, loss_out, gscale_dev=gscale_dev)
+
+    def pred_to_nchw(self, pred, B, H, W):
+        out = torch.empty(B, self.im_channels, H, W, dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().sdmi_nhwc_to_nchw(pred.data_ptr(), 1, 8, B, self.im_channels, H * W, out.data_ptr(),
+                                                K._stream()), "sdmi_nhwc_to_nchw")
+        return out
+
+    def dpred_from_nchw(self, d):
+        B, C, H, W = d.shape
+        dpred = torch.empty(B * H * W, 8, dtype=torch.bfloat16, device=self.device)
+        _lib.check(_lib.lib().sdmi_nchw_to_nhwc_bf16(d.data_ptr(), B, C, H * W, dpred.data_ptr(), 8, K._stream()),
+                   "sdmi_nchw_to_nhwc_bf16")
+        return dpred
+
+    def new_dpred(self, B, H, W):
+        return torch.empty(B * H * W, 8, dtype=torch.bfloat16, device=self.device)
+
+    # ------------------------------------------------------------------------------------------
     @contextlib.contextmanager
     def _wg(self, *keep):
         """Weight-gradient work: issued on the side stream after everything issued so far on the current

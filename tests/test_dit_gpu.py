@@ -1,0 +1,246 @@
+"""GPU parity of the HIP DiT path (sdmi.dit_engine via models/transformer.DIT) against the CPU fp32 DiT
+oracle (oracle/dit_oracle.py, itself pinned to the reference) on identical weights and inputs, plus the
+DiT row kernels against torch fp32 references of the same op.
+
+Tolerances (bf16 activations / MFMA bf16 products, fp32 accumulation and statistics):
+  forward  : MSE(pred_hip, pred_oracle) <= 1e-4 (north_star bound) and max|diff| <= 0.1 * max|ref|
+  gradients: cosine(grad_hip, grad_oracle) >= 0.99 per parameter tensor, global norm within 5 %
+  row kernels: bf16 output rounding (<= 1e-2 relative to the tensor's max)."""
+import os
+
+import pytest
+import torch
+
+from oracle import sd_oracle as O
+from oracle import dit_oracle as DO
+from tests.golden.configs import SMALL_DIT, SMALL_DIT_UNCOND, dit12l_config
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def one_hot(cmap, n=18):
+    return torch.nn.functional.one_hot(cmap.long().clamp(0, n), n + 1).movedim(-1, 1)[:, 1:].float()
+
+
+def cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
+def close(out, ref, tol=1e-2):
+    err = (out.float().cpu() - ref.float().cpu()).abs().max().item()
+    scale = ref.float().abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------------------------------------
+# row kernels
+# ------------------------------------------------------------------------------------------------
+def _lib():
+    from sdmi import _lib as L, kernels as K
+    return L, K
+
+
+@pytest.mark.parametrize("gated", [False, True])
+def test_ln_mod_fwd(gated):
+    L, K = _lib()
+    torch.manual_seed(0)
+    B, N, C = 3, 64, 96
+    M = B * N
+    x = bf(torch.randn(M, C, device="cuda"))
+    v = bf(torch.randn(M, C, device="cuda"))
+    mod = bf(torch.randn(B, 3 * C, device="cuda") * 0.5)
+    sh, sc, g = mod[:, :C], mod[:, C:2 * C], mod[:, 2 * C:]
+    y = torch.empty(M, C, dtype=torch.bfloat16, device="cuda")
+    xo = torch.empty_like(y)
+    mean = torch.empty(M, device="cuda")
+    rstd = torch.empty(M, device="cuda")
+    L.check(L.lib().sdmi_ln_mod_fwd(x.data_ptr(), C, v.data_ptr() if gated else None, C,
+                                    g.data_ptr() if gated else None, xo.data_ptr() if gated else None, C,
+                                    sh.data_ptr(), sc.data_ptr(), 3 * C, y.data_ptr(), C, mean.data_ptr(),
+                                    rstd.data_ptr(), M, C, N, 1e-6, 0, K._stream()), "ln_mod_fwd")
+    xr = x.float()
+    if gated:
+        xr = bf(xr + g.float().repeat_interleave(N, 0) * v.float()).float()
+        close(xo, xr)
+    ref = torch.nn.functional.layer_norm(xr, (C,), eps=1e-6) * (1 + sc.float().repeat_interleave(N, 0)) \
+        + sh.float().repeat_interleave(N, 0)
+    close(y, ref)
+    close(mean, xr.mean(1), 1e-4)
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_ln_mod_bwd_with_gate_and_finalize(f32):
+    """LN(+modulation) backward, fused gate backward, chunk partials + finalize vs torch autograd fp32
+    (f32: fp32 residual stream x / dres / dx plus the bf16 copy of dx)."""
+    L, K = _lib()
+    torch.manual_seed(1)
+    B, N, C = 2, 64, 96
+    M = B * N
+    x = bf(torch.randn(M, C, device="cuda"))
+    if f32:
+        x = x.float()
+    v = bf(torch.randn(M, C, device="cuda"))
+    dy = bf(torch.randn(M, C, device="cuda"))
+    dres = bf(torch.randn(M, C, device="cuda"))
+    if f32:
+        dres = dres.float()
+    mod = bf(torch.randn(B, 3 * C, device="cuda") * 0.5)
+    sc, g = mod[:, C:2 * C], mod[:, 2 * C:]
+    # forward statistics from the kernel
+    y = torch.empty(M, C, dtype=torch.bfloat16, device="cuda")
+    mean = torch.empty(M, device="cuda")
+    rstd = torch.empty(M, device="cuda")
+    L.check(L.lib().sdmi_ln_mod_fwd(x.data_ptr(), C, None, 0, None, None, 0, mod.data_ptr(), sc.data_ptr(), 3 * C,
+                                    y.data_ptr(), C, mean.data_ptr(), rstd.data_ptr(), M, C, N, 1e-6, int(f32),
+                                    K._stream()), "fwd")
+    R = L.lib().sdmi_ln_chunk_rows(N)
+    chunks = N // R
+    ws = torch.full((B * chunks, 3 * C), float("nan"), device="cuda")
+    dx = torch.empty(M, C, dtype=torch.float32 if f32 else torch.bfloat16, device="cuda")
+    dx16 = torch.empty(M, C, dtype=torch.bfloat16, device="cuda")
+    dv = torch.empty(M, C, dtype=torch.bfloat16, device="cuda")
+    L.check(L.lib().sdmi_ln_mod_bwd(x.data_ptr(), C, mean.data_ptr(), rstd.data_ptr(), dy.data_ptr(), C, sc.data_ptr(),
+                                    3 * C, dres.data_ptr(), C, dx.data_ptr(), C, ws.data_ptr(), ws[:, C:].data_ptr(),
+                                    3 * C, g.data_ptr(), v.data_ptr(), C, dv.data_ptr(), C, ws[:, 2 * C:].data_ptr(),
+                                    M, C, N, int(f32), dx16.data_ptr(), C, K._stream()), "bwd")
+    dmod = torch.empty(B, 3 * C, dtype=torch.bfloat16, device="cuda")
+    L.check(L.lib().sdmi_mod_finalize(ws.data_ptr(), B, chunks, 3 * C, 3 * C, dmod.data_ptr(), 3 * C, K._stream()),
+            "finalize")
+    # reference
+    xr = x.float().cpu().requires_grad_(True)
+    shr = mod[:, :C].float().cpu().requires_grad_(True)
+    scr = sc.float().cpu().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (C,), eps=1e-6) * (1 + scr.repeat_interleave(N, 0)) \
+        + shr.repeat_interleave(N, 0)
+    yr.backward(dy.float().cpu())
+    dx_ref = xr.grad + dres.float().cpu()
+    close(dx, dx_ref, 1e-4 if f32 else 1e-2)
+    close(dx16, dx_ref)
+    close(dmod[:, :C], shr.grad)
+    close(dmod[:, C:2 * C], scr.grad)
+    dxb = dx.float().cpu()
+    close(dv, g.float().cpu().repeat_interleave(N, 0) * dxb)
+    dg_ref = (dxb * v.float().cpu()).view(B, N, C).sum(1)
+    close(dmod[:, 2 * C:], dg_ref)
+
+
+def test_gemm_relu_posemb_and_relu_grad():
+    L, K = _lib()
+    torch.manual_seed(2)
+    M, N, Kd, T = 256, 96, 64, 64
+    a = bf(torch.randn(M, Kd, device="cuda"))
+    w = bf(torch.randn(N, Kd, device="cuda"))
+    bias = torch.randn(N, device="cuda")
+    pos = bf(torch.randn(T, N, device="cuda"))
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    K.linear(a, w, out, bias=bias, act=2, rowbias=pos, rb_mod=T)
+    ref = torch.relu(a.float() @ w.float().t() + bias + pos.float().repeat(M // T, 1))
+    close(out, ref)
+    dy = bf(torch.randn(M, N, device="cuda"))
+    dx = torch.empty(M, Kd, dtype=torch.bfloat16, device="cuda")
+    relu_out = bf(torch.randn(M, Kd, device="cuda"))
+    K.linear_dgrad(dy, w, dx, relu_of=relu_out)
+    ref = (dy.float() @ w.float()) * (relu_out.float() > 0)
+    close(dx, ref)
+
+
+def test_patch_layout_roundtrip_and_mse():
+    L, K = _lib()
+    torch.manual_seed(3)
+    B, C, H, W, p = 2, 4, 8, 8, 2
+    x = torch.randn(B, C, H, W, device="cuda")
+    tok = torch.empty(B * (H // p) * (W // p), p * p * C, dtype=torch.bfloat16, device="cuda")
+    L.check(L.lib().sdmi_nchw_to_tokens_bf16(x.data_ptr(), B, C, H, W, p, tok.data_ptr(), p * p * C, K._stream()), "")
+    close(tok.view(B, -1, p * p * C), DO.patchify(x.cpu(), p), 5e-3)
+    back = torch.empty_like(x)
+    tf = tok.float()
+    L.check(L.lib().sdmi_tokens_to_nchw(tf.data_ptr(), 1, p * p * C, B, C, H, W, p, back.data_ptr(), K._stream()), "")
+    close(back, DO.unpatchify(tf.cpu().view(B, -1, p * p * C), C, H, W, p), 1e-6)
+    noise = torch.randn(B, C, H, W, device="cuda")
+    grad = torch.empty_like(tok)
+    loss = torch.empty(1, device="cuda")
+    ws = torch.empty(L.lib().sdmi_mse_workspace() // 4, device="cuda")
+    L.check(L.lib().sdmi_mse_patch(tf.data_ptr(), p * p * C, noise.data_ptr(), B, C, H, W, p, 1.0, None,
+                                   grad.data_ptr(), ws.data_ptr(), loss.data_ptr(), K._stream()), "")
+    pr = DO.unpatchify(tf.cpu().view(B, -1, p * p * C), C, H, W, p).requires_grad_(True)
+    lr = torch.nn.functional.mse_loss(pr, noise.cpu())
+    lr.backward()
+    assert abs(loss.item() - lr.item()) <= 1e-5 * lr.item()
+    close(grad.view(B, -1, p * p * C), DO.patchify(pr.grad, p))
+
+
+# ------------------------------------------------------------------------------------------------
+# whole model
+# ------------------------------------------------------------------------------------------------
+def make(cfg, seed):
+    from models.transformer import DIT
+    m = DIT(4, cfg)
+    sd = O.deterministic_state(DO.dit_param_shapes(cfg), seed)
+    assert list(m.state_dict().keys()) == list(sd.keys())
+    m.load_state_dict(sd)
+    return m.cuda(), sd
+
+
+def cond_of(f, cfg):
+    L = DO.dit_layout(cfg)
+    c = {}
+    if L["text"]:
+        c["text"] = f["text"]
+    if L["image"]:
+        c["image"] = one_hot(f["classmap"])
+    return c or None
+
+
+@pytest.mark.parametrize("name,cfg", [("dit_small", SMALL_DIT), ("dit_small_uncond", SMALL_DIT_UNCOND)])
+def test_small_dit_forward_backward(name, cfg):
+    from safetensors.torch import load_file
+    f = load_file(os.path.join(G, name + ".safetensors"))
+    model, sd = make(cfg, seed=4)
+    c = cond_of(f, cfg)
+    leaves = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ref = DO.dit_forward(leaves, cfg, f["x"], f["t"], c)
+    torch.nn.functional.mse_loss(ref, f["noise"]).backward()
+    cc = {k: v.cuda() for k, v in c.items()} if c else None
+    out = model(f["x"].cuda(), f["t"].cuda(), cc)
+    loss = torch.nn.functional.mse_loss(out, f["noise"].cuda())
+    loss.backward()
+    torch.cuda.synchronize()
+    out = out.detach().cpu()
+    mse = ((out - ref.detach()) ** 2).mean().item()
+    assert mse <= 1e-4, mse
+    assert ((out - f["out"]) ** 2).mean().item() <= 1e-4  # and against the reference's own output
+    assert (out - ref).abs().max().item() <= 0.1 * ref.abs().max().item()
+    for k, p in model.named_parameters():
+        r = leaves[k].grad
+        if r is not None and r.norm() > 1e-6:
+            cval = cos(p.grad.cpu(), r)
+            assert cval >= 0.99, (k, cval)
+    gn = torch.norm(torch.stack([p.grad.norm() for p in model.parameters()])).item()
+    rn = torch.norm(torch.stack([v.grad.norm() for v in leaves.values() if v.grad is not None])).item()
+    assert abs(gn - rn) <= 0.05 * rn, (gn, rn)
+    assert abs(gn - f["grad_norm"].item()) <= 0.05 * f["grad_norm"].item()
+
+
+def test_dit12l_forward_matches_golden():
+    from safetensors.torch import load_file
+    f = load_file(os.path.join(G, "dit12l.safetensors"))
+    cfg = dit12l_config()
+    model, _ = make(cfg, seed=6)
+    with torch.no_grad():
+        out = model(f["x"].cuda(), f["t"].cuda(), {"image": one_hot(f["classmap"]).cuda()}).cpu()
+    mse = ((out - f["out"]) ** 2).mean().item()
+    assert mse <= 1e-4, mse
+
+
+def test_fresh_dit_outputs_zero():
+    """The reference zero-initialises adaLN and proj_out (transformer.py:147-151): a fresh DIT predicts 0."""
+    from models.transformer import DIT
+    m = DIT(4, SMALL_DIT_UNCOND).cuda()
+    out = m(torch.randn(2, 4, 32, 32, device="cuda"), torch.tensor([3, 999], device="cuda"))
+    assert out.abs().max().item() == 0.0
