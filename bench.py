@@ -25,6 +25,11 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "DDPM train steps/sec (cond-UNet, CelebHQ-256 latents, B=32) at 1/2/4/8 MI355X"
 FLOP_PER_STEP = 3.8815e12      # cond-UNet fwd+bwd at B=32 (FlopCounterMode on the oracle)
+# secondary workloads (--workload): DiT-12L training step (fwd+bwd 6.759e11 FLOP at B=32)
+WORKLOADS = {
+    "cond-unet": dict(metric=METRIC, flop=FLOP_PER_STEP),
+    "dit": dict(metric="DDPM train steps/sec (DiT-12L image-cond, CelebHQ-256 latents, B=32) on MI355X", flop=6.759e11),
+}
 PEAK_BF16 = 2.5e15             # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
 
@@ -43,6 +48,36 @@ def synthetic_batch(B, device, seed):
     x0, text, empty = x0.to(device), text.to(device), empty.to(device)
     mask = torch.nn.functional.one_hot(cmap.to(device).long(), 19).movedim(-1, 1)[:, 1:].float().contiguous()
     return x0, text, empty, mask
+
+
+def dit_config():
+    from tests.golden.configs import dit12l_config
+    return dit12l_config()
+
+
+def cpu_baseline_dit(cfg, B=32):
+    """The DiT oracle's fp32 training step (Model_DiT_12L_train.py:300-375) on the host cores."""
+    from oracle import sd_oracle as O, dit_oracle as DO
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = O.deterministic_state(DO.dit_param_shapes(cfg), seed=0)
+    opt = O.AdamState(sd)
+    sched = O.SchedulerTables(1000, 0.00085, 0.012)
+    g = torch.Generator().manual_seed(1111)
+    x0 = torch.randn(B, 4, 32, 32, generator=g)
+    cmap = torch.randint(0, 19, (B, 512, 512), generator=g)
+    mask = torch.nn.functional.one_hot(cmap, 19).movedim(-1, 1)[:, 1:].float()
+    times = []
+    for i in range(3):  # 1 warm-up + 2 timed
+        noise = torch.randn(x0.shape, generator=g)
+        t = torch.randint(0, 1000, (B,), generator=g)
+        t0 = time.perf_counter()
+        DO.dit_train_step(sd, opt, cfg, sched, x0, noise, t, {"image": mask})
+        times.append(time.perf_counter() - t0)
+    per = sum(times[1:]) / 2
+    return dict(value=1.0 / per, unit="steps/s", cores=threads, kind="port",
+                sample=f"DiT oracle fp32 train step (fwd+bwd+clip+Adam), B={B}, 1 warm-up + 2 timed steps, "
+                       f"{per:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
 
 
 def cpu_baseline(cfg, B=32):
@@ -78,6 +113,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="cond-unet", choices=sorted(WORKLOADS),
+                    help="cond-unet (the headline metric, default) or dit (DiT-12L training step)")
     ap.add_argument("--profile-gemm", action="store_true", default=True)
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured hipGraph (N == 1; default off: eager issue with the "
@@ -98,10 +135,21 @@ def main():
     from sdmi import kernels as K
     import models.unet_cond_base as mc
 
-    cfg = cond_config()
+    wl = WORKLOADS[args.workload]
+    is_dit = args.workload == "dit"
+    cfg = dit_config() if is_dit else cond_config()
     torch.manual_seed(1111)  # identical initial weights on every rank (DDP broadcasts rank 0's)
-    init = mc.Unet(4, cfg).state_dict()
-    trainer = DDPMTrainer(cfg, init, device, group=dist.group.WORLD if world > 1 else None)
+    group = dist.group.WORLD if world > 1 else None
+    if is_dit:
+        from models.transformer import DIT
+        init = DIT(4, cfg).state_dict()
+        for k, v in init.items():  # the reference zero-initialises adaLN / proj_out: give them random values so
+            if v.abs().max() == 0:  # the timed step runs on non-trivial data (zeros clock higher, MI355X DVFS)
+                v.normal_(0.0, 0.02)
+        trainer = DDPMTrainer(cfg, init, device, base="dit", lr=1e-4, ema_decay=None, group=group)
+    else:
+        init = mc.Unet(4, cfg).state_dict()
+        trainer = DDPMTrainer(cfg, init, device, group=group)
     B = args.batch
     x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
     gen = torch.Generator(device=device).manual_seed(1111 + rank)
@@ -109,12 +157,16 @@ def main():
     def eager_step():
         noise = torch.randn(x0.shape, device=device, generator=gen)
         t = torch.randint(0, 1000, (B,), device=device, generator=gen)
+        if is_dit:  # image-only conditioning, drop prob 0.9 (Model_DiT_12L_config.py ldm_image_condition_cond_drop_prob)
+            keep = (torch.rand(B, device=device, generator=gen) > 0.9).float()
+            trainer.step(x0, noise, t, None, mask, mask_keep=keep)
+            return
         drop_t = torch.rand(B, device=device, generator=gen) < 0.1       # diffusion_utils.py:21-28
         txt = torch.where(drop_t[:, None, None], empty, text)
         keep = (torch.rand(B, device=device, generator=gen) > 0.1).float()  # diffusion_utils.py:31-37
         trainer.step(x0, noise, t, txt, mask, mask_keep=keep)
 
-    use_graph = args.graph and world == 1
+    use_graph = args.graph and world == 1 and not is_dit
     if use_graph:
         from sdmi.graph import CapturedTrainStep
         cap = CapturedTrainStep(trainer, x0, text, empty, mask, B, generator=gen)
@@ -171,22 +223,26 @@ def main():
                              for k, v in by.items()},
                 "dominant_mode": dom[0]}
 
+    FLOP = wl["flop"]
     result = {
-        "metric": METRIC, "value": steps_per_s * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+        "metric": wl["metric"], "value": steps_per_s * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1000.0 / steps_per_s, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "bf16", "data": "synthetic (seeded CelebHQ-shaped latents, text, masks; "
                                                         "random-init weights of the reference architecture)",
-        "config": {"workload": "cond-UNet celebhq_text_image_cond training step", "model": "cond-UNet 118.5M",
-                   "global_batch": B * world, "per_gpu_batch": B, "latent": [4, 32, 32],
-                   "text": [77, 512], "mask": [18, 512, 512], "parallelism": f"dp{world}"},
+        "config": ({"workload": "DiT-12L Model_DiT_12L_config training step (image cond, no EMA, lr 1e-4)",
+                    "model": "DiT-12L 18.3M", "global_batch": B * world, "per_gpu_batch": B, "latent": [4, 32, 32],
+                    "mask": [18, 512, 512], "parallelism": f"dp{world}"} if is_dit else
+                   {"workload": "cond-UNet celebhq_text_image_cond training step", "model": "cond-UNet 118.5M",
+                    "global_batch": B * world, "per_gpu_batch": B, "latent": [4, 32, 32],
+                    "text": [77, 512], "mask": [18, 512, 512], "parallelism": f"dp{world}"}),
         "per_gpu_steps_per_s": steps_per_s, "samples_per_s": steps_per_s * B * world,
-        "model_flops_utilization": FLOP_PER_STEP * steps_per_s / PEAK_BF16,
+        "model_flops_utilization": FLOP * steps_per_s / PEAK_BF16,
         "last_loss": state[S_LOSS], "last_grad_norm": state[S_NORM], "last_step_skipped": bool(state[S_SKIP]),
         "hip_graph": use_graph,
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg)
+        result["cpu_baseline"] = cpu_baseline_dit(cfg) if is_dit else cpu_baseline(cfg)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

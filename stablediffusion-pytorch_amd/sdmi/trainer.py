@@ -19,6 +19,7 @@ from . import kernels as K
 from .reducer import BucketReducer
 from .store import FlatStore, param_label
 from .unet_engine import UNetEngine
+from .dit_engine import DiTEngine, dit_flat_order
 
 # state vector layout (see csrc/optim.hip)
 S_NORM, S_COEF, S_SCALE, S_GROWTH, S_STEP, S_SKIP, S_LOSS = range(7)
@@ -32,28 +33,38 @@ def scheduler_tables(num_timesteps, beta_start, beta_end):
 
 
 class DDPMTrainer:
+    """base: "cond" / "uncond" (UNet, train_ddpm_cond_celebhq_multi_gpu.py:299-378, EMA 0.9999) or "dit"
+    (Model_DiT_12L_train.py:300-375: same step, no EMA -- pass ema_decay=None -- and lr 1e-4)."""
+
     def __init__(self, cfg, state_dict, device, *, base="cond", lr=1e-5, betas=(0.9, 0.999), eps=1e-8,
                  max_grad_norm=1.0, ema_decay=0.9999, init_scale=65536.0, growth_interval=2000,
                  sched=(1000, 0.00085, 0.012), group=None, bucket_bytes=64 << 20):
         self.cfg = cfg
+        self.base = base
         self.device = torch.device(device)
         shapes = {k: tuple(v.shape) for k, v in state_dict.items()}
-        self.store = FlatStore(shapes, cfg, self.device)
+        order = dit_flat_order(cfg, list(shapes)) if base == "dit" else None
+        self.store = FlatStore(shapes, cfg, self.device, order=order)
         self.store.load(state_dict)
-        self.ema = self.store.params.clone()
+        # EMA copy (train_ddpm_cond_celebhq_multi_gpu.py:376-378); none for the DiT trainer (commented out at
+        # Model_DiT_12L_train.py:377-379): the fused optimizer then skips the EMA stream entirely
+        self.ema = self.store.params.clone() if ema_decay is not None else None
         self.m = torch.zeros_like(self.store.params)
         self.v = torch.zeros_like(self.store.params)
         self.state = torch.tensor([0, 0, init_scale, 0, 0, 0, 0, 0], dtype=torch.float32, device=self.device)
         self.hp = dict(lr=lr, b1=betas[0], b2=betas[1], eps=eps, clip=max_grad_norm, ema=ema_decay,
                        growth=growth_interval)
-        self.engine = UNetEngine(cfg, self.store.p, self.store.g, base=base)
+        if base == "dit":
+            self.engine = DiTEngine(cfg, self.store.p, self.store.g)
+        else:
+            self.engine = UNetEngine(cfg, self.store.p, self.store.g, base=base)
         self.num_timesteps = sched[0]
         sa, s1a = scheduler_tables(*sched)
         self.sqrt_abar, self.sqrt_1m_abar = sa.to(self.device), s1a.to(self.device)
         self.group = group
         self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
         self.reducer = BucketReducer(self.store.grads, group, bucket_bytes) if self.world > 1 else None
-        if self.reducer is not None and self.engine.side is not None:
+        if self.reducer is not None and getattr(self.engine, "side", None) is not None:
             self.reducer.producers.append(self.engine.side)
         self._progress = None
         self.engine.refresh_weights()
@@ -94,10 +105,13 @@ class DDPMTrainer:
         xt = torch.empty_like(x0)
         K.add_noise(x0, noise, t, self.sqrt_abar, self.sqrt_1m_abar, xt)
         pred, ctx = eng.forward(xt, t, text, mask, mask_keep=mask_keep)
-        dpred = torch.empty(B * H * W, 8, dtype=torch.bfloat16, device=self.device)
-        K.mse(pred, 8, noise, B, C, H * W, 1.0, dpred, self.state[S_LOSS:S_LOSS + 1],
-              gscale_dev=self.state[S_SCALE:S_SCALE + 1])
-        if self.reducer is not None:
+        dpred = eng.new_dpred(B, H, W)
+        eng.loss(pred, noise, dpred, self.state[S_LOSS:S_LOSS + 1], gscale_dev=self.state[S_SCALE:S_SCALE + 1])
+        if self.reducer is not None and self.base == "dit":
+            self.reducer.reset()
+            eng.backward(ctx, dpred, on_progress=self._on_progress_dit)
+            self.reducer.finish()
+        elif self.reducer is not None:
             self.reducer.reset()
             if self._progress is None:
                 self._progress = self._watermarks(ctx["tape"])
@@ -111,13 +125,29 @@ class DDPMTrainer:
         _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(), ws.data_ptr(),
                                        hp["growth"], 1, float(self.world), K._stream()), "sdmi_clip_unscale")
         _lib.check(L.sdmi_adam_ema(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
-                                   self.ema.data_ptr(), st.numel, self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"],
-                                   hp["eps"], hp["ema"], K._stream()), "sdmi_adam_ema")
+                                   K._p(self.ema), st.numel, self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"],
+                                   hp["eps"], hp["ema"] if hp["ema"] is not None else 0.0, K._stream()), "sdmi_adam_ema")
         eng.refresh_weights()
         return self.state
+
+    def _on_progress_dit(self, i):
+        """DiT backward finished layer i: proj_out and layers i..L-1 are final (the flat prefix up to layer i)."""
+        if self._dit_marks is None:
+            marks = {}
+            for key in self.store.order:
+                if key.startswith("transformer_layers.") and ".adaptive_norm_layer." not in key:
+                    li = int(key.split(".")[1])
+                    off, n = self.store.offsets[key]
+                    marks[li] = max(marks.get(li, 0), off + n)
+            self._dit_marks = marks
+        self.reducer.ready(self._dit_marks[i])
+
+    _dit_marks = None
 
     def loss(self):
         return self.state[S_LOSS]
 
     def ema_state_dict(self):
+        if self.ema is None:
+            raise RuntimeError("this trainer keeps no EMA copy (ema_decay=None)")
         return {k: self.store.view(self.ema, k) for k in self.store.order}

@@ -244,3 +244,38 @@ def test_fresh_dit_outputs_zero():
     m = DIT(4, SMALL_DIT_UNCOND).cuda()
     out = m(torch.randn(2, 4, 32, 32, device="cuda"), torch.tensor([3, 999], device="cuda"))
     assert out.abs().max().item() == 0.0
+
+
+def test_dit_trainer_two_steps_match_reference():
+    """sdmi.trainer.DDPMTrainer(base="dit"): add_noise -> forward -> MSE -> backward -> clip(1.0) -> Adam(1e-4), no
+    EMA (Model_DiT_12L_train.py:300-375) vs the reference's two fp32 steps (golden) and the fp32 oracle step.
+    Loss within 1 %, clipped-gradient norm within 5 %, parameter updates cosine >= 0.95 (Adam's first steps are
+    ~sign(g) * lr, so bf16 noise on near-zero gradients flips a few elements)."""
+    from safetensors.torch import load_file
+    from sdmi.trainer import DDPMTrainer, S_LOSS, S_NORM
+    f = load_file(os.path.join(G, "dit_train_step.safetensors"))
+    sd0 = O.deterministic_state(DO.dit_param_shapes(SMALL_DIT), seed=4)
+    tr = DDPMTrainer(SMALL_DIT, sd0, "cuda", base="dit", lr=1e-4, ema_decay=None)
+    assert tr.ema is None
+    ref = {k: v.clone() for k, v in sd0.items()}
+    opt = O.AdamState(ref)
+    sched = O.SchedulerTables(1000, 0.00085, 0.012)
+    for s in range(2):
+        inp = {k.split(".", 1)[1]: v for k, v in f.items() if k.startswith(f"s{s}.")}
+        c = cond_of(inp, SMALL_DIT)
+        tr.step(inp["x"].cuda(), inp["noise"].cuda(), inp["t"].cuda(), c["text"].cuda(), c["image"].cuda())
+        rl, rn, _ = DO.dit_train_step(ref, opt, SMALL_DIT, sched, inp["x"], inp["noise"], inp["t"], c)
+        torch.cuda.synchronize()
+        loss, norm = tr.state[S_LOSS].item(), tr.state[S_NORM].item()
+        assert abs(loss - inp["loss"].item()) <= 1e-2 * inp["loss"].item(), (loss, inp["loss"].item())
+        assert abs(norm - inp["grad_norm"].item()) <= 5e-2 * inp["grad_norm"].item(), (norm, inp["grad_norm"].item())
+    p = tr.store.params.cpu()
+    d_hip = torch.cat([(tr.store.view(p, k) - sd0[k]).flatten() for k in tr.store.order])
+    d_ref = torch.cat([(ref[k] - sd0[k]).flatten() for k in tr.store.order])
+    assert cos(d_hip, d_ref) >= 0.95, cos(d_hip, d_ref)
+    for k in f:
+        if k.startswith("param."):
+            key = k[6:]
+            dk = (tr.store.view(p, key).reshape(-1)[:8192] - sd0[key].reshape(-1)[:8192])
+            dr = f[k] - sd0[key].reshape(-1)[:8192]
+            assert cos(dk, dr) >= 0.9, (key, cos(dk, dr))
