@@ -56,3 +56,15 @@ SMALL_DIT = {"hidden_size": 96, "patch_size": 2, "timestep_emb_dim": 64, "num_la
              "head_dim": 32, "condition_config": _cond(64, text=True, image=True)}
 SMALL_DIT_UNCOND = {"hidden_size": 64, "patch_size": 2, "timestep_emb_dim": 32, "num_layers": 2, "num_heads": 2,
                     "head_dim": 32}
+
+
+# ---- VQVAE (models/vqvae.py), config/celebhq.yaml autoencoder_params ----
+def vqvae_celebhq_config():
+    return {"z_channels": 4, "codebook_size": 8192, "down_channels": [64, 128, 256, 256], "mid_channels": [256, 256],
+            "down_sample": [True, True, True], "attn_down": [False, False, False], "norm_channels": 32,
+            "num_heads": 4, "num_down_layers": 2, "num_mid_layers": 2, "num_up_layers": 2}
+
+
+SMALL_VQVAE = {"z_channels": 4, "codebook_size": 512, "down_channels": [32, 64, 64], "mid_channels": [64, 64],
+               "down_sample": [True, True], "attn_down": [False, True], "norm_channels": 16, "num_heads": 2,
+               "num_down_layers": 1, "num_mid_layers": 1, "num_up_layers": 1}

@@ -126,6 +126,48 @@ def gen_dit():
               os.path.join(HERE, "dit_pos.safetensors"))
 
 
+def make_vqvae(cfg, seed):
+    import models.vqvae as ref_vq
+    from oracle import vqvae_oracle as VO
+    model = ref_vq.VQVAE(im_channels=3, model_config=cfg)
+    shapes = VO.vqvae_param_shapes(cfg)
+    ref_sd = model.state_dict()
+    assert list(ref_sd.keys()) == list(shapes.keys()), [k for k in ref_sd if k not in shapes][:5]
+    for k, v in ref_sd.items():
+        assert tuple(v.shape) == tuple(shapes[k]), (k, v.shape, shapes[k])
+    sd = O.deterministic_state(shapes, seed)
+    model.load_state_dict(sd)
+    model.eval()
+    return model, sd
+
+
+def gen_vqvae():
+    from tests.golden.configs import SMALL_VQVAE, vqvae_celebhq_config
+    # quantize KAT (models/vqvae.py:93-126): identical fp32 inputs -> indices must match exactly
+    model, sd = make_vqvae(vqvae_celebhq_config(), seed=8)
+    g = torch.Generator().manual_seed(21)
+    z = torch.randn(2, 4, 32, 32, generator=g) * 0.5
+    with torch.no_grad():
+        q, losses, idx = model.quantize(z)
+    save_file({"z": z, "quant": q.contiguous(), "indices": idx.contiguous(), "codebook_loss": losses["codebook_loss"].reshape(1),
+               "commitment_loss": losses["commitment_loss"].reshape(1)}, os.path.join(HERE, "vqvae_quantize.safetensors"))
+    # full celebhq autoencoder at 128x128 (fully convolutional; the bench runs 256x256) and a small config
+    for name, cfg, seed, B, hw in (("vqvae_celebhq", vqvae_celebhq_config(), 8, 1, 128),
+                                   ("vqvae_small", SMALL_VQVAE, 9, 2, 64)):
+        model, sd = make_vqvae(cfg, seed)
+        g = torch.Generator().manual_seed(22)
+        x = torch.rand(B, 3, hw, hw, generator=g) * 2 - 1
+        pre = {}
+        h = model.pre_quant_conv.register_forward_hook(lambda m, i, o: pre.__setitem__("z", o.detach().clone()))
+        with torch.no_grad():
+            out, zq, losses = model(x)
+        h.remove()
+        _, _, idx = model.quantize(pre["z"])
+        f = {"x": x, "pre_quant": pre["z"], "zq": zq, "indices": idx, "out": out,
+             "codebook_loss": losses["codebook_loss"].reshape(1)}
+        save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, f"{name}.safetensors"))
+
+
 def main():
     what = sys.argv[1:] or ["dit", "vqvae"]
     if "dit" in what:
