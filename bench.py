@@ -29,6 +29,9 @@ FLOP_PER_STEP = 3.8815e12      # cond-UNet fwd+bwd at B=32 (Flop
 WORKLOADS = {
     "cond-unet": dict(metric=METRIC, flop=FLOP_PER_STEP),
     "dit": dict(metric="DDPM train steps/sec (DiT-12L image-cond, CelebHQ-256 latents, B=32) on MI355X", flop=6.759e11),
+    # VQVAE encode + decode (no grad) of a batch of 8 CelebHQ-256 images: 2.9497e11 FLOP per image
+    "vqvae": dict(metric="VQVAE encode+decode steps/sec (celebhq.yaml autoencoder, 256x256, B=8) on MI355X",
+                  flop=8 * 2.9497e11),
 }
 PEAK_BF16 = 2.5e15             # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
@@ -80,6 +83,30 @@ def cpu_baseline_dit(cfg, B=32):
                        f"{per:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
 
 
+def vqvae_config():
+    from tests.golden.configs import vqvae_celebhq_config
+    return vqvae_celebhq_config()
+
+
+def cpu_baseline_vqvae(cfg, B=8):
+    """The VQVAE oracle's fp32 encode + decode on the host cores (bounded sample: 1 warm-up + 1 timed)."""
+    from oracle import sd_oracle as O, vqvae_oracle as VO
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = O.deterministic_state(VO.vqvae_param_shapes(cfg), seed=0)
+    x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1111)) * 2 - 1
+    times = []
+    with torch.no_grad():
+        for i in range(2):
+            t0 = time.perf_counter()
+            zq, _, _ = VO.encode(sd, cfg, x)
+            VO.decode(sd, cfg, zq)
+            times.append(time.perf_counter() - t0)
+    return dict(value=1.0 / times[-1], unit="steps/s", cores=threads, kind="port",
+                sample=f"VQVAE oracle fp32 encode+decode, B={B} at 256x256, 1 warm-up + 1 timed, {times[-1]:.2f} s/step, "
+                       f"torch CPU {torch.__version__} with {threads} threads")
+
+
 def cpu_baseline(cfg, B=32):
     """The oracle (CPU fp32 restatement of the reference step) on the host cores; bounded sample."""
     from oracle import sd_oracle as O
@@ -104,6 +131,62 @@ def cpu_baseline(cfg, B=32):
     return dict(value=1.0 / times[-1], unit="steps/s", cores=threads, kind="port",
                 sample=f"oracle fp32 train step (fwd+bwd+clip+Adam+EMA), B={B}, 1 warm-up + 1 timed step, "
                        f"{times[-1]:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
+
+
+def main_vqvae(args, wl, world, rank, device):
+    """VQVAE encode + decode (inference) of a synthetic CelebHQ-256 batch of 8 images per GPU (replicas)."""
+    from models.vqvae import VQVAE
+    cfg = vqvae_config()
+    torch.manual_seed(1111)
+    model = VQVAE(3, cfg).to(device)
+    B = 8
+    x = (torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1111 + rank)) * 2 - 1).to(device)
+    eng = model._eng(x)
+
+    def step():
+        zq, loss, idx = eng.encode(x)
+        eng.decode(zq)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = e.item()
+    sps = args.steps / elapsed
+    from sdmi import kernels as K
+    K.PROFILE = []
+    step()
+    torch.cuda.synchronize()
+    prof, K.PROFILE = K.PROFILE, None
+    fl = sum(p[1] for p in prof if p[0].startswith("gemm"))
+    ms = sum(p[2].elapsed_time(p[3]) for p in prof if p[0].startswith("gemm"))
+    result = {"metric": wl["metric"], "value": sps * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+              "warmup": args.warmup, "ms_per_step": 1000.0 / sps, "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": "bf16", "data": "synthetic 256x256 images, random-init weights",
+              "config": {"workload": "VQVAE celebhq.yaml encode + quantize + decode (inference)", "model": "VQVAE 22.0M",
+                         "per_gpu_batch": B, "image": [3, 256, 256], "latent": [4, 32, 32],
+                         "parallelism": f"replicas{world}"},
+              "images_per_s": sps * B * world, "model_flops_utilization": wl["flop"] * sps / PEAK_BF16,
+              "roofline": {"bound": "mfma", "kernel": "sdmi gemm_kernel (all implicit-GEMM conv launches of one step)",
+                           "achieved": fl / (ms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
+                           "frac": fl / (ms * 1e-3) / PEAK_BF16, "traffic": None, "gemm_ms_per_step": ms}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_vqvae(cfg)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -137,6 +220,8 @@ def main():
 
     wl = WORKLOADS[args.workload]
     is_dit = args.workload == "dit"
+    if args.workload == "vqvae":
+        return main_vqvae(args, wl, world, rank, device)
     cfg = dit_config() if is_dit else cond_config()
     torch.manual_seed(1111)  # identical initial weights on every rank (DDP broadcasts rank 0's)
     group = dist.group.WORLD if world > 1 else None

@@ -194,6 +194,21 @@ int sdmi_nchw_to_tokens_bf16(const float* src, int B, int C, int H, int W, int p
 int sdmi_mse_patch(const float* pred, int ld, const float* target, int B, int C, int H, int W, int p, float gscale,
                    const float* gscale_dev, void* grad, float* ws, float* loss, sdmi_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * VQVAE latent interface (models/vqvae.py:93-153).
+ *  sdmi_vq_quantize : pre_quant_conv (1x1, fp32; w = NULL: identity) of the encoder output z (NHWC fp32 [P][ldz],
+ *                     C <= 8 valid channels), nearest codebook row by torch.cdist's mm form sqrt(max(|x|^2 + |e|^2
+ *                     - 2 x.e, 0)) with first-minimum argmin, straight-through output zq = x + (q - x) (NCHW fp32),
+ *                     int64 indices (B*H*W), optional pre-quantisation latent xq (NCHW fp32) and the codebook /
+ *                     commitment loss mean((q - x)^2). ws: sdmi_vq_workspace(B*HW) bytes.
+ *  sdmi_pointwise_in: post_quant_conv (1x1, fp32) of an NCHW fp32 latent into NHWC bf16 [P][ld] (tail zeroed).
+ * ------------------------------------------------------------------------------------------- */
+size_t sdmi_vq_workspace(long long pixels);
+int sdmi_vq_quantize(const float* z, int ldz, const float* w, const float* b, const float* codebook, int K, int B,
+                     int HW, int C, float* zq, long long* idx, float* xq, float* ws, float* loss, sdmi_stream_t stream);
+int sdmi_pointwise_in(const float* z, int B, int C, int HW, const float* w, const float* b, int cout, void* out,
+                      int ld, sdmi_stream_t stream);
+
 /* bf16 GEMM-layout weight packing (the per-step fp32 -> bf16 cast that autocast performs,
  * train_ddpm_cond_celebhq_multi_gpu.py:281-283, fused with the layout change):
  * dst[o][a][b][i] = bf16(src[o*so + i*si + (kh_off + kh_mul*a)*skh + (kw_off + kw_mul*b)*skw]), 0 for i >= I. */

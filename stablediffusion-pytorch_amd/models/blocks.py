@@ -84,6 +84,20 @@ class MidBlock(_ParamBlock):
         _add_residual(self, num_layers + 1, in_channels, out_channels)
 
 
+class UpBlock(_ParamBlock):
+    """VQVAE decoder block: ConvTranspose(4, 2, 1) of the full input, num_layers x (resnet, [self-attn])
+    (blocks.py:270-370; no skip concatenation)."""
+
+    def __init__(self, in_channels, out_channels, t_emb_dim, up_sample, num_heads, num_layers, attn, norm_channels):
+        super().__init__()
+        self.num_layers, self.up_sample, self.t_emb_dim, self.attn = num_layers, up_sample, t_emb_dim, attn
+        _add_resnets(self, num_layers, in_channels, out_channels, t_emb_dim, norm_channels)
+        if attn:
+            _add_attention(self, num_layers, out_channels, num_heads, norm_channels)
+        _add_residual(self, num_layers, in_channels, out_channels)
+        self.up_sample_conv = nn.ConvTranspose2d(in_channels, in_channels, 4, 2, 1) if up_sample else nn.Identity()
+
+
 class UpBlockUnet(_ParamBlock):
     """ConvTranspose(4, 2, 1) of the lower half, concat skip, num_layers x (resnet, self-attn, [cross])
     (blocks.py:373-499)."""

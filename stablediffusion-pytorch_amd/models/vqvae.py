@@ -1,0 +1,105 @@
+"""Drop-in VQVAE (reference models/vqvae.py:6-158) on the MI355X HIP path.
+
+Same constructor, assertions, module tree and state-dict keys as the reference (encoder_conv_in,
+encoder_layers / encoder_mids (DownBlock / MidBlock), encoder_norm_out, encoder_conv_out, pre_quant_conv,
+embedding, post_quant_conv, decoder_conv_in, decoder_mids, decoder_layers (UpBlock), decoder_norm_out,
+decoder_conv_out), so gen_vqvae_latents.py / sample_ddpm_*.py load a reference checkpoint and call
+`encode(im)` -> (z, {'codebook_loss', 'commitment_loss'}), `decode(z)` and `forward(x)` -> (out, z, losses)
+unchanged. encode / decode run as one schedule of gfx950 kernels (sdmi.vqvae_engine) in inference mode
+(the reference's latent-generation and decoding path); gradients through the VQVAE are not provided.
+"""
+import torch
+import torch.nn as nn
+
+from models.blocks import DownBlock, MidBlock, UpBlock
+from sdmi import _lib
+from sdmi.vqvae_engine import VQVAEEngine
+
+
+class VQVAE(nn.Module):
+    def __init__(self, im_channels, model_config):
+        super().__init__()
+        cfg = model_config
+        self.im_channels = im_channels
+        self.down_channels = cfg["down_channels"]
+        self.mid_channels = cfg["mid_channels"]
+        self.down_sample = cfg["down_sample"]
+        self.num_down_layers = cfg["num_down_layers"]
+        self.num_mid_layers = cfg["num_mid_layers"]
+        self.num_up_layers = cfg["num_up_layers"]
+        self.attns = cfg["attn_down"]
+        self.z_channels = cfg["z_channels"]
+        self.codebook_size = cfg["codebook_size"]
+        self.norm_channels = cfg["norm_channels"]
+        self.num_heads = cfg["num_heads"]
+        assert self.mid_channels[0] == self.down_channels[-1]
+        assert self.mid_channels[-1] == self.down_channels[-1]
+        assert len(self.down_sample) == len(self.down_channels) - 1
+        assert len(self.attns) == len(self.down_channels) - 1
+        self.up_sample = list(reversed(self.down_sample))
+        dc, mc = self.down_channels, self.mid_channels
+        self.encoder_conv_in = nn.Conv2d(im_channels, dc[0], kernel_size=3, padding=(1, 1))
+        self.encoder_layers = nn.ModuleList([
+            DownBlock(dc[i], dc[i + 1], t_emb_dim=None, down_sample=self.down_sample[i], num_heads=self.num_heads,
+                      num_layers=self.num_down_layers, attn=self.attns[i], norm_channels=self.norm_channels)
+            for i in range(len(dc) - 1)])
+        self.encoder_mids = nn.ModuleList([
+            MidBlock(mc[i], mc[i + 1], t_emb_dim=None, num_heads=self.num_heads, num_layers=self.num_mid_layers,
+                     norm_channels=self.norm_channels)
+            for i in range(len(mc) - 1)])
+        self.encoder_norm_out = nn.GroupNorm(self.norm_channels, dc[-1])
+        self.encoder_conv_out = nn.Conv2d(dc[-1], self.z_channels, kernel_size=3, padding=1)
+        self.pre_quant_conv = nn.Conv2d(self.z_channels, self.z_channels, kernel_size=1)
+        self.embedding = nn.Embedding(self.codebook_size, self.z_channels)
+        self.post_quant_conv = nn.Conv2d(self.z_channels, self.z_channels, kernel_size=1)
+        self.decoder_conv_in = nn.Conv2d(self.z_channels, mc[-1], kernel_size=3, padding=(1, 1))
+        self.decoder_mids = nn.ModuleList([
+            MidBlock(mc[i], mc[i - 1], t_emb_dim=None, num_heads=self.num_heads, num_layers=self.num_mid_layers,
+                     norm_channels=self.norm_channels)
+            for i in reversed(range(1, len(mc)))])
+        self.decoder_layers = nn.ModuleList([
+            UpBlock(dc[i], dc[i - 1], t_emb_dim=None, up_sample=self.down_sample[i - 1], num_heads=self.num_heads,
+                    num_layers=self.num_up_layers, attn=self.attns[i - 1], norm_channels=self.norm_channels)
+            for i in reversed(range(1, len(dc)))])
+        self.decoder_norm_out = nn.GroupNorm(self.norm_channels, dc[0])
+        self.decoder_conv_out = nn.Conv2d(dc[0], im_channels, kernel_size=3, padding=1)
+        self._engine = None
+        self._ptrs = None
+
+    def _eng(self, t):
+        if not t.is_cuda:
+            raise RuntimeError("the sdmi VQVAE runs on the MI355X HIP path only (move the model and inputs to cuda)")
+        _lib.lib()
+        params = dict(self.named_parameters())
+        ptrs = [p.data_ptr() for p in params.values()]
+        if self._engine is None or ptrs != self._ptrs:
+            self._engine = VQVAEEngine(self.model_config_dict(), {k: v.detach() for k, v in params.items()},
+                                       im_channels=self.im_channels)
+            self._ptrs = ptrs
+        self._engine.refresh_weights()  # bf16 GEMM-layout copies of the (possibly updated) fp32 weights
+        return self._engine
+
+    def model_config_dict(self):
+        return {"down_channels": self.down_channels, "mid_channels": self.mid_channels,
+                "down_sample": self.down_sample, "attn_down": self.attns, "num_down_layers": self.num_down_layers,
+                "num_mid_layers": self.num_mid_layers, "num_up_layers": self.num_up_layers,
+                "z_channels": self.z_channels, "codebook_size": self.codebook_size,
+                "norm_channels": self.norm_channels, "num_heads": self.num_heads}
+
+    @torch.no_grad()
+    def quantize_indices(self, x):
+        """Encode and also return the codebook indices (B, h, w) int64 (vqvae.py:124-125)."""
+        return self._eng(x).encode(x)
+
+    @torch.no_grad()
+    def encode(self, x):
+        zq, loss, _ = self._eng(x).encode(x)
+        return zq, {"codebook_loss": loss[0], "commitment_loss": loss[0]}
+
+    @torch.no_grad()
+    def decode(self, z):
+        return self._eng(z).decode(z)
+
+    def forward(self, x):
+        z, quant_losses = self.encode(x)
+        return self.decode(z), z, quant_losses

@@ -91,6 +91,9 @@ SIGNATURES = {
     "sdmi_mod_finalize": ([_P, _I, _I, _I, _I, _P, _I, _P], _I),
     "sdmi_tokens_to_nchw": ([_P, _I, _I, _I, _I, _I, _I, _I, _P, _P], _I),
     "sdmi_nchw_to_tokens_bf16": ([_P, _I, _I, _I, _I, _I, _P, _I, _P], _I),
+    "sdmi_vq_workspace": ([_L], _SZ),
+    "sdmi_vq_quantize": ([_P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P], _I),
+    "sdmi_pointwise_in": ([_P, _I, _I, _I, _P, _P, _I, _P, _I, _P], _I),
     "sdmi_mse_patch": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
 }
 

@@ -72,3 +72,22 @@ def test_scheduler_tables_host():
     assert torch.equal(s.alpha_cum_prod, o.alpha_cum_prod)
     with pytest.raises(RuntimeError):
         s.add_noise(torch.zeros(1, 4, 8, 8), torch.zeros(1, 4, 8, 8), torch.zeros(1, dtype=torch.long))
+
+
+def test_dit_and_vqvae_module_surfaces_match_reference_keys():
+    """The drop-in DIT / VQVAE modules register exactly the reference's state-dict keys and shapes (the oracle's
+    tables are themselves checked against the reference modules by the golden generator)."""
+    from models.transformer import DIT
+    from models.vqvae import VQVAE
+    from oracle import dit_oracle as DO, vqvae_oracle as VO
+    from tests.golden.configs import SMALL_DIT, dit12l_config, vqvae_celebhq_config, SMALL_VQVAE
+    for cfg in (SMALL_DIT, dit12l_config()):
+        sd = DIT(4, cfg).state_dict()
+        ref = DO.dit_param_shapes(cfg)
+        assert list(sd) == list(ref) and all(tuple(sd[k].shape) == tuple(ref[k]) for k in sd)
+    for cfg in (SMALL_VQVAE, vqvae_celebhq_config()):
+        sd = VQVAE(3, cfg).state_dict()
+        ref = VO.vqvae_param_shapes(cfg)
+        assert list(sd) == list(ref) and all(tuple(sd[k].shape) == tuple(ref[k]) for k in sd)
+    assert sum(v.numel() for v in DIT(4, dit12l_config()).state_dict().values()) == 18286054
+    assert sum(v.numel() for v in VQVAE(3, vqvae_celebhq_config()).state_dict().values()) == 21994479
