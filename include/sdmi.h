@@ -209,6 +209,23 @@ int sdmi_vq_quantize(const float* z, int ldz, const float* w, const float* b, co
 int sdmi_pointwise_in(const float* z, int B, int C, int HW, const float* w, const float* b, int cout, void* out,
                       int ld, sdmi_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Sampling steps (scheduler/linear_noise_scheduler.py), fp32 elementwise, bit-exact to the reference given the
+ * same noise (correctly rounded fp32 div / sqrt, no FMA contraction).
+ *  sdmi_ddpm_prev : LinearNoiseScheduler.sample_prev_timestep (:50-78); timestep read from device memory
+ *                   (t_dev), z unused at t == 0, x0 (clamped prediction) optional; decrement_t: t_dev -= 1 after
+ *                   the step (capturable sampling loop, no host round trip per step).
+ *  sdmi_ddim_prev : DDIMSampler.sample_one_step (:164-182) for alpha_t = abar[t], alpha_prev = abar[t_prev].
+ *  sdmi_affine_step: DDPMSampler.sample_one_step (:111-124): out = (c1 x - c2 eps) + sqrt(var) z (z NULL: + 0).
+ * ------------------------------------------------------------------------------------------- */
+int sdmi_ddpm_prev(const float* xt, const float* eps, const float* z, long long n, long long* t_dev, const float* betas,
+                   const float* alphas, const float* abar, const float* s1m, float* prev, float* x0, int decrement_t,
+                   sdmi_stream_t stream);
+int sdmi_ddim_prev(const float* xt, const float* eps, const float* noise, long long n, float alpha_t, float alpha_prev,
+                   float eta, float* out, sdmi_stream_t stream);
+int sdmi_affine_step(const float* x, const float* eps, const float* z, long long n, float c1, float c2, float var,
+                     float* out, sdmi_stream_t stream);
+
 /* bf16 GEMM-layout weight packing (the per-step fp32 -> bf16 cast that autocast performs,
  * train_ddpm_cond_celebhq_multi_gpu.py:281-283, fused with the layout change):
  * dst[o][a][b][i] = bf16(src[o*so + i*si + (kh_off + kh_mul*a)*skh + (kw_off + kw_mul*b)*skw]), 0 for i >= I. */

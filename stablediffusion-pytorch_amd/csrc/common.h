@@ -26,6 +26,22 @@ __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
+// IEEE fp32 operations that the compiler may not fuse into FMAs (HIP compiles with fp-contract=fast; the
+// header intrinsics __fmul_rn / __fadd_rn are plain contractible operators). Used where results must be
+// bit-identical to the reference's eager fp32 ops (scheduler arithmetic).
+__device__ __forceinline__ float mul_ieee(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float add_ieee(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ float sub_ieee(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
+
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 
 // d/dx silu(x) = s(x) * (1 + x * (1 - s(x)))

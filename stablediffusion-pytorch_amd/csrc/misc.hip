@@ -101,7 +101,7 @@ __global__ void add_noise_kernel(const float* x0, const float* eps, const long l
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
     int b = (int)(i / per);
     long long ti = t[b];
-    out[i] = __fadd_rn(__fmul_rn(sa[ti], x0[i]), __fmul_rn(s1a[ti], eps[i]));
+    out[i] = add_ieee(mul_ieee(sa[ti], x0[i]), mul_ieee(s1a[ti], eps[i]));
   }
 }
 

@@ -1,0 +1,115 @@
+// Reverse-diffusion (sampling) steps for gfx950, one fused elementwise pass each
+// (reference scheduler/linear_noise_scheduler.py).
+//
+//  ddpm_prev : LinearNoiseScheduler.sample_prev_timestep (:50-78). The timestep is read from DEVICE memory and
+//              the per-step scalars (sqrt(abar_t), sqrt(alpha_t), the posterior sigma) are derived in-kernel
+//              from the reference's fp32 tables with correctly rounded fp32 division / sqrt and no FMA
+//              contraction, so x_{t-1} and x0 are bit-identical to the reference for the same z -- and a
+//              whole sampling step (model forward + this kernel) can be captured once and replayed with a
+//              device-side timestep counter (no host sync per step; the reference syncs on `t == 0`).
+//  ddim_prev : DDIMSampler.sample_one_step (:164-182): x_{t-1} = sqrt(a_prev/a_t) x_t + (sqrt(1 - a_prev -
+//              sigma^2) - sqrt(a_prev (1 - a_t) / a_t)) eps + sigma noise, sigma = eta sqrt(...).
+//  affine    : DDPMSampler.sample_one_step (:111-124): (c1 x - c2 eps) + sqrt(var) z with host table scalars.
+#include "common.h"
+#include "../../include/sdmi.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int NT = 256;
+
+// IEEE fp32 division / square root, correctly rounded: evaluated in fp64 and rounded once to fp32 (a double
+// result of two floats' quotient or a float's root rounds to the correctly rounded float: p = 53 >= 2*24 + 2).
+// The gfx950 fp32 fast paths (v_rcp / v_sqrt based) are ~1 ulp and would break bit parity with the reference.
+__device__ __forceinline__ float div_ieee(float a, float b) { return (float)((double)a / (double)b); }
+__device__ __forceinline__ float sqrt_ieee(float a) { return (float)__dsqrt_rn((double)a); }
+
+__global__ void ddpm_prev_kernel(const float* xt, const float* eps, const float* z, long long n, const long long* tp,
+                                 const float* betas, const float* alphas, const float* abar, const float* s1m,
+                                 float* prev, float* x0out) {
+#pragma clang fp contract(off)
+  const long long t = *tp;
+  const float sq_abar = sqrt_ieee(abar[t]);
+  const float s1 = s1m[t], beta = betas[t], sq_alpha = sqrt_ieee(alphas[t]);
+  float sigma = 0.f;
+  if (t > 0) {
+    const float var = mul_ieee(div_ieee(sub_ieee(1.0f, abar[t - 1]), sub_ieee(1.0f, abar[t])), beta);
+    sigma = sqrt_ieee(var);  // variance ** 0.5 (torch pow(x, 0.5) is sqrt)
+  }
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const float x = xt[i], e = eps[i];
+    float x0 = div_ieee(sub_ieee(x, mul_ieee(s1, e)), sq_abar);
+    x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+    float mean = sub_ieee(x, div_ieee(mul_ieee(beta, e), s1));
+    mean = div_ieee(mean, sq_alpha);
+    if (x0out) x0out[i] = x0;
+    prev[i] = t > 0 ? add_ieee(mean, mul_ieee(sigma, z[i])) : mean;
+  }
+}
+
+// the device timestep counter moves to t - 1 once every block of the step kernel has read it: a separate
+// single-thread launch ordered after the step on the same stream
+__global__ void dec_t_kernel(long long* tp) {
+  if (threadIdx.x == 0 && *tp > 0) *tp = *tp - 1;
+}
+
+__global__ void ddim_prev_kernel(const float* xt, const float* eps, const float* noise, long long n, float at,
+                                 float ap, float eta, float* out) {
+#pragma clang fp contract(off)
+  // sigma_t = eta * sqrt((1 - a_prev) / (1 - a_t) * (1 - a_t / a_prev))
+  const float sigma = mul_ieee(eta, sqrt_ieee(mul_ieee(div_ieee(sub_ieee(1.0f, ap), sub_ieee(1.0f, at)),
+                                                     sub_ieee(1.0f, div_ieee(at, ap)))));
+  const float c1 = sqrt_ieee(div_ieee(ap, at));
+  const float c2 = sub_ieee(sqrt_ieee(sub_ieee(sub_ieee(1.0f, ap), mul_ieee(sigma, sigma))),
+                             sqrt_ieee(div_ieee(mul_ieee(ap, sub_ieee(1.0f, at)), at)));
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    float v = add_ieee(mul_ieee(c1, xt[i]), mul_ieee(c2, eps[i]));
+    out[i] = add_ieee(v, mul_ieee(sigma, noise ? noise[i] : 0.0f));
+  }
+}
+
+__global__ void affine_kernel(const float* x, const float* eps, const float* z, long long n, float c1, float c2,
+                              float var, float* out) {
+#pragma clang fp contract(off)
+  const float s = sqrt_ieee(var);  // torch.sqrt(var), correctly rounded (host-CPU vector sqrt is not always)
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const float mean = sub_ieee(mul_ieee(c1, x[i]), mul_ieee(c2, eps[i]));
+    out[i] = z ? add_ieee(mean, mul_ieee(s, z[i])) : add_ieee(mean, 0.0f);
+  }
+}
+
+int grid_for(long long n) { return (int)std::max<long long>(1, std::min<long long>((n + NT - 1) / NT, 4096)); }
+
+}  // namespace
+
+extern "C" int sdmi_ddpm_prev(const float* xt, const float* eps, const float* z, long long n, long long* t_dev,
+                              const float* betas, const float* alphas, const float* abar, const float* s1m,
+                              float* prev, float* x0, int decrement_t, sdmi_stream_t stream) {
+  if (!xt || !eps || !t_dev || !betas || !alphas || !abar || !s1m || !prev || n <= 0) return -1;
+  hipLaunchKernelGGL(ddpm_prev_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, xt, eps, z, n, t_dev,
+                     betas, alphas, abar, s1m, prev, x0);
+  SDMI_CHECK_LAUNCH();
+  if (decrement_t) {
+    hipLaunchKernelGGL(dec_t_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t_dev);
+    SDMI_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int sdmi_ddim_prev(const float* xt, const float* eps, const float* noise, long long n, float alpha_t,
+                              float alpha_prev, float eta, float* out, sdmi_stream_t stream) {
+  if (!xt || !eps || !out || n <= 0) return -1;
+  hipLaunchKernelGGL(ddim_prev_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, xt, eps, noise, n, alpha_t,
+                     alpha_prev, eta, out);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_affine_step(const float* x, const float* eps, const float* z, long long n, float c1, float c2,
+                                float var, float* out, sdmi_stream_t stream) {
+  if (!x || !eps || !out || n <= 0) return -1;
+  hipLaunchKernelGGL(affine_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, x, eps, z, n, c1, c2, var,
+                     out);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}

@@ -94,6 +94,9 @@ SIGNATURES = {
     "sdmi_vq_workspace": ([_L], _SZ),
     "sdmi_vq_quantize": ([_P, _I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P], _I),
     "sdmi_pointwise_in": ([_P, _I, _I, _I, _P, _P, _I, _P, _I, _P], _I),
+    "sdmi_ddpm_prev": ([_P, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
+    "sdmi_ddim_prev": ([_P, _P, _P, _L, _F, _F, _F, _P, _P], _I),
+    "sdmi_affine_step": ([_P, _P, _P, _L, _F, _F, _F, _P, _P], _I),
     "sdmi_mse_patch": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
 }
 

@@ -2,7 +2,7 @@
 implementation (read-only at /root/reference) in THIS container. Only input/output tensors are
 committed (safetensors); weights regenerate from oracle.sd_oracle.deterministic_state.
 
-Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae]
+Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae] [sampler]
 
 The reference DIT zero-initialises adaptive_norm_layer and proj_out (models/transformer.py:147-151,
 transformer_layer.py:70-71), so a freshly built reference model outputs exactly 0; the fixtures load
@@ -168,12 +168,47 @@ def gen_vqvae():
         save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, f"{name}.safetensors"))
 
 
+def gen_sampler():
+    """DDIMSampler / DDPMSampler steps (scheduler/linear_noise_scheduler.py:93-232) with a fixed-output model
+    and fixed noise (torch.randn_like patched), so the step arithmetic alone is pinned."""
+    import scheduler.linear_noise_scheduler as S
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(2, 4, 8, 8, generator=g)
+    eps = torch.randn(2, 4, 8, 8, generator=g)
+    noise = torch.randn(2, 4, 8, 8, generator=g)
+    f = {"x": x, "eps": eps, "noise": noise}
+
+    class Fixed(torch.nn.Module):
+        def forward(self, *a, **k):
+            return eps.clone()
+
+    real = torch.randn_like
+    torch.randn_like = lambda t, *a, **k: noise.clone()
+    try:
+        ddim = S.DDIMSampler(Fixed(), beta=(0.00085, 0.012), T=1000)
+        ddim.cond_input = None
+        for eta in (0.0, 1.0):
+            for (t, tp) in ((801, 760), (11, 1), (1, 0)):
+                f[f"ddim_eta{eta:g}_{t}_{tp}"] = ddim.sample_one_step(x, t, tp, eta)
+        f["ddim_alpha_t_bar"] = ddim.alpha_t_bar.clone()
+        ddpm = S.DDPMSampler(Fixed(), beta=(0.0001, 0.02), T=1000)
+        for k in ("coeff_1", "coeff_2", "posterior_variance"):
+            f[f"ddpm_{k}"] = getattr(ddpm, k).clone()  # host-CPU cumprod rounding varies by CPU: pin the tables
+        for t in (999, 500, 0):
+            f[f"ddpm_{t}"] = ddpm.sample_one_step(x, t)
+    finally:
+        torch.randn_like = real
+    save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, "samplers.safetensors"))
+
+
 def main():
-    what = sys.argv[1:] or ["dit", "vqvae"]
+    what = sys.argv[1:] or ["dit", "vqvae", "sampler"]
     if "dit" in what:
         gen_dit()
-    if "vqvae" in what and "gen_vqvae" in globals():
-        globals()["gen_vqvae"]()
+    if "vqvae" in what:
+        gen_vqvae()
+    if "sampler" in what:
+        gen_sampler()
     print("fixtures written to", HERE)
 
 

@@ -117,3 +117,15 @@ def test_full_unet_forward(name, cfg):
     with torch.no_grad():
         out = O.unet_forward(sd, cfg, f["x"], f["t"], cond)
     assert rel(out, f["out"]) < 1e-5
+
+
+def test_sampler_steps_bit_exact():
+    """DDIMSampler / DDPMSampler step arithmetic (scheduler/linear_noise_scheduler.py:93-232) vs the reference."""
+    f = fx("samplers")
+    abar = O.ddim_alpha_bar((0.00085, 0.012), 1000)
+    for eta in (0.0, 1.0):
+        for (t, tp) in ((801, 760), (11, 1), (1, 0)):
+            out = O.ddim_step(abar, f["x"], f["eps"], f["noise"], t, tp, eta)
+            assert torch.equal(out, f[f"ddim_eta{eta:g}_{t}_{tp}"]), (eta, t, tp)
+    for t in (999, 500, 0):
+        assert torch.equal(O.ddpm_sampler_step((0.0001, 0.02), 1000, f["x"], f["eps"], f["noise"], t), f[f"ddpm_{t}"])
