@@ -199,9 +199,9 @@ def main():
     ap.add_argument("--workload", default="cond-unet", choices=sorted(WORKLOADS),
                     help="cond-unet (the headline metric, default) or dit (DiT-12L training step)")
     ap.add_argument("--profile-gemm", action="store_true", default=True)
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the step as one captured hipGraph (N == 1; default off: eager issue with the "
-                         "weight-gradient stream overlapped measured faster than the captured graph)")
+    ap.add_argument("--issue", default="plan", choices=("plan", "eager", "graph"),
+                    help="plan (default): the step recorded once and its native calls replayed (sdmi.plan); eager: "
+                         "per-step Python issue; graph: single-stream hipGraph (N == 1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -239,6 +239,8 @@ def main():
     x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
     gen = torch.Generator(device=device).manual_seed(1111 + rank)
 
+    drop_p = 0.9 if is_dit else 0.1  # image cond-drop (Model_DiT_12L_config: 0.9; celebhq_text_image_cond: 0.1)
+
     def eager_step():
         noise = torch.randn(x0.shape, device=device, generator=gen)
         t = torch.randint(0, 1000, (B,), device=device, generator=gen)
@@ -251,10 +253,15 @@ def main():
         keep = (torch.rand(B, device=device, generator=gen) > 0.1).float()  # diffusion_utils.py:31-37
         trainer.step(x0, noise, t, txt, mask, mask_keep=keep)
 
-    use_graph = args.graph and world == 1 and not is_dit
-    if use_graph:
+    issue = args.issue
+    if issue == "graph" and world > 1:
+        issue = "plan"
+    if issue != "eager":
         from sdmi.graph import CapturedTrainStep
-        cap = CapturedTrainStep(trainer, x0, text, empty, mask, B, generator=gen)
+        if issue == "graph" and not is_dit:
+            trainer.engine.side = None  # single-stream capture
+        cap = CapturedTrainStep(trainer, x0, None if is_dit else text, empty, mask, B, generator=gen, drop_p=drop_p,
+                                mode=issue)
         one_step = cap.step
     else:
         one_step = eager_step
@@ -323,7 +330,7 @@ def main():
         "per_gpu_steps_per_s": steps_per_s, "samples_per_s": steps_per_s * B * world,
         "model_flops_utilization": FLOP * steps_per_s / PEAK_BF16,
         "last_loss": state[S_LOSS], "last_grad_norm": state[S_NORM], "last_step_skipped": bool(state[S_SKIP]),
-        "hip_graph": use_graph,
+        "issue": issue,
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -13,6 +13,7 @@ import torch.nn.functional as F
 
 from sdmi import _lib
 from sdmi import kernels as K
+from sdmi import plan
 
 
 def _require_cuda(t, what):
@@ -46,9 +47,9 @@ class LinearNoiseScheduler:
         if not original.is_cuda:
             raise RuntimeError("sdmi LinearNoiseScheduler.add_noise runs on the HIP path only (cuda tensors)")
         tab = self.tables(original.device)
-        x0 = original.float().contiguous()
-        eps = noise.float().contiguous()
-        tt = torch.as_tensor(t, device=original.device).long().reshape(-1).contiguous()
+        x0 = plan.as_operand(original)
+        eps = plan.as_operand(noise)
+        tt = plan.timesteps(t, original.device)
         if tt.numel() != x0.shape[0]:
             raise ValueError("t must have one timestep per sample")
         out = torch.empty_like(x0)
@@ -63,8 +64,8 @@ class LinearNoiseScheduler:
         sampling step can then be replayed T times)."""
         _require_cuda(xt, "LinearNoiseScheduler.sample_prev_timestep")
         tab = self.tables(xt.device)
-        x = xt.float().contiguous()
-        e = noise_pred.float().contiguous()
+        x = plan.as_operand(xt)
+        e = plan.as_operand(noise_pred)
         if isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.int64:
             t_dev = t.reshape(-1)[:1]
             if z is None:  # t unknown on the host: always draw (unused by the kernel at t == 0)
@@ -75,7 +76,7 @@ class LinearNoiseScheduler:
             if z is None and ti > 0:
                 z = torch.randn(xt.shape).to(xt.device)
         prev, x0 = out if out is not None else (torch.empty_like(x), torch.empty_like(x))
-        zz = z.float().contiguous() if z is not None else None
+        zz = plan.as_operand(z) if z is not None else None
         _lib.check(_lib.lib().sdmi_ddpm_prev(x.data_ptr(), e.data_ptr(), K._p(zz), x.numel(), t_dev.data_ptr(),
                                              tab["betas"].data_ptr(), tab["alphas"].data_ptr(),
                                              tab["alpha_cum_prod"].data_ptr(),

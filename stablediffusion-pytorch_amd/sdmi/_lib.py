@@ -5,6 +5,8 @@ The product path has no fallback: if the library is missing or fails to load, ev
 import ctypes
 import os
 
+from . import plan
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsdmi.so")
 
@@ -101,6 +103,39 @@ SIGNATURES = {
 }
 
 
+class _Recorded:
+    """Launch entry point (takes a stream): called now, and appended to the plan while one is recorded."""
+    __slots__ = ("fn", "__name__")
+
+    def __init__(self, fn, name):
+        self.fn = fn
+        self.__name__ = name
+
+    def __call__(self, *args):
+        r = self.fn(*args)
+        if plan.RECORDING is not None:
+            plan.RECORDING.append((self.fn, args))
+        return r
+
+
+class _Lib:
+    """libsdmi.so with its stream-taking entry points wrapped for plan recording (sdmi.plan)."""
+
+    def __init__(self, cdll):
+        self._cdll = cdll
+        for name, (argt, rest) in SIGNATURES.items():
+            fn = getattr(cdll, name)
+            fn.argtypes = argt
+            fn.restype = rest
+            launches = len(argt) > 0 and name not in _HOST_ONLY
+            setattr(self, name, _Recorded(fn, name) if launches else fn)
+
+
+# entry points that only answer host-side queries (never launch; not recorded)
+_HOST_ONLY = {"sdmi_gemm_plan", "sdmi_chan_reduce_workspace", "sdmi_mse_workspace", "sdmi_pack_chunk",
+              "sdmi_optim_workspace", "sdmi_ln_chunk_rows", "sdmi_vq_workspace"}
+
+
 def lib():
     """Load libsdmi.so once (raises if absent: there is no CPU fallback on the product path)."""
     global _lib
@@ -110,12 +145,7 @@ def lib():
         # torch must bring in its HIP runtime first: libsdmi.so's libamdhip64.so.7 dependency then binds
         # to that same (already loaded, same SONAME) runtime instead of loading a second copy.
         import torch  # noqa: F401
-        L = ctypes.CDLL(LIB_PATH)
-        for name, (argt, rest) in SIGNATURES.items():
-            fn = getattr(L, name)
-            fn.argtypes = argt
-            fn.restype = rest
-        _lib = L
+        _lib = _Lib(ctypes.CDLL(LIB_PATH))
     return _lib
 
 

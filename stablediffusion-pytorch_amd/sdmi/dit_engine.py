@@ -17,6 +17,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
+from . import plan
 from .unet_engine import PackPlan, contiguous_run
 
 
@@ -198,12 +199,12 @@ class DiTEngine:
         gh, gw = H // p, W // p
         N = gh * gw
         M = B * N
-        x = x.float().contiguous()
+        x = plan.as_operand(x)
         st = dict(B=B, H=H, W=W, N=N, M=M)
         # ---- patch source (transformer.py:180-188) + patch embedding (patch_embed.py:75-96) ----
         xin = self._new(B * H * W, self.cpad)
         if L["image"]:
-            m = mask.float().contiguous()
+            m = plan.as_operand(mask)
             _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, m.data_ptr(), L["im_in"], m.shape[2],
                                                   m.shape[3], P["cond_conv_in.weight"].data_ptr(), L["im_out"],
                                                   xin.data_ptr(), self.cpad, K._p(mask_keep), K._stream()),
@@ -221,7 +222,7 @@ class DiTEngine:
                geom=g, bias=P["patch_embed_layer.patch_embed.0.bias"], rowbias=self.pos_table(gh, gw), rb_ld=D,
                rb_shift=0, rb_mod=N)
         # ---- time embedding -> t_proj (ReLU) -> ReLU(t_emb) -> all adaLN tables in one GEMM ----
-        t = torch.as_tensor(t, device=self.device).long().reshape(-1)
+        t = plan.timesteps(t, self.device)
         if t.numel() not in (1, B):
             raise ValueError("t must have 1 or B elements")
         e = self._new(B, L["T"])
@@ -237,7 +238,7 @@ class DiTEngine:
         st.update(e=e, h1=h1, r=r, mod=mod)
         ctx = None
         if L["text"]:
-            txt = text.float().contiguous()
+            txt = plan.as_operand(text)
             S = txt.shape[1]
             ctx = self._new(B * S, txt.shape[2])
             _lib.check(_lib.lib().sdmi_nchw_to_nhwc_bf16(txt.data_ptr(), B * S, txt.shape[2], 1, ctx.data_ptr(),

@@ -1,17 +1,21 @@
-"""hipGraph capture of the whole training step.
+"""Captured training step: the reference's step (train_ddpm_cond_celebhq_multi_gpu.py:299-378 /
+Model_DiT_12L_train.py:300-375) recorded once and replayed every iteration.
 
-One eager training step issues ~1,100 kernel launches through ctypes; on MI355X the GPU finishes
-many of them faster than Python can enqueue them. The step is therefore captured once into a
-hipGraph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replayed: every launch, every temporary
-(allocated from the graph's private pool) and every pointer is fixed at capture time. Per-step
-randomness (noise, t, cond-drop) is drawn into static input buffers before each replay, exactly as
-the reference draws it per step (train_ddpm_cond_celebhq_multi_gpu.py:309-342)."""
+mode "plan" (default): sdmi.plan.StepPlan -- the step's native calls (every libsdmi launch, stream / event edge
+and RCCL bucket all-reduce) replayed from a flat list, keeping the two-stream weight-gradient overlap and the
+backward-overlapped gradient all-reduce (N > 1), with all temporaries in a private pool.
+mode "graph": one hipGraph (torch.cuda.CUDAGraph); single-stream only (a two-stream hipGraph replays at the
+same host cost as eager issue on this ROCm) and N == 1 only.
+Per-step randomness (noise, t, cond-drop) is drawn into static buffers before each replay, exactly as the
+reference draws it per step."""
 import torch
+
+from .plan import StepPlan
 
 
 class CapturedTrainStep:
     def __init__(self, trainer, x0, text, empty_text, mask, B, *, warmup=2, generator=None, drop_p=0.1,
-                 text_drop_p=0.1):
+                 text_drop_p=0.1, mode="plan"):
         self.tr = trainer
         dev = x0.device
         self.x0, self.text, self.empty, self.mask = x0, text, empty_text, mask
@@ -22,18 +26,29 @@ class CapturedTrainStep:
         self.t = torch.empty(B, dtype=torch.long, device=dev)
         self.txt = torch.empty_like(text) if text is not None else None
         self.keep = torch.empty(B, dtype=torch.float32, device=dev)
+        self.mode = mode
         self._draw()
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):  # warm the allocator / lazy init outside the capture
-            for _ in range(warmup):
-                self.tr.step(self.x0, self.noise, self.t, self.txt, self.mask, mask_keep=self.keep)
-        torch.cuda.current_stream(dev).wait_stream(s)
+        for _ in range(warmup):  # allocator / lazy init outside the recording
+            self._run()
         torch.cuda.synchronize(dev)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.tr.step(self.x0, self.noise, self.t, self.txt, self.mask, mask_keep=self.keep)
-        torch.cuda.synchronize(dev)
+        if mode == "plan":
+            self.plan = StepPlan(self._run, dev)
+        elif mode == "graph":
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                self._run()
+            torch.cuda.current_stream(dev).wait_stream(s)
+            torch.cuda.synchronize(dev)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._run()
+            torch.cuda.synchronize(dev)
+        else:
+            raise ValueError(mode)
+
+    def _run(self):
+        self.tr.step(self.x0, self.noise, self.t, self.txt, self.mask, mask_keep=self.keep)
 
     def _draw(self):
         g = self.gen
@@ -42,8 +57,12 @@ class CapturedTrainStep:
         if self.txt is not None:
             drop = torch.rand(self.B, device=self.t.device, generator=g) < self.text_drop_p  # diffusion_utils.py:21-28
             torch.where(drop[:, None, None], self.empty, self.text, out=self.txt)
-        self.keep.copy_((torch.rand(self.B, device=self.t.device, generator=g) > self.drop_p).float())
+        if self.mask is not None:
+            self.keep.copy_((torch.rand(self.B, device=self.t.device, generator=g) > self.drop_p).float())
 
     def step(self):
         self._draw()
-        self.graph.replay()
+        if self.mode == "plan":
+            self.plan.replay()
+        else:
+            self.graph.replay()

@@ -9,6 +9,8 @@ On ROCm the "nccl" backend is RCCL over xGMI; the same class runs with gloo on C
 import torch
 import torch.distributed as dist
 
+from . import plan
+
 
 class BucketReducer:
     def __init__(self, flat, group=None, bucket_bytes=64 << 20):
@@ -25,20 +27,22 @@ class BucketReducer:
         self.launched = 0
         self.works = []
 
-    def _launch(self, lo, hi):
-        view = self.flat[lo:hi]
+    def _issue(self, view):
+        """all-reduce on the reducer stream (also the unit a recorded StepPlan re-issues)."""
         if self.cuda:
-            evs = []
-            for st in [torch.cuda.current_stream(self.flat.device)] + list(self.producers):
-                ev = torch.cuda.Event()
-                ev.record(st)
-                evs.append(ev)
             with torch.cuda.stream(self.stream):
-                for ev in evs:
-                    self.stream.wait_event(ev)
                 self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
         else:
             self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+
+    def _launch(self, lo, hi):
+        view = self.flat[lo:hi]
+        if self.cuda:
+            for st in [torch.cuda.current_stream(self.flat.device)] + list(self.producers):
+                ev = torch.cuda.Event()
+                plan.record_event(ev, st)
+                plan.wait_event(self.stream, ev)
+        plan.record(self._issue, view)
 
     def ready(self, upto):
         """Gradients at flat offsets < upto are final."""
@@ -50,11 +54,14 @@ class BucketReducer:
             self._launch(self.launched, self.total)
             self.launched = self.total
 
+    def _drain(self):
+        for w in self.works:
+            w.wait()  # NCCL/RCCL: makes the current stream wait for the collective (no host sync)
+        self.works = []
+
     def finish(self):
         if self.launched < self.total:
             self.ready(self.total)
-        for w in self.works:
-            w.wait()  # NCCL/RCCL: makes the current stream wait for the collective (no host sync)
+        plan.record(self._drain)
         if self.cuda:
-            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
-        self.works = []
+            plan.wait_stream(torch.cuda.current_stream(self.flat.device), self.stream)

@@ -24,6 +24,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
+from . import plan
 
 
 def _log2(v):
@@ -331,7 +332,7 @@ class UNetEngine:
         st = dict(B=B, H=H, W=W)
         grads = Grads(dev)
         self._grads = grads
-        x = x.float().contiguous()
+        x = plan.as_operand(x)
         # ---- resolutions and concat buffers ----
         nd = len(L["down"]) - 1
         res = [(H, W)]
@@ -349,7 +350,7 @@ class UNetEngine:
         # ---- input staging + first conv (unet_cond_base.py:131-140) ----
         xin = self._new(B * H * W, self.cin_pad)
         if L["image"]:
-            m = mask.float().contiguous()
+            m = plan.as_operand(mask)
             _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, m.data_ptr(), L["im_in"], m.shape[2],
                                                   m.shape[3], P["cond_conv_in.weight"].data_ptr(), L["im_out"],
                                                   xin.data_ptr(), self.cin_pad, K._p(mask_keep), K._stream()),
@@ -366,7 +367,7 @@ class UNetEngine:
         # ---- time embedding (blocks.py:5-24, unet_cond_base.py:148-149) ----
         tape.label = "time"
         T = L["T"]
-        t = torch.as_tensor(t, device=dev).long().reshape(-1)
+        t = plan.timesteps(t, dev)
         if t.numel() not in (1, B):
             raise ValueError("t must have 1 or B elements")
         e = self._new(B, T)
@@ -390,7 +391,7 @@ class UNetEngine:
 
         ctx = None
         if L["text"]:
-            txt = text.float().contiguous()
+            txt = plan.as_operand(text)
             S = txt.shape[1]
             ctx = self._new(B * S, txt.shape[2])
             _lib.check(_lib.lib().sdmi_nchw_to_nhwc_bf16(txt.data_ptr(), B * S, txt.shape[2], 1, ctx.data_ptr(),
@@ -638,7 +639,7 @@ class UNetEngine:
             grads.alias(c["xn"], dy)
             dx, addend = dy, dy
             if dy_read is not None:  # the GroupNorm backward below rewrites dy in place
-                torch.cuda.current_stream(self.device).wait_event(dy_read)
+                plan.wait_event(torch.cuda.current_stream(self.device), dy_read)
         else:
             dx, fresh = grads.get(c["xn"])
             if not fresh:
@@ -790,16 +791,16 @@ class UNetEngine:
             yield
             return
         self._keep.extend(keep)
-        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        plan.wait_stream(self.side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             yield
         self.wg_event = torch.cuda.Event()
-        self.wg_event.record(self.side)
+        plan.record_event(self.wg_event, self.side)
 
     def _join(self):
         """The current stream waits for all weight-gradient work issued so far."""
         if self.side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            plan.wait_stream(torch.cuda.current_stream(self.device), self.side)
 
     # ------------------------------------------------------------------------------------------
     def backward(self, ctx, dpred, grads=None, on_progress=None):

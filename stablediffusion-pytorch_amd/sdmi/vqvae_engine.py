@@ -12,6 +12,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
+from . import plan
 from .unet_engine import PackPlan
 
 
@@ -184,7 +185,7 @@ class VQVAEEngine:
         L, P = self.L, self.P
         B, Cx, H, W = x.shape
         assert Cx == self.im_channels
-        x = x.float().contiguous()
+        x = plan.as_operand(x)
         xin = self._new(B * H * W, self.cin_pad)
         _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, None, 0, 1, 1, None, 0, xin.data_ptr(),
                                               self.cin_pad, None, K._stream()), "sdmi_prep_input")
@@ -228,7 +229,7 @@ class VQVAEEngine:
         L, P = self.L, self.P
         B, Cz, h, w = z.shape
         assert Cz == L["z"]
-        z = z.float().contiguous()
+        z = plan.as_operand(z)
         zin = self._new(B * h * w, 8)
         _lib.check(_lib.lib().sdmi_pointwise_in(z.data_ptr(), B, Cz, h * w, P["post_quant_conv.weight"].data_ptr(),
                                                 P["post_quant_conv.bias"].data_ptr(), Cz, zin.data_ptr(), 8,
