@@ -89,6 +89,9 @@ typedef struct sdmi_gemm_desc {
   /* act 3 (ReLU backward, models/transformer_layer.py:38-42 / transformer.py:107-111): v is kept where
    * aux[orow*ld_aux + n] > 0 (aux = the saved bf16 ReLU output), else 0 */
   const void* aux; int ld_aux;
+  /* split-K slices requested by the caller (0 = built-in heuristic); clamped to >= 1 k-tile per slice and to
+   * 32-bit slab offsets. Used with the measured per-shape table of sdmi/tuned_gemm.json. */
+  int splits_hint;
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */

@@ -1,0 +1,119 @@
+"""Measure the split-K slice count of every GEMM launch of one training step in isolation and write the
+per-shape best to stablediffusion-pytorch_amd/sdmi/tuned_gemm.json (consumed by sdmi.kernels.gemm).
+
+    python scripts/tune_gemm.py [--workload cond-unet|dit] [--out path]
+
+The step is recorded once as a StepPlan (sdmi.plan); each recorded sdmi_gemm call is then re-issued with
+splits_hint in {1, 2, 4, ..., 128} on its own recorded operands (single stream, HIP events, median of 3
+rounds of 10 launches) and the fastest is kept when it beats the built-in heuristic by > 3 %."""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "stablediffusion-pytorch_amd"), REPO]
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def time_launch(L, d, ws, stream, iters=10, rounds=3):
+    import ctypes
+    res = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        L.sdmi_gemm(ctypes.byref(d), ws.data_ptr(), ws.numel() * 4, stream)
+        e0.record()
+        for _ in range(iters):
+            rc = L.sdmi_gemm(ctypes.byref(d), ws.data_ptr(), ws.numel() * 4, stream)
+            assert rc == 0, rc
+        e1.record()
+        torch.cuda.synchronize()
+        res.append(e0.elapsed_time(e1) * 1e3 / iters)
+    return sorted(res)[len(res) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "dit"))
+    ap.add_argument("--out", default=os.path.join(REPO, "stablediffusion-pytorch_amd", "sdmi", "tuned_gemm.json"))
+    args = ap.parse_args()
+    from sdmi import _lib, kernels as K
+    from sdmi.trainer import DDPMTrainer
+    from sdmi.plan import StepPlan
+    import models.unet_cond_base as mc
+    dev = torch.device("cuda", 0)
+    B = 32
+    if args.workload == "dit":
+        from models.transformer import DIT
+        cfg = bench.dit_config()
+        sd = DIT(4, cfg).state_dict()
+        for v in sd.values():
+            if v.abs().max() == 0:
+                v.normal_(0, 0.02)
+        tr = DDPMTrainer(cfg, sd, dev, base="dit", lr=1e-4, ema_decay=None)
+        text = None
+    else:
+        cfg = bench.cond_config()
+        torch.manual_seed(0)
+        tr = DDPMTrainer(cfg, mc.Unet(4, cfg).state_dict(), dev)
+    x0, text_, empty, mask = bench.synthetic_batch(B, dev, 1)
+    if args.workload != "dit":
+        text = text_
+    noise = torch.randn_like(x0)
+    t = torch.randint(0, 1000, (B,), device=dev)
+    keep = torch.ones(B, device=dev)
+    K.TUNED = {}  # tune from the built-in heuristic, not from a previous table
+    step = lambda: tr.step(x0, noise, t, text, mask, mask_keep=keep)  # noqa: E731
+    for _ in range(2):
+        step()
+    tr.engine.side = None if hasattr(tr.engine, "side") else None  # single stream for isolated timing
+    plan = StepPlan(step, dev)
+    L = _lib.lib()
+    ws = torch.empty(1 << 28, dtype=torch.float32, device=dev)  # 1 GiB split-K slabs
+    stream = torch.cuda.current_stream().cuda_stream
+    table = {}
+    if os.path.exists(args.out):
+        table = json.load(open(args.out))
+    seen = {}
+    tot_def = tot_best = 0.0
+    for fn, a in plan.ops:
+        if getattr(fn, "__name__", "") != "sdmi_gemm":
+            continue
+        d = a[0]._obj
+        key = K.gemm_key(d)
+        nkt = (d.k + 63) // 64
+        if key in seen:
+            n, td, tb = seen[key]
+            seen[key] = (n + 1, td, tb)
+            continue
+        d.splits_hint = 0
+        t_def = time_launch(L, d, ws, stream)
+        best, t_best = 0, t_def
+        s = 1
+        while s <= min(128, nkt):
+            if s * d.m * d.n * 4 < min(ws.numel() * 4, 1 << 31):
+                d.splits_hint = s
+                ts = time_launch(L, d, ws, stream)
+                if ts < t_best * 0.97:
+                    best, t_best = s, ts
+            s *= 2
+        d.splits_hint = 0
+        seen[key] = (1, t_def, t_best)
+        if best:
+            table[key] = best
+        elif key in table:
+            del table[key]
+        print(f"{key:60s} default {t_def:8.1f} us  best {t_best:8.1f} us  splits {best or 'heuristic'}", flush=True)
+    for key, (n, td, tb) in seen.items():
+        tot_def += n * td
+        tot_best += n * tb
+    print(f"step GEMM time (isolated, single stream): heuristic {tot_def / 1e3:.3f} ms -> tuned {tot_best / 1e3:.3f} ms")
+    with open(args.out, "w") as f:
+        json.dump(dict(sorted(table.items())), f, indent=0)
+    print("wrote", args.out, len(table), "entries")
+
+
+if __name__ == "__main__":
+    main()

@@ -897,6 +897,11 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
 int plan_splits(const sdmi_gemm_desc* d) {
   long long tiles = (long long)((d->m + BM - 1) / BM) * ((d->n + BN - 1) / BN);
   int nkt = (d->k + BK - 1) / BK;
+  if (d->splits_hint > 0) {
+    int s = std::min(d->splits_hint, nkt);
+    while (s > 1 && (long long)s * d->m * d->n * 4 >= (1LL << 31)) s >>= 1;
+    return std::max(s, 1);
+  }
   int s = 1;
   static int policy = -1;
   if (policy < 0) {

@@ -42,6 +42,7 @@ class GemmDesc(ctypes.Structure):
         ("bias2", ctypes.c_void_p),
         ("rb_mod", ctypes.c_int),
         ("aux", ctypes.c_void_p), ("ld_aux", ctypes.c_int),
+        ("splits_hint", ctypes.c_int),
     ]
 
 

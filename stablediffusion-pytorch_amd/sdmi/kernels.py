@@ -5,6 +5,8 @@ libsdmi.so on torch's current stream. Tensors are NHWC bf16 activations (2-D vie
 with a row stride) and fp32 parameters/statistics.
 """
 import ctypes
+import json
+import os
 
 import torch
 
@@ -29,6 +31,25 @@ def _log2(v):
 
 # optional per-launch timing hook (bench.py): list of (tag, flops, start_event, end_event, info)
 PROFILE = None
+PHASE = ""  # label prefixed to profiled launches ("fwd" / "bwd" / "wg" ...; set by the engines)
+
+# measured split-K slice counts per GEMM shape (scripts/tune_gemm.py -> sdmi/tuned_gemm.json); None = not loaded
+TUNED = None
+_TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gemm.json")
+
+
+def gemm_key(d):
+    """Shape key of a GemmDesc for the tuned split table."""
+    g = d.geom
+    return (f"a{d.a_mode}b{d.b_mode} m{d.m} n{d.n} k{d.k} g{g.kh}x{g.kw}s{g.sy} i{g.ih}c{g.cin} "
+            f"x{int(bool(d.a2))}p{d.perm}")
+
+
+def _tuned():
+    global TUNED
+    if TUNED is None:
+        TUNED = json.load(open(_TUNED_PATH)) if os.path.exists(_TUNED_PATH) else {}
+    return TUNED
 
 
 class _Prof:
@@ -47,7 +68,7 @@ class _Prof:
     def __exit__(self, *a):
         if PROFILE is not None:
             self.e1.record()
-            PROFILE.append((self.tag, self.flops, self.e0, self.e1, self.info))
+            PROFILE.append((self.tag, self.flops, self.e0, self.e1, f"[{PHASE}] {self.info}" if PHASE else self.info))
 
 
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
@@ -87,6 +108,9 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     d.rb_mod = rb_mod
     if aux is not None:
         d.aux, d.ld_aux = aux.data_ptr(), ld_aux or ld_of(aux)
+    tuned = _tuned()
+    if tuned:
+        d.splits_hint = tuned.get(gemm_key(d), 0)
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")

@@ -10,12 +10,14 @@ Master weights, Adam moments and the EMA copy are flat fp32 buffers (sdmi.store.
 GradScaler state (scale, growth tracker, step, skip flag) lives on the device, so a step never
 synchronises with the host (the reference's .item()/isfinite syncs at :348-371 become device flags)."""
 import math
+import os
 
 import torch
 import torch.distributed as dist
 
 from . import _lib
 from . import kernels as K
+from . import plan
 from .reducer import BucketReducer
 from .store import FlatStore, param_label
 from .unet_engine import UNetEngine
@@ -67,6 +69,10 @@ class DDPMTrainer:
         if self.reducer is not None and getattr(self.engine, "side", None) is not None:
             self.reducer.producers.append(self.engine.side)
         self._progress = None
+        self.main_stream = None
+        if self.device.type == "cuda" and os.environ.get("SDMI_MAIN_PRIORITY", "0") == "1":
+            lo, hi = torch.cuda.Stream.priority_range()
+            self.main_stream = torch.cuda.Stream(device=self.device, priority=hi)
         self.engine.refresh_weights()
 
     # ------------------------------------------------------------------------------------------
@@ -99,7 +105,19 @@ class DDPMTrainer:
     # ------------------------------------------------------------------------------------------
     def step(self, x0, noise, t, text=None, mask=None, mask_keep=None):
         """One training step on device tensors: x0/noise (B,4,H,W) fp32, t (B,) int64, text (B,S,C) fp32,
-        mask (B,18,MH,MW) fp32 (one-hot), mask_keep (B,) fp32 cond-drop multipliers or None."""
+        mask (B,18,MH,MW) fp32 (one-hot), mask_keep (B,) fp32 cond-drop multipliers or None.
+        With SDMI_MAIN_PRIORITY=1 the step's critical path (forward + data-gradient chain + optimizer) runs on a
+        high-priority stream, so the overlapped weight-gradient stream yields to it under contention."""
+        if self.main_stream is None:
+            return self._step(x0, noise, t, text, mask, mask_keep)
+        caller = torch.cuda.current_stream(self.device)
+        plan.wait_stream(self.main_stream, caller)
+        with torch.cuda.stream(self.main_stream):
+            r = self._step(x0, noise, t, text, mask, mask_keep)
+        plan.wait_stream(caller, self.main_stream)
+        return r
+
+    def _step(self, x0, noise, t, text, mask, mask_keep):
         eng, st = self.engine, self.store
         B, C, H, W = x0.shape
         xt = torch.empty_like(x0)

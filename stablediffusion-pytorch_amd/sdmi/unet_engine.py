@@ -328,6 +328,7 @@ class UNetEngine:
         assert Cx == self.im_channels
         dev = self.device
         G, Hh = L["G"], L["heads"]
+        K.PHASE = "fwd"
         tape = Tape()
         st = dict(B=B, H=H, W=W)
         grads = Grads(dev)
@@ -787,13 +788,21 @@ class UNetEngine:
         stream. `keep` pins the operand tensors until the backward's final join, so the caching
         allocator cannot hand their memory to the current stream while the side stream still reads it.
         The block's completion event is left in self.wg_event."""
+        prev = K.PHASE
+        K.PHASE = "wg"
         if self.side is None:
-            yield
+            try:
+                yield
+            finally:
+                K.PHASE = prev
             return
         self._keep.extend(keep)
         plan.wait_stream(self.side, torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self.side):
-            yield
+        try:
+            with torch.cuda.stream(self.side):
+                yield
+        finally:
+            K.PHASE = prev
         self.wg_event = torch.cuda.Event()
         plan.record_event(self.wg_event, self.side)
 
@@ -816,6 +825,7 @@ class UNetEngine:
         self.temb_grad_all = self._temb_grad_view()
         grads = ctx["grads"]
         tape = ctx["tape"]
+        K.PHASE = "bwd"
         for k in range(len(tape) - 1, -1, -1):
             fn, c = tape[k]
             fn(c, grads)
@@ -824,6 +834,7 @@ class UNetEngine:
         self._join()
         self._keep = []
         self.dpred = None
+        K.PHASE = ""
 
     def _temb_grad_view(self):
         """The t_emb_layers weight gradients are one contiguous [sum C][T] region of the flat store."""
