@@ -37,6 +37,23 @@ PEAK_BF16 = 2.5e15             # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
 
 
+# GEMM mode tag -> kernel symbol (gemm.hip launch_t: DMA mainloop for row-major / conv A, register staging for col-major A)
+DOMINANT_KERNEL = {"gemm_a1b0": "gemm_dma_kernel<1, 0, 2>", "gemm_a0b0": "gemm_dma_kernel<0, 0, 2>",
+                   "gemm_a0b1": "gemm_dma_kernel<0, 1, 2>", "gemm_a2b1": "gemm_kernel<2, 1>",
+                   "gemm_a2b2": "gemm_kernel<2, 2>"}
+PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` (read x2-corrected FETCH_SIZE + WRITE_SIZE) from the committed rocprofv3
+    --pmc passes of this same bench command (scripts/gpu_pmc.sh -> profiles/*_pmc_traffic.json), or None."""
+    try:
+        d = json.load(open(PMC_FILE))[kernel]
+        return d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
+    except (OSError, KeyError, TypeError, ValueError):
+        return None
+
+
 def cond_config():
     from tests.golden.configs import full_cond_config
     return full_cond_config()
@@ -307,10 +324,15 @@ def main():
         tot_fl = sum(v[0] for v in by.values())
         tot_ms = sum(v[1] for v in by.values())
         dom = max(by.items(), key=lambda kv: kv[1][1])
-        roof = {"bound": "mfma", "kernel": "sdmi gemm_kernel (all implicit-GEMM conv + linear launches of one step)",
-                "achieved": tot_fl / (tot_ms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
-                "frac": tot_fl / (tot_ms * 1e-3) / PEAK_BF16, "traffic": None,
-                "launches": sum(v[2] for v in by.values()), "gemm_ms_per_step": tot_ms,
+        dfl, dms, dn = dom[1]
+        traffic = pmc_traffic(DOMINANT_KERNEL.get(dom[0]))
+        roof = {"bound": "mfma", "kernel": f"sdmi {DOMINANT_KERNEL.get(dom[0], dom[0])} ({dom[0]}: implicit-GEMM conv "
+                                           f"fwd/dgrad launches of one step)" if dom[0] == "gemm_a1b0" else dom[0],
+                "achieved": dfl / (dms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
+                "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
+                "launches": dn, "avg_launch_us": dms * 1e3 / dn, "flop_per_launch": dfl / dn,
+                "all_gemm": {"tflops": tot_fl / (tot_ms * 1e-3) / 1e12, "ms_per_step": tot_ms,
+                             "launches": sum(v[2] for v in by.values())},
                 "per_mode": {k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms": v[1], "launches": v[2]}
                              for k, v in by.items()},
                 "dominant_mode": dom[0]}

@@ -1,0 +1,51 @@
+"""Per-kernel average HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
+FETCH_SIZE is doubled (gfx950 tallies 128-B requests of wide streaming reads at 64 B: MI355X_MICROARCH.md HBM).
+Usage: python scripts/pmc_summary.py <fetch_dir> <write_dir> [--json out.json]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    per = collections.defaultdict(list)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name", counter) != counter:
+                continue
+            name = row.get("Kernel_Name") or row.get("Kernel-Name") or "?"
+            per[name].append(float(row["Counter_Value"]))
+    return per
+
+
+def short(name):
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0][:70]
+
+
+def main():
+    fd, wd = sys.argv[1], sys.argv[2]
+    fetch, write = load(fd, "FETCH_SIZE"), load(wd, "WRITE_SIZE")
+    rows = []
+    for k in set(fetch) | set(write):
+        f = fetch.get(k, [])
+        w = write.get(k, [])
+        # FETCH_SIZE / WRITE_SIZE are in KiB (rocprofv3 derived counters)
+        fb = 2 * 1024 * sum(f) / len(f) if f else 0.0
+        wb = 1024 * sum(w) / len(w) if w else 0.0
+        rows.append((short(k), len(f), fb, wb, 2 * 1024 * sum(f) + 1024 * sum(w)))
+    rows.sort(key=lambda r: -r[4])
+    print(f"{'kernel':70s} {'launches':>8s} {'read MB/launch':>14s} {'write MB/launch':>15s}")
+    for name, n, fb, wb, tot in rows[:40]:
+        print(f"{name:70s} {n:8d} {fb / 1e6:14.3f} {wb / 1e6:15.3f}")
+    if "--json" in sys.argv:
+        out = sys.argv[sys.argv.index("--json") + 1]
+        json.dump({r[0]: {"launches": r[1], "read_bytes_per_launch": r[2], "write_bytes_per_launch": r[3]}
+                   for r in rows}, open(out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
