@@ -197,14 +197,14 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m[g], mx * c);
-      const float alpha = exp2f(m[g] - mn);
+      const float alpha = fast_exp2(m[g] - mn);
       m[g] = mn;
       float ls = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          float p = exp2f(fmaf(s[g][kb][i], c, -mn));
+          float p = fast_exp2(fmaf(s[g][kb][i], c, -mn));
           s[g][kb][i] = p;
           ls += p;
         }
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
         const float L = sLD[cur][0][qi], D = sLD[cur][1][qi];
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-          float pv = exp2f(fmaf(p[g][qb][i], c, -L));
+          float pv = fast_exp2(fmaf(p[g][qb][i], c, -L));
           p[g][qb][i] = pv;
           ds[g][qb][i] = pv * (ds[g][qb][i] - D);
         }
@@ -448,8 +448,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const bool kok = !ragged || (k0 + kb * 16 + (lane >> 4) * 4 + i < a.S);
-        float p0 = kok ? exp2f(fmaf(s0[i], c, -lse[0])) : 0.f;
-        float p1 = kok ? exp2f(fmaf(s1[i], c, -lse[1])) : 0.f;
+        float p0 = kok ? fast_exp2(fmaf(s0[i], c, -lse[0])) : 0.f;
+        float p1 = kok ? fast_exp2(fmaf(s1[i], c, -lse[1])) : 0.f;
         ds[0][kb][i] = p0 * (d0[i] - dlt[0]);
         ds[1][kb][i] = p1 * (d1[i] - dlt[1]);
       }

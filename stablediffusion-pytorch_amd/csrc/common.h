@@ -42,11 +42,19 @@ __device__ __forceinline__ float sub_ieee(float a, float b) {
   return a - b;
 }
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// raw v_exp_f32 (2^x): the libm exp2f adds a denormal-range fix-up (compare, 2 selects, add, ldexp) around it,
+// 5 extra VALU ops per element that softmax / sigmoid never need (2^x below 2^-126 contributes nothing)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// raw v_rcp_f32 (1 ulp): replaces the ~10-instruction correctly rounded division where results are rounded to bf16
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ float silu_f(float x) { return x * fast_rcp(1.0f + fast_exp2(-x * kLog2e)); }
 
 // d/dx silu(x) = s(x) * (1 + x * (1 - s(x)))
 __device__ __forceinline__ float silu_grad_f(float x) {
-  float s = 1.0f / (1.0f + __expf(-x));
+  float s = fast_rcp(1.0f + fast_exp2(-x * kLog2e));
   return s * (1.0f + x * (1.0f - s));
 }
 
