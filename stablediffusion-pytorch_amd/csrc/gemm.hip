@@ -47,6 +47,8 @@ struct EpiArgs {
   float alpha; int act;
   int remap, r_ghl, r_gwl, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
   int perm, p_cin, p_taps, p_cvalid;
+  unsigned p_magic;   // ceil(2^32 / p_cin): tap = umulhi(col, p_magic), exact for col < 2^32 / p_cin
+  unsigned n8_magic;  // ceil(2^32 / (N / 8)) for the reducer's row split (0: N / 8 == 1)
   int m_store, n_store;
   int raw;  // 1: write raw fp32 partials (split-K) to ws, epilogue applied by the reducer
   int nsplit;
@@ -93,7 +95,7 @@ struct Epi {
     v = act1(g, v, orow, col);
     long long ocol = col;
     if (g.perm) {
-      int tap = col / g.p_cin;
+      int tap = (int)__umulhi((unsigned)col, g.p_magic);
       int c = col - tap * g.p_cin;
       if (c >= g.p_cvalid) return;
       ocol = g.perm == 2 ? (long long)tap * g.p_cvalid + c : (long long)c * g.p_taps + tap;
@@ -180,7 +182,7 @@ struct Epi {
     v = act1(g, v, orow, col);
     long long ocol = col;
     if (g.perm) {
-      int tap = col / g.p_cin;
+      int tap = (int)__umulhi((unsigned)col, g.p_magic);
       int c = col - tap * g.p_cin;
       if (c >= g.p_cvalid) return;
       ocol = g.perm == 2 ? (long long)tap * g.p_cvalid + c : (long long)c * g.p_taps + tap;
@@ -278,17 +280,41 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
   }
 }
 
+// XCD-aware tile order. Workgroups are dispatched round-robin over the 8 XCDs (dispatch id d runs on XCD d % 8,
+// each XCD has its own 4 MiB L2). The grid is (N tiles, M tiles, splits); re-number it so every XCD owns a
+// CONTIGUOUS band of logical tiles (bijective for any grid size), with N tiles fastest: the N tiles of one
+// 128-row A band -- and, for implicit-GEMM convs, the neighbouring bands whose halo rows it re-reads -- are
+// then fetched into ONE L2 instead of up to eight.
+struct TileId {
+  int m0, n0, z, tile;  // tile = logical (m, n) index within the split slice
+};
+
+__device__ __forceinline__ TileId tile_id() {
+  const int gx = gridDim.x, per = gridDim.x * gridDim.y;
+  const int total = per * gridDim.z;
+  const int d = (blockIdx.z * gridDim.y + blockIdx.y) * gx + blockIdx.x;
+  const int xcd = d & 7, q = total >> 3, r = total & 7;
+  const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (d >> 3);
+  TileId t;
+  t.z = l / per;
+  t.tile = l - t.z * per;
+  const int mt = t.tile / gx;
+  t.m0 = mt * BM;
+  t.n0 = (t.tile - mt * gx) * BN;
+  return t;
+}
+
 // Split-K without a second launch: every split of a tile publishes its slab and bumps the tile's
 // arrival counter; the split that arrives last sums the slabs in fixed z order (deterministic) and
 // applies the epilogue, then re-arms the counter for the next launch (graph replays included).
-__device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0, int n0) {
+__device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0, int n0, int tile) {
   // Slabs were written with device-coherent (sc1) stores, so no L2 write-back fence is needed: wait
   // for this block's stores to complete, then count the arrival with a relaxed device-scope atomic.
   int* flag = (int*)smem;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned* ctr = e.counters + blockIdx.y * gridDim.x + blockIdx.x;
+    unsigned* ctr = e.counters + tile;
     const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == (unsigned)(e.nsplit - 1);
     if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -345,8 +371,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int z = blockIdx.z;
+  const TileId tl = tile_id();
+  const int m0 = tl.m0, n0 = tl.n0;
+  const int z = tl.z;
   const int nkt_total = (g.K + BK - 1) / BK;
   const int kt0 = z * g.ktiles_per_split;
   const int kt1 = min(nkt_total, kt0 + g.ktiles_per_split);
@@ -540,7 +567,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   }
 
   gemm_epilogue(e, acc, smem, m0, n0, wm, wn, lane, z);
-  if (e.raw && e.counters) splitk_tail(e, smem, m0, n0);
+  if (e.raw && e.counters) splitk_tail(e, smem, m0, n0, tl.tile);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -582,8 +609,9 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int z = blockIdx.z;
+  const TileId tl = tile_id();
+  const int m0 = tl.m0, n0 = tl.n0;
+  const int z = tl.z;
   const int nkt_total = (g.K + BK - 1) / BK;
   const int kt0 = z * g.ktiles_per_split;
   const int kt1 = min(nkt_total, kt0 + g.ktiles_per_split);
@@ -655,6 +683,15 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
     }
   }
 
+  // implicit-conv tap state (cin % 64 == 0): the (ty, tx, channel offset) of the next k-tile to issue, advanced
+  // incrementally -- issue() is called for consecutive k-tiles -- instead of two runtime divisions per tile
+  int c_ty = 0, c_tx = 0, c_ci = 0;
+  if (AM == SDMI_A_CONV && cin64 && kt0 * BK < g.k_split) {
+    const int tap = (kt0 * BK) / g.cin;
+    c_ci = kt0 * BK - tap * g.cin;
+    c_ty = tap / g.kw;
+    c_tx = tap - c_ty * g.kw;
+  }
   auto issue = [&](int kt, int stage) __attribute__((always_inline)) {
     char* sa = smem + stage * 2 * TILE_BYTES;
     char* sb = sa + TILE_BYTES;
@@ -677,10 +714,9 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
           off = (a_ok[j] && k < g.K) ? (a_base[j] + (k - g.k_split)) * 2 : OOB;
           dma16(rsA2, dst, off);
         } else if (cin64) {
-          // tap, and with it the (ty, tx) shift, is uniform over the tile: scalar math once per tile
-          const int tap = k0 / g.cin;
-          const int ty = tap / g.kw, tx = tap - ty * g.kw;
-          const int sh = (ty * g.iw + tx) * g.ldx + (k0 - tap * g.cin);
+          // tap, and with it the (ty, tx) shift, is uniform over the tile (tracked incrementally)
+          const int ty = c_ty, tx = c_tx;
+          const int sh = (ty * g.iw + tx) * g.ldx + c_ci;
           int iy = a_iy[j] + ty, ix = a_ix[j] + tx;
           bool ok = a_ok[j] && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
           off = ok ? (a_pix[j] + sh + a_kk[j]) * 2 : OOB;
@@ -693,6 +729,16 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
           bool ok = a_ok[j] && k < g.k_split && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
           off = ok ? (((a_pb[j] + iy) * g.iw + ix) * g.ldx + ci) * 2 : OOB;
           dma16(rsA, dst, off);
+        }
+      }
+    }
+    if (AM == SDMI_A_CONV && cin64 && k0 < g.k_split) {
+      c_ci += BK;
+      if (c_ci >= g.cin) {
+        c_ci = 0;
+        if (++c_tx == g.kw) {
+          c_tx = 0;
+          ++c_ty;
         }
       }
     }
@@ -761,7 +807,7 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
   }
   __syncthreads();
   gemm_epilogue(e, acc, smem, m0, n0, wm, wn, lane, z);
-  if (e.raw && e.counters) splitk_tail(e, smem, m0, n0);
+  if (e.raw && e.counters) splitk_tail(e, smem, m0, n0, tl.tile);
 }
 
 // Sum split-K slabs and apply the epilogue (8 columns per thread on the vector path).
@@ -769,13 +815,17 @@ __global__ void splitk_reduce_kernel(const EpiArgs g) {
   const float* ws = g.ws;
   long long stride = (long long)gridDim.x * blockDim.x;
   if (g.n8) {  // 16-B slab reads; permuted (weight-gradient) outputs store element-wise
-    const int N8 = g.N >> 3;
-    long long total = (long long)g.M * N8;
-    for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
-      int row = (int)(idx / N8), col = (int)(idx - (long long)row * N8) * 8;
+    // 32-bit index math (slabs are < 2^31 bytes) and a multiply-high row split: no 64-bit division per chunk
+    const unsigned N8 = g.N >> 3;
+    const unsigned total = (unsigned)g.M * N8;
+    const int zs = (int)g.split_stride;
+    for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+      const unsigned r = g.n8_magic ? __umulhi(idx, g.n8_magic) : (N8 == 1 ? idx : idx / N8);
+      const int row = (int)r, col = (int)(idx - r * N8) * 8;
       float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const int base = row * g.N + col;
       for (int zz = 0; zz < g.nsplit; ++zz) {
-        const float* p = ws + (long long)zz * g.split_stride + (long long)row * g.N + col;
+        const float* p = ws + zz * zs + base;
         const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
         v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
       }
@@ -877,6 +927,13 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   e.remap = d->remap; e.r_ghl = d->r_gh_log2; e.r_gwl = d->r_gw_log2; e.r_oh = d->r_oh; e.r_ow = d->r_ow;
   e.r_sy = d->r_sy; e.r_sx = d->r_sx; e.r_oy = d->r_oy; e.r_ox = d->r_ox;
   e.perm = d->perm; e.p_cin = d->p_cin; e.p_taps = d->p_taps;
+  if (d->perm && (d->p_cin < 8 || d->p_cin % 8)) return -10;
+  e.p_magic = d->perm ? (unsigned)(((1ULL << 32) + d->p_cin - 1) / d->p_cin) : 0u;
+  {  // multiply-high division by N/8 is exact for idx < 2^32 / (N/8), i.e. when M * (N/8)^2 < 2^32
+    const unsigned long long n8 = (unsigned long long)(d->n >> 3);
+    e.n8_magic = (n8 > 1 && (unsigned long long)d->m * n8 * n8 < (1ULL << 32)) ? (unsigned)(((1ULL << 32) + n8 - 1) / n8)
+                                                                               : 0u;
+  }
   e.p_cvalid = d->p_cvalid > 0 ? d->p_cvalid : d->p_cin;
   e.m_store = d->m_store > 0 ? d->m_store : d->m;
   e.n_store = d->n_store > 0 ? d->n_store : d->n;
