@@ -32,6 +32,17 @@ def main():
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         us = timeit(lambda: K.gemm(M, N, Kd, a, _lib.A_ROWMAJOR, Kd, w, _lib.B_NK, Kd, c, N))
         print(f"plain  M={M:6d} N={N:5d} K={Kd:5d}  {2 * M * N * Kd / us / 1e6:7.1f} TF  {us:8.1f} us", flush=True)
+    for (M, N, Kd, mode) in ((32768, 1152, 384, "nk"), (32768, 384, 384, "nk"), (32768, 384, 1152, "kn"),
+                             (32768, 384, 384, "kn"), (8192, 1536, 512, "nk"), (8192, 512, 1536, "kn")):
+        a = rnd(M, Kd)
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        if mode == "nk":
+            w = rnd(N, Kd)
+            us = timeit(lambda: K.gemm(M, N, Kd, a, _lib.A_ROWMAJOR, Kd, w, _lib.B_NK, Kd, c, N))
+        else:
+            w = rnd(Kd, N)
+            us = timeit(lambda: K.gemm(M, N, Kd, a, _lib.A_ROWMAJOR, Kd, w, _lib.B_KN, N, c, N))
+        print(f"linear {mode} M={M:6d} N={N:5d} K={Kd:5d}  {2 * M * N * Kd / us / 1e6:7.1f} TF  {us:8.1f} us", flush=True)
     for (B, H, C, Co) in ((32, 32, 384, 384), (32, 32, 384, 512), (32, 32, 384, 256), (64, 32, 384, 384)):
         x = rnd(B * H * H, C)
         w = rnd(Co, 9 * C)
