@@ -92,6 +92,9 @@ typedef struct sdmi_gemm_desc {
   /* split-K slices requested by the caller (0 = built-in heuristic); clamped to >= 1 k-tile per slice and to
    * 32-bit slab offsets. Used with the measured per-shape table of sdmi/tuned_gemm.json. */
   int splits_hint;
+  /* column-tile width request (0 = by occupancy: 192 when N % 192 == 0 fills the 512 workgroup slots in fewer
+   * rounds; 128 / 192 = that width where the 192-wide tile applies: B_NK, row-major or implicit-conv A) */
+  int tile_n_hint;
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */

@@ -23,6 +23,7 @@
 //            with P recomputed from the forward's log-sum-exp and delta = rowsum(dO * O).
 #include "common.h"
 #include "../../include/sdmi.h"
+#include <type_traits>
 
 namespace {
 
@@ -125,23 +126,48 @@ __device__ __forceinline__ void store4(bf16_t* dst, const f32x4& v, float s) {
   *(uint2*)dst = w;
 }
 
+// max / sum over the four lanes l, l^16, l^32, l^48 (the four 4-key row groups of one query column):
+// v_permlane16_swap then v_permlane32_swap, no LDS round trip
+__device__ __forceinline__ float xmax4(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r2[0]), __uint_as_float(r2[1]));
+}
+__device__ __forceinline__ float xsum4(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+}
+
+__device__ __forceinline__ f32x2_t lo2(const f32x4& v) { return (f32x2_t){v[0], v[1]}; }
+__device__ __forceinline__ f32x2_t hi2(const f32x4& v) { return (f32x2_t){v[2], v[3]}; }
+
+// DT = ceil(d / 16) output column tiles (compile time: no per-tile branches); DP = contraction width over d
+template <int DT> struct Dim {
+  static constexpr int DP = DT <= 2 ? 32 : 64;
+  static constexpr int KS = DP / 32;
+};
+using Full = std::false_type;
+using Ragged = std::true_type;
+
 // =============================================================================================
 // forward
 // =============================================================================================
-template <int DP>
+template <int DT>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
-  constexpr int DT = DP / 16;
+  constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int dt_n = (a.d + 15) / 16;
   const float c = a.scale * LOG2E;
   const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
   const bf16_t* K = a.k + (long long)b * a.S * a.ldk;
   const bf16_t* V = a.v + (long long)b * a.S * a.ldv;
 
   int myq[2];
-  s16x8 qf[2][DP / 32];
+  s16x8 qf[2][KS];
   float m[2], l[2];
   f32x4 o[2][DT];
 #pragma unroll
@@ -161,7 +187,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   tile_store<DP>(smem + Tile<DP>::ELEMS, rv);
   __syncthreads();
   int cur = 0;
-  for (int k0 = 0; k0 < a.S; k0 += TILE) {
+  auto step = [&](int k0, auto rag) __attribute__((always_inline)) {
     const bool more = k0 + TILE < a.S;
     if (more) {
       tile_fetch<DP>(rk, K, a.ldk, k0 + TILE, a.S, h * a.d, a.d);
@@ -174,41 +200,44 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
     for (int kb = 0; kb < 4; ++kb) {
       s[0][kb] = s[1][kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < DP / 32; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         s16x8 kf = frag_rows<DP>(sK, kb * 16, ks * 32, lane);
         s[0][kb] = mfma(kf, qf[0][ks], s[0][kb]);
         s[1][kb] = mfma(kf, qf[1][ks], s[1][kb]);
       }
     }
-    if (k0 + TILE > a.S) {  // ragged last tile (cross-attention S = 77): mask keys >= S
+    if constexpr (decltype(rag)::value) {  // last key tile of a ragged S (cross-attention S = 77): keys >= S out
+      const int lim = a.S - k0 - (lane >> 4) * 4;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (k0 + kb * 16 + (lane >> 4) * 4 + i >= a.S) s[0][kb][i] = s[1][kb][i] = -INFINITY;
+          if (kb * 16 + i >= lim) s[0][kb][i] = s[1][kb][i] = -INFINITY;
     }
     s16x8 pf[2][2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      float mx = -INFINITY;
+      float mx = fmaxf(fmaxf(s[g][0][0], s[g][0][1]), s[g][0][2]);
+      mx = fmaxf(fmaxf(mx, s[g][0][3]), s[g][1][0]);
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-        mx = fmaxf(mx, fmaxf(fmaxf(s[g][kb][0], s[g][kb][1]), fmaxf(s[g][kb][2], s[g][kb][3])));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      for (int j = 5; j < 16; j += 2) mx = fmaxf(fmaxf(mx, s[g][j >> 2][j & 3]), s[g][(j + 1) >> 2][(j + 1) & 3]);
+      mx = xmax4(mx);
       const float mn = fmaxf(m[g], mx * c);
       const float alpha = fast_exp2(m[g] - mn);
       m[g] = mn;
-      float ls = 0.f;
+      const f32x2_t cc = {c, c}, nm = {-mn, -mn};
+      f32x2_t ls = {0.f, 0.f};
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float p = fast_exp2(fmaf(s[g][kb][i], c, -mn));
-          s[g][kb][i] = p;
-          ls += p;
-        }
-      l[g] = fmaf(l[g], alpha, ls);
+      for (int kb = 0; kb < 4; ++kb) {
+        f32x2_t x0 = __builtin_elementwise_fma(lo2(s[g][kb]), cc, nm);
+        f32x2_t x1 = __builtin_elementwise_fma(hi2(s[g][kb]), cc, nm);
+        x0 = (f32x2_t){fast_exp2(x0[0]), fast_exp2(x0[1])};
+        x1 = (f32x2_t){fast_exp2(x1[0]), fast_exp2(x1[1])};
+        ls += x0;
+        ls += x1;
+        s[g][kb] = (f32x4){x0[0], x0[1], x1[0], x1[1]};
+      }
+      l[g] = fmaf(l[g], alpha, ls[0] + ls[1]);
 #pragma unroll
       for (int t = 0; t < DT; ++t) o[g][t] *= alpha;
       pf[g][0] = pack_acc(s[g][0], s[g][1]);
@@ -217,12 +246,11 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int t = 0; t < DT; ++t)
-        if (t < dt_n) {
-          s16x8 vf = frag_tr<DP>(sV, 32 * s2, 16 * t, lane);
-          o[0][t] = mfma(vf, pf[0][s2], o[0][t]);
-          o[1][t] = mfma(vf, pf[1][s2], o[1][t]);
-        }
+      for (int t = 0; t < DT; ++t) {
+        s16x8 vf = frag_tr<DP>(sV, 32 * s2, 16 * t, lane);
+        o[0][t] = mfma(vf, pf[0][s2], o[0][t]);
+        o[1][t] = mfma(vf, pf[1][s2], o[1][t]);
+      }
     if (more) {
       bf16_t* nK = smem + (cur ^ 1) * 2 * Tile<DP>::ELEMS;
       tile_store<DP>(nK, rk);
@@ -230,19 +258,20 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
     }
     __syncthreads();
     cur ^= 1;
-  }
+  };
+  int k0 = 0;
+  for (; k0 + TILE <= a.S; k0 += TILE) step(k0, Full{});
+  if (k0 < a.S) step(k0, Ragged{});
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    float lt = l[g];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = xsum4(l[g]);
     if (myq[g] < a.N) {
       const float inv = 1.f / lt;
       bf16_t* O = a.out + ((long long)b * a.N + myq[g]) * a.ldo + h * a.d;
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         int d0 = 16 * t + (lane >> 4) * 4;
-        if (t < dt_n && d0 < a.d) store4(O + d0, o[g][t], inv);
+        if (d0 < a.d) store4(O + d0, o[g][t], inv);
       }
       if ((lane >> 4) == 0) a.lse[(long long)bh * a.N + myq[g]] = m[g] + __log2f(lt);
     }
@@ -274,20 +303,19 @@ __global__ void attn_delta_kernel(AttnArgs a) {
 // =============================================================================================
 // backward: dK, dV (keys on lanes, 128 keys per workgroup, query tiles streamed)
 // =============================================================================================
-template <int DP>
+template <int DT>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
-  constexpr int DT = DP / 16;
+  constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][Q|dO]
-  __shared__ float sLD[2][2][64];                                            // [buf][lse|delta]
+  __shared__ __attribute__((aligned(16))) float sLD[2][2][64];               // [buf][-lse|-delta]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int dt_n = (a.d + 15) / 16;
   const float c = a.scale * LOG2E;
   const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
   const bf16_t* dO = a.dout + (long long)b * a.N * a.lddo;
 
   int mykey[2];
-  s16x8 kf[2][DP / 32], vf[2][DP / 32];
+  s16x8 kf[2][KS], vf[2][KS];
   f32x4 dk[2][DT], dv[2][DT];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
@@ -305,8 +333,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
     tile_fetch<DP>(ro, dO, a.lddo, q0, a.N, h * a.d, a.d);
     if (threadIdx.x < 64) {
       int q = q0 + threadIdx.x;
-      rl = q < a.N ? a.lse[(long long)bh * a.N + q] : INFINITY;  // invalid rows: p = 0
-      rd = q < a.N ? a.delta[(long long)bh * a.N + q] : 0.f;
+      rl = q < a.N ? -a.lse[(long long)bh * a.N + q] : -INFINITY;  // invalid rows: p = 0
+      rd = q < a.N ? -a.delta[(long long)bh * a.N + q] : 0.f;
     }
   };
   auto put = [&](int buf) __attribute__((always_inline)) {
@@ -321,6 +349,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   put(0);
   __syncthreads();
   int cur = 0;
+  const f32x2_t cc = {c, c};
   for (int q0 = 0; q0 < a.N; q0 += TILE) {
     const bool more = q0 + TILE < a.N;
     if (more) fetch(q0 + TILE);
@@ -331,7 +360,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
     for (int qb = 0; qb < 4; ++qb) {
       p[0][qb] = p[1][qb] = ds[0][qb] = ds[1][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < DP / 32; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         s16x8 qa = frag_rows<DP>(sQ, qb * 16, ks * 32, lane);
         s16x8 oa = frag_rows<DP>(sO, qb * 16, ks * 32, lane);
         p[0][qb] = mfma(qa, kf[0][ks], p[0][qb]);
@@ -339,16 +368,17 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
         ds[0][qb] = mfma(oa, vf[0][ks], ds[0][qb]);
         ds[1][qb] = mfma(oa, vf[1][ks], ds[1][qb]);
       }
+      const int qi = qb * 16 + (lane >> 4) * 4;
+      const f32x4 nL = *(const f32x4*)&sLD[cur][0][qi], nD = *(const f32x4*)&sLD[cur][1][qi];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int qi = qb * 16 + (lane >> 4) * 4 + i;
-        const float L = sLD[cur][0][qi], D = sLD[cur][1][qi];
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          float pv = fast_exp2(fmaf(p[g][qb][i], c, -L));
-          p[g][qb][i] = pv;
-          ds[g][qb][i] = pv * (ds[g][qb][i] - D);
-        }
+      for (int g = 0; g < 2; ++g) {
+        f32x2_t p0 = __builtin_elementwise_fma(lo2(p[g][qb]), cc, lo2(nL));
+        f32x2_t p1 = __builtin_elementwise_fma(hi2(p[g][qb]), cc, hi2(nL));
+        p0 = (f32x2_t){fast_exp2(p0[0]), fast_exp2(p0[1])};
+        p1 = (f32x2_t){fast_exp2(p1[0]), fast_exp2(p1[1])};
+        const f32x2_t d0 = p0 * (lo2(ds[g][qb]) + lo2(nD)), d1 = p1 * (hi2(ds[g][qb]) + hi2(nD));
+        p[g][qb] = (f32x4){p0[0], p0[1], p1[0], p1[1]};
+        ds[g][qb] = (f32x4){d0[0], d0[1], d1[0], d1[1]};
       }
     }
 #pragma unroll
@@ -356,15 +386,14 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
       s16x8 pf0 = pack_acc(p[0][2 * s2], p[0][2 * s2 + 1]), pf1 = pack_acc(p[1][2 * s2], p[1][2 * s2 + 1]);
       s16x8 df0 = pack_acc(ds[0][2 * s2], ds[0][2 * s2 + 1]), df1 = pack_acc(ds[1][2 * s2], ds[1][2 * s2 + 1]);
 #pragma unroll
-      for (int t = 0; t < DT; ++t)
-        if (t < dt_n) {
-          s16x8 ot = frag_tr<DP>(sO, 32 * s2, 16 * t, lane);
-          dv[0][t] = mfma(ot, pf0, dv[0][t]);
-          dv[1][t] = mfma(ot, pf1, dv[1][t]);
-          s16x8 qt = frag_tr<DP>(sQ, 32 * s2, 16 * t, lane);
-          dk[0][t] = mfma(qt, df0, dk[0][t]);
-          dk[1][t] = mfma(qt, df1, dk[1][t]);
-        }
+      for (int t = 0; t < DT; ++t) {
+        s16x8 ot = frag_tr<DP>(sO, 32 * s2, 16 * t, lane);
+        dv[0][t] = mfma(ot, pf0, dv[0][t]);
+        dv[1][t] = mfma(ot, pf1, dv[1][t]);
+        s16x8 qt = frag_tr<DP>(sQ, 32 * s2, 16 * t, lane);
+        dk[0][t] = mfma(qt, df0, dk[0][t]);
+        dk[1][t] = mfma(qt, df1, dk[1][t]);
+      }
     }
     if (more) put(cur ^ 1);
     __syncthreads();
@@ -378,7 +407,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         int d0 = 16 * t + (lane >> 4) * 4;
-        if (t < dt_n && d0 < a.d) {
+        if (d0 < a.d) {
           store4(DK + d0, dk[g][t], a.scale);
           store4(DV + d0, dv[g][t], 1.f);
         }
@@ -389,20 +418,19 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
 // =============================================================================================
 // backward: dQ (queries on lanes, 128 queries per workgroup, key tiles streamed)
 // =============================================================================================
-template <int DP>
+template <int DT>
 __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
-  constexpr int DT = DP / 16;
+  constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int dt_n = (a.d + 15) / 16;
   const float c = a.scale * LOG2E;
   const bf16_t* K = a.k + (long long)b * a.S * a.ldk;
   const bf16_t* V = a.v + (long long)b * a.S * a.ldv;
 
   int myq[2];
-  s16x8 qf[2][DP / 32], of[2][DP / 32];
-  float lse[2], dlt[2];
+  s16x8 qf[2][KS], of[2][KS];
+  f32x2_t nlse[2], ndlt[2];
   f32x4 dq[2][DT];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
@@ -410,8 +438,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     row_frags<DP>(qf[g], a.q + (long long)b * a.N * a.ldq, a.ldq, myq[g], a.N, h * a.d, a.d, lane);
     row_frags<DP>(of[g], a.dout + (long long)b * a.N * a.lddo, a.lddo, myq[g], a.N, h * a.d, a.d, lane);
     const bool ok = myq[g] < a.N;
-    lse[g] = ok ? a.lse[(long long)bh * a.N + myq[g]] : INFINITY;
-    dlt[g] = ok ? a.delta[(long long)bh * a.N + myq[g]] : 0.f;
+    const float L = ok ? -a.lse[(long long)bh * a.N + myq[g]] : -INFINITY;
+    const float D = ok ? -a.delta[(long long)bh * a.N + myq[g]] : 0.f;
+    nlse[g] = (f32x2_t){L, L};
+    ndlt[g] = (f32x2_t){D, D};
 #pragma unroll
     for (int t = 0; t < DT; ++t) dq[g][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
@@ -423,7 +453,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   tile_store<DP>(smem + Tile<DP>::ELEMS, rv);
   __syncthreads();
   int cur = 0;
-  for (int k0 = 0; k0 < a.S; k0 += TILE) {
+  const f32x2_t cc = {c, c};
+  auto step = [&](int k0, auto rag) __attribute__((always_inline)) {
     const bool more = k0 + TILE < a.S;
     if (more) {
       tile_fetch<DP>(rk, K, a.ldk, k0 + TILE, a.S, h * a.d, a.d);
@@ -431,39 +462,46 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     }
     const bf16_t* sK = smem + cur * 2 * Tile<DP>::ELEMS;
     const bf16_t* sV = sK + Tile<DP>::ELEMS;
-    const bool ragged = k0 + TILE > a.S;
     f32x4 ds[2][4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      f32x4 s0 = (f32x4){0.f, 0.f, 0.f, 0.f}, s1 = s0, d0 = s0, d1 = s0;
+      f32x4 sc[2], dp[2];
+      sc[0] = sc[1] = dp[0] = dp[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < DP / 32; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         s16x8 ka = frag_rows<DP>(sK, kb * 16, ks * 32, lane);
         s16x8 va = frag_rows<DP>(sV, kb * 16, ks * 32, lane);
-        s0 = mfma(ka, qf[0][ks], s0);
-        s1 = mfma(ka, qf[1][ks], s1);
-        d0 = mfma(va, of[0][ks], d0);
-        d1 = mfma(va, of[1][ks], d1);
+        sc[0] = mfma(ka, qf[0][ks], sc[0]);
+        sc[1] = mfma(ka, qf[1][ks], sc[1]);
+        dp[0] = mfma(va, of[0][ks], dp[0]);
+        dp[1] = mfma(va, of[1][ks], dp[1]);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool kok = !ragged || (k0 + kb * 16 + (lane >> 4) * 4 + i < a.S);
-        float p0 = kok ? fast_exp2(fmaf(s0[i], c, -lse[0])) : 0.f;
-        float p1 = kok ? fast_exp2(fmaf(s1[i], c, -lse[1])) : 0.f;
-        ds[0][kb][i] = p0 * (d0[i] - dlt[0]);
-        ds[1][kb][i] = p1 * (d1[i] - dlt[1]);
+      for (int g = 0; g < 2; ++g) {
+        f32x2_t p0 = __builtin_elementwise_fma(lo2(sc[g]), cc, nlse[g]);
+        f32x2_t p1 = __builtin_elementwise_fma(hi2(sc[g]), cc, nlse[g]);
+        p0 = (f32x2_t){fast_exp2(p0[0]), fast_exp2(p0[1])};
+        p1 = (f32x2_t){fast_exp2(p1[0]), fast_exp2(p1[1])};
+        if constexpr (decltype(rag)::value) {  // keys >= S of the last ragged tile contribute nothing
+          const int lim = a.S - k0 - kb * 16 - (lane >> 4) * 4;
+          if (0 >= lim) p0[0] = 0.f;
+          if (1 >= lim) p0[1] = 0.f;
+          if (2 >= lim) p1[0] = 0.f;
+          if (3 >= lim) p1[1] = 0.f;
+        }
+        const f32x2_t d0 = p0 * (lo2(dp[g]) + ndlt[g]), d1 = p1 * (hi2(dp[g]) + ndlt[g]);
+        ds[g][kb] = (f32x4){d0[0], d0[1], d1[0], d1[1]};
       }
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       s16x8 df0 = pack_acc(ds[0][2 * s2], ds[0][2 * s2 + 1]), df1 = pack_acc(ds[1][2 * s2], ds[1][2 * s2 + 1]);
 #pragma unroll
-      for (int t = 0; t < DT; ++t)
-        if (t < dt_n) {
-          s16x8 kt = frag_tr<DP>(sK, 32 * s2, 16 * t, lane);
-          dq[0][t] = mfma(kt, df0, dq[0][t]);
-          dq[1][t] = mfma(kt, df1, dq[1][t]);
-        }
+      for (int t = 0; t < DT; ++t) {
+        s16x8 kt = frag_tr<DP>(sK, 32 * s2, 16 * t, lane);
+        dq[0][t] = mfma(kt, df0, dq[0][t]);
+        dq[1][t] = mfma(kt, df1, dq[1][t]);
+      }
     }
     if (more) {
       bf16_t* nK = smem + (cur ^ 1) * 2 * Tile<DP>::ELEMS;
@@ -472,7 +510,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     }
     __syncthreads();
     cur ^= 1;
-  }
+  };
+  int k0 = 0;
+  for (; k0 + TILE <= a.S; k0 += TILE) step(k0, Full{});
+  if (k0 < a.S) step(k0, Ragged{});
 #pragma unroll
   for (int g = 0; g < 2; ++g)
     if (myq[g] < a.N) {
@@ -480,7 +521,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         int d0 = 16 * t + (lane >> 4) * 4;
-        if (t < dt_n && d0 < a.d) store4(DQ + d0, dq[g][t], a.scale);
+        if (d0 < a.d) store4(DQ + d0, dq[g][t], a.scale);
       }
     }
 }
@@ -503,8 +544,12 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
   if (rc) return rc;
   dim3 grid((N + ROWS - 1) / ROWS, B * H);
   hipStream_t s = (hipStream_t)stream;
-  if (d <= 32) hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(NT), 0, s, a);
+  switch ((d + 15) / 16) {
+    case 1: hipLaunchKernelGGL(attn_fwd_kernel<1>, grid, dim3(NT), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(NT), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(attn_fwd_kernel<3>, grid, dim3(NT), 0, s, a); break;
+    default: hipLaunchKernelGGL(attn_fwd_kernel<4>, grid, dim3(NT), 0, s, a); break;
+  }
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -526,12 +571,17 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, a);
   SDMI_CHECK_LAUNCH();
   dim3 gk((S + ROWS - 1) / ROWS, B * H), gq((N + ROWS - 1) / ROWS, B * H);
-  if (d <= 32) {
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, gk, dim3(NT), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, gq, dim3(NT), 0, s, a);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, gk, dim3(NT), 0, s, a);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, gq, dim3(NT), 0, s, a);
+  switch ((d + 15) / 16) {
+#define SDMI_ATTN_BWD(DT)                                            \
+  case DT:                                                           \
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<DT>, gk, dim3(NT), 0, s, a); \
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<DT>, gq, dim3(NT), 0, s, a);  \
+    break;
+    SDMI_ATTN_BWD(1)
+    SDMI_ATTN_BWD(2)
+    SDMI_ATTN_BWD(3)
+    default: SDMI_ATTN_BWD(4)
+#undef SDMI_ATTN_BWD
   }
   SDMI_CHECK_LAUNCH();
   return 0;

@@ -194,19 +194,21 @@ struct Epi {
 
 // Shared epilogue of the GEMM kernels: acc = this wave's 64x64 sub-tile (4x4 MFMA tiles), smem >= 34 KB
 // of LDS that no wave reads any more (the caller synchronises before).
-__device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][4], char* smem, int m0, int n0,
+template <int TBN = BN>
+__device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][TBN / 32], char* smem, int m0, int n0,
                                               int wm, int wn, int lane, int z) {
+  constexpr int NJ = TBN / 32;  // 16-column MFMA tiles per wave
   // ---------------- epilogue ----------------
   if (e.vec || (e.raw && e.n8)) {
     // Stage the fp32 tile through LDS in two 64-row halves and write whole rows with 16-B stores
     // (8 bf16 or 4 fp32 per lane) instead of 64 scattered 2-byte stores per lane.
-    float* st = (float*)smem;  // [64][SROW] fp32, 33 KB
-    constexpr int SROW = 132;  // +4 floats: lanes of one ds_write hit distinct banks
+    float* st = (float*)smem;  // [64][SROW] fp32, 33 KB (TBN 128) / 49 KB (TBN 192)
+    constexpr int SROW = TBN + 4;  // +4 floats: lanes of one ds_write hit distinct banks
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       if (wm == half * 64) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           const int cl = wn + 16 * j + (lane & 15);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -216,9 +218,9 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
       }
       __syncthreads();
 #pragma unroll
-      for (int it = 0; it < 4; ++it) {  // 64 rows x 16 chunks of 8 columns
+      for (int it = 0; it < TBN / 32; ++it) {  // 64 rows x TBN/8 chunks of 8 columns
         const int ch = threadIdx.x + it * NT;
-        const int rl = ch >> 4, c8 = (ch & 15) * 8;
+        const int rl = ch / (TBN / 8), c8 = (ch - rl * (TBN / 8)) * 8;
         const int row = m0 + half * 64 + rl, col = n0 + c8;
         float v[8];
         const float4 lo = *(const float4*)(st + rl * SROW + c8), hi = *(const float4*)(st + rl * SROW + c8 + 4);
@@ -243,7 +245,7 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
     const long long zoff = (long long)z * e.split_stride;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int col = n0 + wn + 16 * j + (lane & 15);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -259,7 +261,7 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int col = n0 + wn + 16 * j + (lane & 15);
       const bool cok = col < e.n_store;
       float bsum = 0.f;
@@ -289,6 +291,7 @@ struct TileId {
   int m0, n0, z, tile;  // tile = logical (m, n) index within the split slice
 };
 
+template <int TBN = BN>
 __device__ __forceinline__ TileId tile_id() {
   const int gx = gridDim.x, per = gridDim.x * gridDim.y;
   const int total = per * gridDim.z;
@@ -300,13 +303,14 @@ __device__ __forceinline__ TileId tile_id() {
   t.tile = l - t.z * per;
   const int mt = t.tile / gx;
   t.m0 = mt * BM;
-  t.n0 = (t.tile - mt * gx) * BN;
+  t.n0 = (t.tile - mt * gx) * TBN;
   return t;
 }
 
 // Split-K without a second launch: every split of a tile publishes its slab and bumps the tile's
 // arrival counter; the split that arrives last sums the slabs in fixed z order (deterministic) and
 // applies the epilogue, then re-arms the counter for the next launch (graph replays included).
+template <int TBN = BN>
 __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0, int n0, int tile) {
   // Slabs were written with device-coherent (sc1) stores, so no L2 write-back fence is needed: wait
   // for this block's stores to complete, then count the arrival with a relaxed device-scope atomic.
@@ -327,8 +331,9 @@ __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0
   if (e.n8) {
     // 2048 chunks of 8 columns, 8 per thread; 4 splits (8 loads) in flight per thread
 #pragma unroll 1
-    for (int ch = threadIdx.x; ch < BM * (BN / 8); ch += NT) {
-      const int row = m0 + (ch >> 4), col = n0 + (ch & 15) * 8;
+    for (int ch = threadIdx.x; ch < BM * (TBN / 8); ch += NT) {
+      const int rl = ch / (TBN / 8);
+      const int row = m0 + rl, col = n0 + (ch - rl * (TBN / 8)) * 8;
       if (e.vec ? (row >= e.m_store || col >= e.n_store) : (row >= e.M || col >= e.N)) continue;
       float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       const int off = (row * e.N + col) * 4;
@@ -349,8 +354,8 @@ __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0
     return;
   }
 #pragma unroll 1
-  for (int idx = threadIdx.x; idx < BM * BN; idx += NT) {
-    const int row = m0 + idx / BN, col = n0 + idx % BN;
+  for (int idx = threadIdx.x; idx < BM * TBN; idx += NT) {
+    const int row = m0 + idx / TBN, col = n0 + idx % TBN;
     if (row >= e.M || col >= e.N) continue;
     float acc = 0.f;
     int off = (row * e.N + col) * 4;
@@ -602,14 +607,20 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (SDMI_LDS void*)lds_wave_base, 16, off, 0, 0, 0);
 }
 
-template <int AM, int BMODE, int STAGES>
+// TBN = 192 (B_NK only): 128 x 192 tiles, each wave 64 x 96 -- 2 x 80 KiB of LDS still fits two workgroups per CU,
+// and N = 384 outputs split into 2 (not 3) column tiles, so a 32768 x 384 conv is exactly 512 tiles = one round
+template <int AM, int BMODE, int STAGES, int TBN = BN>
 __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(const Args g, const EpiArgs e) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // STAGES x (A 16 KiB | B 16 KiB)
+  static_assert(TBN == BN || (TBN == 192 && BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR), "192-column tiles: B_NK");
+  constexpr int NJ = TBN / 32;                       // 16-column MFMA tiles per wave
+  constexpr int B_BYTES = TBN * BK * 2;              // B tile bytes
+  constexpr int STAGE_BYTES = TILE_BYTES + B_BYTES;  // A | B
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // STAGES x (A 16 KiB | B 16 / 24 KiB)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const TileId tl = tile_id();
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (TBN / 2);
+  const TileId tl = tile_id<TBN>();
   const int m0 = tl.m0, n0 = tl.n0;
   const int z = tl.z;
   const int nkt_total = (g.K + BK - 1) / BK;
@@ -625,11 +636,11 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
   // ---- per-lane, per-instruction (j = 0..3) coordinates, fixed over the K loop ----
   // K-contiguous image: instruction j of wave w fills rows (w*4+j)*8 .. +8, lane -> row +lane>>3, slot lane&7
   // MN-contiguous image: fills k-rows (w*4+j)*4 .. +4, lane -> k-row +lane>>4, slot lane&15
-  int a_base[4], b_base[4];   // element offsets (without the k / pixel part)
-  int a_kk[4], b_kk[4];       // k offset inside the tile (KC: chunk*8) or k-row (MN)
-  bool a_ok[4], b_ok[4];
+  int a_base[4], b_base[NJ];   // element offsets (without the k / pixel part)
+  int a_kk[4], b_kk[NJ];       // k offset inside the tile (KC: chunk*8) or k-row (MN)
+  bool a_ok[4], b_ok[NJ];
   int a_iy[4], a_ix[4], a_pb[4], a_pix[4];
-  int b_ty[4], b_tx[4];
+  int b_ty[NJ], b_tx[NJ];
   const bool cin64 = AM == SDMI_A_CONV && (g.cin & 63) == 0;  // k tile lies inside one tap
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -659,8 +670,11 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
         a_pix[j] = ((a_pb[j] + a_iy[j]) * g.iw + a_ix[j]) * g.ldx;
       }
     }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
     if (BMODE == SDMI_B_NK) {
-      int r = (wave * 4 + j) * 8 + (lane >> 3);
+      int r = (wave * NJ + j) * 8 + (lane >> 3);
       int c = (lane & 7) ^ (r & 7);
       int n = n0 + r;
       b_ok[j] = n < g.N;
@@ -693,7 +707,7 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
     c_tx = tap - c_ty * g.kw;
   }
   auto issue = [&](int kt, int stage) __attribute__((always_inline)) {
-    char* sa = smem + stage * 2 * TILE_BYTES;
+    char* sa = smem + stage * STAGE_BYTES;
     char* sb = sa + TILE_BYTES;
     const int k0 = kt * BK;
 #pragma unroll
@@ -743,8 +757,8 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      char* dst = sb + (wave * 4 + j) * 1024;
+    for (int j = 0; j < NJ; ++j) {
+      char* dst = sb + (wave * NJ + j) * 1024;
       int off;
       if (BMODE == SDMI_B_NK) {
         int k = k0 + b_kk[j];
@@ -765,11 +779,11 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nt = kt1 - kt0;
   if (nt > 0) {
@@ -778,57 +792,85 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
     for (int s = 0; s < STAGES - 1; ++s)
       if (s < nt) issue(kt0 + s, s);
     for (int t = 0; t < nt; ++t) {
-      // tile t landed for this thread: at most (tiles issued after t) x 8 DMA instructions outstanding
+      // tile t landed for this thread: at most (tiles issued after t) x (4 + NJ) DMA instructions outstanding
       const int after = min(STAGES - 2, nt - 1 - t);
-      if (after >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if (after >= 1) {
+        if constexpr (NJ == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      }
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMA for tile t done; every wave done with tile t-1
       if (t + STAGES - 1 < nt) issue(kt0 + t + STAGES - 1, (t + STAGES - 1) % STAGES);
-      const char* ta = smem + (t % STAGES) * 2 * TILE_BYTES;
+      const char* ta = smem + (t % STAGES) * STAGE_BYTES;
       const char* tb = ta + TILE_BYTES;
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        s16x8 fa[4], fb[4];
+        s16x8 fa[4], fb[NJ];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           fa[i] = (AM == SDMI_A_COLMAJOR) ? frag_tr(ta, wm + 16 * i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           fb[j] = (BMODE == SDMI_B_NK) ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_tr(tb, wn + 16 * j, ks, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < NJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
       }
       __builtin_amdgcn_s_setprio(0);
     }
   }
   __syncthreads();
-  gemm_epilogue(e, acc, smem, m0, n0, wm, wn, lane, z);
-  if (e.raw && e.counters) splitk_tail(e, smem, m0, n0, tl.tile);
+  gemm_epilogue<TBN>(e, acc, smem, m0, n0, wm, wn, lane, z);
+  if (e.raw && e.counters) splitk_tail<TBN>(e, smem, m0, n0, tl.tile);
 }
 
-// Sum split-K slabs and apply the epilogue (8 columns per thread on the vector path).
-__global__ void splitk_reduce_kernel(const EpiArgs g) {
+// Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
+// 8-column items; its SL slab lanes sum disjoint slab subsets (a wave reads 64 consecutive items of ONE slab:
+// contiguous 2 KiB) and are merged in LDS in a fixed order, so the result is deterministic. SL > 1 spreads the
+// deep split-K of small weight gradients (a 128 x 128 dW = 2048 items) over enough workgroups to fill the chip.
+template <int SL>
+__global__ __launch_bounds__(256) void splitk_reduce_n8_kernel(const EpiArgs g) {
+  constexpr int IPB = 256 / SL;
+  __shared__ float4 part[SL > 1 ? SL : 1][IPB][2];
   const float* ws = g.ws;
-  long long stride = (long long)gridDim.x * blockDim.x;
-  if (g.n8) {  // 16-B slab reads; permuted (weight-gradient) outputs store element-wise
+  const unsigned N8 = g.N >> 3;
+  const unsigned total = (unsigned)g.M * N8;
+  const int zs = (int)g.split_stride;
+  const int li = threadIdx.x % IPB, sl = threadIdx.x / IPB;
+  for (unsigned i0 = blockIdx.x * IPB; i0 < total; i0 += gridDim.x * IPB) {  // uniform trip count per block
+    const unsigned idx = i0 + li;
     // 32-bit index math (slabs are < 2^31 bytes) and a multiply-high row split: no 64-bit division per chunk
-    const unsigned N8 = g.N >> 3;
-    const unsigned total = (unsigned)g.M * N8;
-    const int zs = (int)g.split_stride;
-    for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-      const unsigned r = g.n8_magic ? __umulhi(idx, g.n8_magic) : (N8 == 1 ? idx : idx / N8);
-      const int row = (int)r, col = (int)(idx - r * N8) * 8;
-      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const int base = row * g.N + col;
-      for (int zz = 0; zz < g.nsplit; ++zz) {
+    const unsigned r = g.n8_magic ? __umulhi(idx, g.n8_magic) : (N8 == 1 ? idx : idx / N8);
+    const int row = (int)r, col = (int)(idx - r * N8) * 8;
+    const int base = row * g.N + col;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (idx < total) {
+      for (int zz = sl; zz < g.nsplit; zz += SL) {
         const float* p = ws + zz * zs + base;
-        const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
-        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+        const float4 x = *(const float4*)p, y = *(const float4*)(p + 4);
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+        b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
       }
+    }
+    if constexpr (SL > 1) {
+      part[sl][li][0] = a;
+      part[sl][li][1] = b;
+      __syncthreads();
+      if (sl == 0) {
+#pragma unroll
+        for (int q = 1; q < SL; ++q) {
+          const float4 x = part[q][li][0], y = part[q][li][1];
+          a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+          b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+        }
+      }
+      __syncthreads();
+    }
+    if (sl == 0 && idx < total) {
+      float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       if (g.vec) {
         if (row < g.m_store && col < g.n_store) Epi::finish8(g, row, col, v);
       } else {
@@ -836,8 +878,13 @@ __global__ void splitk_reduce_kernel(const EpiArgs g) {
         for (int e = 0; e < 8; ++e) Epi::store_final(g, row, col + e, v[e]);
       }
     }
-    return;
   }
+}
+
+// Sum split-K slabs and apply the epilogue, general N (one element per thread).
+__global__ void splitk_reduce_kernel(const EpiArgs g) {
+  const float* ws = g.ws;
+  long long stride = (long long)gridDim.x * blockDim.x;
   long long total = (long long)g.M * g.N;
   for (long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += stride) {
     float s = 0.f;
@@ -845,6 +892,28 @@ __global__ void splitk_reduce_kernel(const EpiArgs g) {
     int row = (int)(idx / g.N), col = (int)(idx - (long long)row * g.N);
     Epi::store(g, row, col, s, 0);
   }
+}
+
+hipError_t launch_reduce(const EpiArgs& red, hipStream_t s) {
+  if (!red.n8) {
+    const long long total = (long long)red.M * red.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096)), dim3(256),
+                       0, s, red);
+    return hipGetLastError();
+  }
+  const long long items = (long long)red.M * (red.N / 8);
+  int sl = 1;  // slab lanes: aim for >= 1024 workgroups
+  while (sl < 32 && sl * 2 <= red.nsplit && items * sl / 256 < 1024) sl *= 2;
+  const unsigned blocks = (unsigned)std::min<long long>((items * sl + 255) / 256, 8192);
+  switch (sl) {
+    case 1: hipLaunchKernelGGL(splitk_reduce_n8_kernel<1>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 2: hipLaunchKernelGGL(splitk_reduce_n8_kernel<2>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 4: hipLaunchKernelGGL(splitk_reduce_n8_kernel<4>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 8: hipLaunchKernelGGL(splitk_reduce_n8_kernel<8>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 16: hipLaunchKernelGGL(splitk_reduce_n8_kernel<16>, dim3(blocks), dim3(256), 0, s, red); break;
+    default: hipLaunchKernelGGL(splitk_reduce_n8_kernel<32>, dim3(blocks), dim3(256), 0, s, red); break;
+  }
+  return hipGetLastError();
 }
 
 // Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged, 2 / 3 LDS-DMA ring
@@ -860,18 +929,43 @@ int gemm_variant() {
   return v;
 }
 
-template <int AM, int BMODE>
-hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
+int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0) v = AM == SDMI_A_COLMAJOR ? 0 : 2;
+  if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
   // the DMA path needs a tile-uniform second source (k_split % BK == 0)
-  const bool dma_ok = AM != SDMI_A_CONV || !a.A2 || a.k_split % BK == 0;
-  if (v == 0 || !dma_ok) {
+  if (d->a_mode == SDMI_A_CONV && d->a2 && d->k_split % BK) v = 0;
+  return v;
+}
+
+// Column-tile width: 192 (2-stage DMA, B_NK, N % 192 == 0) when it needs fewer rounds x columns of the
+// 512 workgroup slots (2 per CU) than 128 -- e.g. 32768 x 384: 768 tiles = 1.5 rounds at 128, 512 = 1 at 192.
+int pick_tbn(const sdmi_gemm_desc* d, int variant) {
+  static int force = -2;
+  if (force == -2) {
+    const char* s = getenv("SDMI_GEMM_TBN");
+    force = s ? atoi(s) : -1;
+  }
+  if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR || d->n % 192) return BN;
+  if (force == 128 || force == 192) return force;
+  if (d->tile_n_hint == 128 || d->tile_n_hint == 192) return d->tile_n_hint;
+  const long long mt = (d->m + BM - 1) / BM;
+  const long long r128 = (mt * ((d->n + BN - 1) / BN) + 511) / 512, r192 = (mt * (d->n / 192) + 511) / 512;
+  return r192 * 192 <= r128 * 128 ? 192 : BN;
+}
+
+template <int AM, int BMODE>
+hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
+  if (v == 0) {
     hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
-  } else if (v == 2) {
-    hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2>), grid, dim3(NT), 2 * 2 * TILE_BYTES, s, a, e);
-  } else {
+  } else if (v == 3) {
     hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 3>), grid, dim3(NT), 3 * 2 * TILE_BYTES, s, a, e);
+  } else if (tbn == BN) {
+    hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2>), grid, dim3(NT), 2 * 2 * TILE_BYTES, s, a, e);
+  } else if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR) {
+    hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2, 192>), grid, dim3(NT), 2 * (TILE_BYTES + 192 * BK * 2), s, a,
+                       e);
+  } else {
+    return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
@@ -952,7 +1046,8 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
 }
 
 int plan_splits(const sdmi_gemm_desc* d) {
-  long long tiles = (long long)((d->m + BM - 1) / BM) * ((d->n + BN - 1) / BN);
+  const int tbn = pick_tbn(d, pick_variant(d));
+  long long tiles = (long long)((d->m + BM - 1) / BM) * ((d->n + tbn - 1) / tbn);
   int nkt = (d->k + BK - 1) / BK;
   if (d->splits_hint > 0) {
     int s = std::min(d->splits_hint, nkt);
@@ -1009,7 +1104,8 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
   splits = (nkt + a.ktiles_per_split - 1) / a.ktiles_per_split;
   a.nsplit = splits;
   EpiArgs run = e;
-  dim3 grid((d->n + BN - 1) / BN, (d->m + BM - 1) / BM, splits);
+  const int variant = pick_variant(d), tbn = pick_tbn(d, variant);
+  dim3 grid((d->n + tbn - 1) / tbn, (d->m + BM - 1) / BM, splits);
   if (splits > 1) {
     run.raw = 1;
     run.ws = (const float*)workspace;
@@ -1020,11 +1116,11 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
   switch (key) {
-    case SDMI_A_ROWMAJOR * 3 + SDMI_B_NK: err = launch_t<SDMI_A_ROWMAJOR, SDMI_B_NK>(a, run, grid, s); break;
-    case SDMI_A_ROWMAJOR * 3 + SDMI_B_KN: err = launch_t<SDMI_A_ROWMAJOR, SDMI_B_KN>(a, run, grid, s); break;
-    case SDMI_A_CONV * 3 + SDMI_B_NK: err = launch_t<SDMI_A_CONV, SDMI_B_NK>(a, run, grid, s); break;
-    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN: err = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN>(a, run, grid, s); break;
-    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN_CONV: err = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN_CONV>(a, run, grid, s); break;
+    case SDMI_A_ROWMAJOR * 3 + SDMI_B_NK: err = launch_t<SDMI_A_ROWMAJOR, SDMI_B_NK>(a, run, grid, s, variant, tbn); break;
+    case SDMI_A_ROWMAJOR * 3 + SDMI_B_KN: err = launch_t<SDMI_A_ROWMAJOR, SDMI_B_KN>(a, run, grid, s, variant, tbn); break;
+    case SDMI_A_CONV * 3 + SDMI_B_NK: err = launch_t<SDMI_A_CONV, SDMI_B_NK>(a, run, grid, s, variant, tbn); break;
+    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN: err = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN>(a, run, grid, s, variant, tbn); break;
+    case SDMI_A_COLMAJOR * 3 + SDMI_B_KN_CONV: err = launch_t<SDMI_A_COLMAJOR, SDMI_B_KN_CONV>(a, run, grid, s, variant, tbn); break;
     default: return -6;
   }
   if (err != hipSuccess) return (int)err;
@@ -1034,10 +1130,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     red.nsplit = splits;
     red.split_stride = (long long)d->m * d->n;
     red.ws = (const float*)workspace;
-    long long total = (long long)d->m * d->n / (red.n8 ? 8 : 1);
-    int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, red);
-    err = hipGetLastError();
+    err = launch_reduce(red, s);
     if (err != hipSuccess) return (int)err;
   }
   return 0;

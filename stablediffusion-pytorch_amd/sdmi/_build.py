@@ -12,6 +12,10 @@ CSRC = os.path.join(PKG, "csrc")
 REPO = os.path.dirname(PKG)
 LIB = os.path.join(HERE, "libsdmi.so")
 ARCH = os.environ.get("SDMI_ARCH", "gfx950")
+# per-source extra flags. attention.hip: softmax maxima are taken straight from MFMA accumulators; in the default
+# IEEE mode every fmaxf input would first be quieted by a canonicalising v_max_f32 (one extra VALU op per score).
+# The kernels never produce or consume NaNs (masked scores are -inf), so IEEE mode is switched off there.
+EXTRA_FLAGS = {"attention.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
 
 
 def sources():
@@ -23,7 +27,7 @@ def needs_build():
         return True
     t = os.path.getmtime(LIB)
     deps = sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    deps.append(os.path.join(REPO, "include", "sdmi.h"))
+    deps += [os.path.join(REPO, "include", "sdmi.h"), os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
@@ -36,6 +40,7 @@ def build(force=False, verbose=False):
         obj = os.path.join("/tmp", "sdmi_" + os.path.basename(src) + f".{os.getpid()}.o")
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
                "-I", os.path.join(REPO, "include"), "-Rpass-analysis=kernel-resource-usage"]
+        cmd += EXTRA_FLAGS.get(os.path.basename(src), [])
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), src, cmd))
         objs.append(obj)
     spills = []

@@ -8,7 +8,7 @@ import os
 from . import plan
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsdmi.so")
+LIB_PATH = os.environ.get("SDMI_LIB_PATH") or os.path.join(_HERE, "libsdmi.so")  # override: A/B timing only
 
 # ---- enums (include/sdmi.h) ----
 A_ROWMAJOR, A_CONV, A_COLMAJOR = 0, 1, 2
@@ -43,6 +43,7 @@ class GemmDesc(ctypes.Structure):
         ("rb_mod", ctypes.c_int),
         ("aux", ctypes.c_void_p), ("ld_aux", ctypes.c_int),
         ("splits_hint", ctypes.c_int),
+        ("tile_n_hint", ctypes.c_int),
     ]
 
 

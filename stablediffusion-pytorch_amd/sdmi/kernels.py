@@ -32,6 +32,10 @@ def _log2(v):
 # optional per-launch timing hook (bench.py): list of (tag, flops, start_event, end_event, info)
 PROFILE = None
 PHASE = ""  # label prefixed to profiled launches ("fwd" / "bwd" / "wg" ...; set by the engines)
+# phases whose GEMMs may take the 192-column tile (measured per phase: faster in fwd / bwd; in the weight-gradient
+# phase its 80 KiB of LDS per workgroup crowds out the concurrent streams and the step ran 0.4 ms slower)
+# elsewhere the 128-column tile is requested
+TILE192_PHASES = set(os.environ.get("SDMI_TILE192_PHASES", "fwd,bwd").split(","))
 
 # measured split-K slice counts per GEMM shape (scripts/tune_gemm.py -> sdmi/tuned_gemm.json); None = not loaded
 TUNED = None
@@ -108,6 +112,7 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     d.rb_mod = rb_mod
     if aux is not None:
         d.aux, d.ld_aux = aux.data_ptr(), ld_aux or ld_of(aux)
+    d.tile_n_hint = 0 if (not PHASE or PHASE in TILE192_PHASES) else 128
     tuned = _tuned()
     if tuned:
         d.splits_hint = tuned.get(gemm_key(d), 0)

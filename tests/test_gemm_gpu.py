@@ -106,3 +106,41 @@ def test_convT_phases(B, H, cin, cout):
     out = torch.empty(B, 2 * H, 2 * H, cout, device="cuda", dtype=torch.bfloat16)
     k.convT_fwd_phases(xn, B, H, H, cin, cin, wph, cout, out, cout)
     close(out.permute(0, 3, 1, 2), ref)
+
+
+@pytest.mark.parametrize("splits", [0, 4])
+def test_rowmajor_nk_tile192(splits):
+    """32700 x 384 picks the 128 x 192 tile (one round of 512 workgroups); ragged M and K, bias + residual
+    epilogue, and a forced split-K (raw slabs + reducer) on the same tile."""
+    k, L = _k()
+    torch.manual_seed(5)
+    M, N, K = 32700, 384, 200
+    a = bf(torch.randn(M, K, device="cuda"))
+    w = bf(torch.randn(N, K, device="cuda"))
+    bias = torch.randn(N, device="cuda")
+    res = bf(torch.randn(M, N, device="cuda"))
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    saved = k.TUNED
+    try:
+        if splits:
+            d = k.GemmDesc()
+            d.m, d.n, d.k, d.a_mode, d.b_mode = M, N, K, L.A_ROWMAJOR, L.B_NK
+            k.TUNED = {k.gemm_key(d): splits}
+        k.gemm(M, N, K, a, L.A_ROWMAJOR, K, w, L.B_NK, K, c, N, bias=bias, resid=res, ldr=N)
+    finally:
+        k.TUNED = saved
+    close(c, a.float() @ w.float().t() + bias + res.float())
+
+
+def test_conv_fwd_tile192():
+    k, L = _k()
+    torch.manual_seed(6)
+    B, H, cin, cout = 32, 32, 64, 384
+    x = bf(torch.randn(B, cin, H, H, device="cuda"))
+    w = bf(torch.randn(cout, cin, 3, 3, device="cuda") * 0.1)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    wpk = w.permute(0, 2, 3, 1).contiguous()
+    out = torch.empty(B, H, H, cout, device="cuda", dtype=torch.bfloat16)
+    k.conv_fwd(xn, B, H, H, cin, cin, wpk, cout, 3, 3, 1, 1, out, cout)
+    close(out.permute(0, 3, 1, 2), ref)
