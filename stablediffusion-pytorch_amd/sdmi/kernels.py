@@ -39,7 +39,7 @@ TILE192_PHASES = set(os.environ.get("SDMI_TILE192_PHASES", "fwd,bwd").split(",")
 
 # measured split-K slice counts per GEMM shape (scripts/tune_gemm.py -> sdmi/tuned_gemm.json); None = not loaded
 TUNED = None
-_TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gemm.json")
+_TUNED_PATH = os.environ.get("SDMI_TUNED_GEMM") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gemm.json")
 
 
 def gemm_key(d):
