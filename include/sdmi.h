@@ -129,6 +129,9 @@ size_t sdmi_chan_reduce_workspace(int B, int P, int C);
  * statistics folded with the affine), produced by sdmi_gn_stats and consumed by apply / backward. */
 int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G, float eps, const float* gamma, const float* beta,
                   float* ws, float* table, sdmi_stream_t stream);
+/* stats + apply in one call (a single pass over x for small images); table as sdmi_gn_stats */
+int sdmi_gn_fwd(const void* x, int ldx, void* y, int ldy, int B, int P, int C, int G, float eps, const float* gamma,
+                const float* beta, int silu, float* ws, float* table, sdmi_stream_t stream);
 int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* table, int B, int P, int C, int silu,
                   sdmi_stream_t stream);
 int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,

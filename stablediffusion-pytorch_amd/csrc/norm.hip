@@ -16,6 +16,7 @@
 //   sdmi_chan_sum     : per-(b, c) and per-c sums of dy (bias / time-embedding gradients)
 //   sdmi_gn_apply / gn_bwd_apply : vectorised elementwise passes (8 channels per lane).
 #include <atomic>
+#include <cstdlib>
 
 #include "common.h"
 #include "../../include/sdmi.h"
@@ -300,6 +301,195 @@ __global__ __launch_bounds__(NT) void chan_sum_kernel(StripArgs a) {
   batch_tail(a, c0, cw, a.sum1, a.sum2, a.c_store, /*dup=*/true);  // per_c2: a second bias with the same gradient
 }
 
+// ---------------------------------------------------------------------------------------------
+// Single-pass GroupNorm for small images (P <= SMALL_IT * rows per iteration, i.e. the 16x16 and smaller
+// levels): one workgroup owns a (batch row, channel strip of whole groups), keeps its P x strip slab in
+// registers, reduces, and applies -- one launch and one read of x (and dy) instead of a statistics pass, a
+// cross-workgroup combine and a second elementwise pass.
+// ---------------------------------------------------------------------------------------------
+constexpr int SMALL_IT = 10;  // pixel rows per thread: P <= 10 * (256 / (strip/8)), >= 256 for 64/72-wide strips
+
+__host__ __device__ __forceinline__ int small_rows(int cw) { return NT / (cw >> 3); }
+
+// host: single-pass kernels enabled (SDMI_GN_SMALL=0 disables them for A/B runs)
+bool gn_small_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("SDMI_GN_SMALL");
+    on = e ? atoi(e) != 0 : 1;
+  }
+  return on != 0;
+}
+
+// per-channel sums of u (and v) over the workgroup's rows -> s1/s2[cw] in LDS (red: [NT][17] scratch)
+__device__ __forceinline__ void small_reduce(const float* u, const float* v, int cw, float (*red)[17], float* s1,
+                                             float* s2) {
+  const int t = threadIdx.x, L = cw >> 3, R = NT / L;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[t][e] = u[e]; red[t][8 + e] = v[e]; }
+  __syncthreads();
+  for (int ch = t; ch < cw; ch += NT) {
+    const int l = ch >> 3, e = ch & 7;
+    float x1 = 0.f, x2 = 0.f;
+    for (int rr = 0; rr < R; ++rr) {
+      x1 += red[rr * L + l][e];
+      x2 += red[rr * L + l][8 + e];
+    }
+    s1[ch] = x1;
+    s2[ch] = x2;
+  }
+  __syncthreads();
+}
+
+// grid (nchunks, B): y = act(GroupNorm(x)), and the forward table for the backward pass
+__global__ __launch_bounds__(NT) void gn_fwd_small_kernel(StripArgs a, bf16_t* y, int ldy) {
+  __shared__ float red[NT][17];
+  __shared__ float s1[NT], s2[NT];
+  __shared__ float2 grp[NT];
+  const int b = blockIdx.y, c0 = blockIdx.x * a.CW, cw = min(a.CW, a.C - c0);
+  const int L = cw >> 3, R = NT / L, t = threadIdx.x, lane = t % L, r = t / L;
+  const int cc = c0 + lane * 8, Cg = a.C / a.G;
+  const bool act = r < R;
+  float xv[SMALL_IT][8];
+  float u[8], v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { u[e] = 0.f; v[e] = 0.f; }
+  const bf16_t* X = a.x + (long long)b * a.P * a.ldx + cc;
+#pragma unroll
+  for (int it = 0; it < SMALL_IT; ++it) {
+    const int p = r + it * R;
+    if (act && p < a.P) {
+      unpack8(*(const uint4*)(X + (long long)p * a.ldx), xv[it]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { u[e] += xv[it][e]; v[e] = fmaf(xv[it][e], xv[it][e], v[e]); }
+    }
+  }
+  small_reduce(u, v, cw, red, s1, s2);
+  const int ng = cw / Cg;
+  if (t < ng) {
+    double m1 = 0, m2 = 0;
+    for (int c = t * Cg; c < (t + 1) * Cg; ++c) { m1 += s1[c]; m2 += s2[c]; }
+    const double n = (double)a.P * Cg, mu = m1 / n;
+    double var = m2 / n - mu * mu;
+    if (var < 0) var = 0;
+    grp[t] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)a.eps)));
+  }
+  __syncthreads();
+  for (int ch = t; ch < cw; ch += NT) {
+    const int c = c0 + ch;
+    const float2 mr = grp[ch / Cg];
+    const float sc = mr.y * a.gamma[c];
+    a.out_tab[(long long)b * a.C + c] = make_float4(sc, a.beta[c] - mr.x * sc, mr.x, mr.y);
+  }
+  if (!act) return;
+  float ta[8], ts[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float2 mr = grp[(lane * 8 + e) / Cg];
+    ta[e] = mr.y * a.gamma[cc + e];
+    ts[e] = a.beta[cc + e] - mr.x * ta[e];
+  }
+  bf16_t* Y = y + (long long)b * a.P * ldy + cc;
+#pragma unroll
+  for (int it = 0; it < SMALL_IT; ++it) {
+    const int p = r + it * R;
+    if (p < a.P) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float z = fmaf(xv[it][e], ta[e], ts[e]);
+        o[e] = a.silu ? silu_f(z) : z;
+      }
+      *(uint4*)(Y + (long long)p * ldy) = pack8(o);
+    }
+  }
+}
+
+// grid (nchunks, B): GroupNorm (+SiLU) backward in one pass; dgamma/dbeta by the batch tail
+__global__ __launch_bounds__(NT) void gn_bwd_small_kernel(StripArgs a, bf16_t* dx, int lddx, const bf16_t* add,
+                                                          int ldadd) {
+  __shared__ float red[NT][17];
+  __shared__ float s1[NT], s2[NT];
+  __shared__ float2 grp[NT];
+  const int b = blockIdx.y, c0 = blockIdx.x * a.CW, cw = min(a.CW, a.C - c0);
+  const int L = cw >> 3, R = NT / L, t = threadIdx.x, lane = t % L, r = t / L;
+  const int cc = c0 + lane * 8, Cg = a.C / a.G;
+  const bool act = r < R;
+  float xv[SMALL_IT][8], dz[SMALL_IT][8];
+  float u[8], v[8];
+  float4 tb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    u[e] = 0.f;
+    v[e] = 0.f;
+    tb[e] = act ? a.tab[(long long)b * a.C + cc + e] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const long long rb = (long long)b * a.P;
+#pragma unroll
+  for (int it = 0; it < SMALL_IT; ++it) {
+    const int p = r + it * R;
+    if (act && p < a.P) {
+      unpack8(*(const uint4*)(a.x + (rb + p) * a.ldx + cc), xv[it]);
+      unpack8(*(const uint4*)(a.dy + (rb + p) * a.ldy + cc), dz[it]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (a.silu) dz[it][e] *= silu_grad_f(fmaf(xv[it][e], tb[e].x, tb[e].y));
+        u[e] += dz[it][e];
+        v[e] = fmaf(dz[it][e], (xv[it][e] - tb[e].z) * tb[e].w, v[e]);
+      }
+    }
+  }
+  small_reduce(u, v, cw, red, s1, s2);
+  const int ng = cw / Cg;
+  const float inv_n = 1.0f / ((float)a.P * Cg);
+  if (t < ng) {
+    float A = 0.f, Bc = 0.f;
+    for (int ch = t * Cg; ch < (t + 1) * Cg; ++ch) {
+      A += a.gamma[c0 + ch] * s1[ch];
+      Bc += a.gamma[c0 + ch] * s2[ch];
+    }
+    const float4 tt = a.tab[(long long)b * a.C + c0 + t * Cg];
+    const float rs = tt.w, mu = tt.z;
+    grp[t] = make_float2(-rs * rs * Bc * inv_n, rs * rs * mu * Bc * inv_n - rs * A * inv_n);
+  }
+  if (a.sum1) {
+    for (int ch = t; ch < cw; ch += NT) {
+      float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
+      st_coherent(rp, s1[ch]);
+      st_coherent(rp + 1, s2[ch]);
+    }
+  }
+  __syncthreads();
+  if (act) {
+    float q[8], o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float2 qo = grp[(lane * 8 + e) / Cg];
+      q[e] = qo.x;
+      o[e] = qo.y;
+    }
+#pragma unroll
+    for (int it = 0; it < SMALL_IT; ++it) {
+      const int p = r + it * R;
+      if (p < a.P) {
+        float av[8], ov[8];
+        if (add) {
+          unpack8(*(const uint4*)(add + (rb + p) * ldadd + cc), av);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) av[e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ov[e] = av[e] + fmaf(tb[e].x, dz[it][e], fmaf(q[e], xv[it][e], o[e]));
+        *(uint4*)(dx + (rb + p) * lddx + cc) = pack8(ov);
+      }
+    }
+  }
+  if (!a.sum1) return;
+  if (!arrive_last(a.ctr + BATCH_CTR + blockIdx.x, a.nb)) return;
+  batch_tail(a, c0, cw, a.sum1, a.sum2, a.C);
+}
+
 struct ApplyArgs {
   const bf16_t* x; int ldx;
   bf16_t* y; int ldy;
@@ -455,6 +645,25 @@ extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G,
   return 0;
 }
 
+// stats + apply in one call: the single-pass kernel when the image is small, else gn_stats then gn_apply
+extern "C" int sdmi_gn_fwd(const void* x, int ldx, void* y, int ldy, int B, int P, int C, int G, float eps,
+                           const float* gamma, const float* beta, int silu, float* ws, float* table, sdmi_stream_t stream) {
+  if (C % 8 || G <= 0 || C % G) return -1;
+  const int cw = strip_width(C, C / G);
+  if (cw <= NT && P <= SMALL_IT * small_rows(cw) && gn_small_enabled()) {
+    StripArgs a = {};
+    a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.eps = eps; a.silu = silu;
+    a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table; a.CW = cw;
+    hipLaunchKernelGGL(gn_fwd_small_kernel, dim3((C + cw - 1) / cw, B), dim3(NT), 0, (hipStream_t)stream, a, (bf16_t*)y,
+                       ldy);
+    SDMI_CHECK_LAUNCH();
+    return 0;
+  }
+  int rc = sdmi_gn_stats(x, ldx, B, P, C, G, eps, gamma, beta, ws, table, stream);
+  if (rc) return rc;
+  return sdmi_gn_apply(x, ldx, y, ldy, table, B, P, C, silu, stream);
+}
+
 extern "C" int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* table, int B, int P, int C,
                              int silu, sdmi_stream_t stream) {
   if (C % 8) return -1;
@@ -480,6 +689,13 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   const int nch = (C + r.CW - 1) / r.CW;
   if (r.CW > NT || nch > BATCH_CTR) return -2;
   r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
+  if (P <= SMALL_IT * small_rows(r.CW) && gn_small_enabled()) {  // single pass
+    if (dgamma && !(r.ctr = counter_slot())) return -4;
+    hipLaunchKernelGGL(gn_bwd_small_kernel, dim3(nch, B), dim3(NT), 0, s, r, (bf16_t*)dx, lddx, (const bf16_t*)addend,
+                       ldadd);
+    SDMI_CHECK_LAUNCH();
+    return 0;
+  }
   const int ps = pick_psplit(nch, B, P);
   r.part = part_base(ws, B, C);
   if ((dgamma || ps > 1) && !(r.ctr = counter_slot())) return -4;

@@ -71,6 +71,7 @@ SIGNATURES = {
     "sdmi_chan_reduce_workspace": ([_I, _I, _I], _SZ),
     "sdmi_gn_stats": ([_P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
     "sdmi_gn_apply": ([_P, _I, _P, _I, _P, _I, _I, _I, _I, _P], _I),
+    "sdmi_gn_fwd": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _P, _P], _I),
     "sdmi_gn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P], _I),
     "sdmi_chan_sum": ([_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _I, _P], _I),
     "sdmi_prep_input": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),

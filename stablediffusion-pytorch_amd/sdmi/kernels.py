@@ -237,6 +237,17 @@ def gn_stats(x, B, P, C, G, gamma, beta, eps=1e-5):
     return tab
 
 
+def gn_fwd(x, B, P, C, G, gamma, beta, silu, out, eps=1e-5):
+    """out = [SiLU](GroupNorm(x)); returns the forward table (as gn_stats) for the backward pass."""
+    L = _lib.lib()
+    ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=x.device)
+    tab = torch.empty(B * C * 4, dtype=torch.float32, device=x.device)
+    with _Prof("gn_fwd", 0, f"B={B} P={P} C={C}"):
+        check(L.sdmi_gn_fwd(_p(x), ld_of(x), _p(out), ld_of(out), B, P, C, G, eps, _p(gamma), _p(beta),
+                            1 if silu else 0, _p(ws), _p(tab), _stream()), "sdmi_gn_fwd")
+    return tab
+
+
 def gn_apply(x, tab, B, P, C, silu, out):
     with _Prof("gn_apply", 0, f"B={B} P={P} C={C}"):
         check(_lib.lib().sdmi_gn_apply(_p(x), ld_of(x), _p(out), ld_of(out), _p(tab), B, P, C, 1 if silu else 0,

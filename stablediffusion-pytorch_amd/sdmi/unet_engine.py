@@ -473,9 +473,8 @@ class UNetEngine:
         tape.label = "head"
         C = L["conv_out"]
         Pn = H * W
-        tab = K.gn_stats(cur, B, Pn, C, G, P["norm_out.weight"], P["norm_out.bias"])
         hs = self._new(B * Pn, C)
-        K.gn_apply(cur, tab, B, Pn, C, True, hs)
+        tab = K.gn_fwd(cur, B, Pn, C, G, P["norm_out.weight"], P["norm_out.bias"], True, hs)
         pred = self._new(B * Pn, 8, torch.float32)
         K.conv_fwd(hs, B, H, W, C, C, self.W("conv_out#f"), 8, 3, 3, 1, 1, pred, 8, bias=P["conv_out.bias"],
                    n_store=self.im_channels)
@@ -510,16 +509,14 @@ class UNetEngine:
         P, G = self.P, self.L["G"]
         Pn = h * w
         a, b = f"{p}.resnet_conv_first.{l}", f"{p}.resnet_conv_second.{l}"
-        t1 = K.gn_stats(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"])
         h0 = self._new(B * Pn, cin)
-        K.gn_apply(x, t1, B, Pn, cin, True, h0)
+        t1 = K.gn_fwd(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"], True, h0)
         h1 = self._new(B * Pn, cout)
         off = self.temb_off[(p, l)]
         K.conv_fwd(h0, B, h, w, cin, cin, self.W(a + ".2#f"), cout, 3, 3, 1, 1, h1, cout, bias=P[a + ".2.bias"],
                    rowbias=st["temb_all"][:, off:], rb_ld=self.temb_total)
-        t2 = K.gn_stats(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"])
         h2 = self._new(B * Pn, cout)
-        K.gn_apply(h1, t2, B, Pn, cout, True, h2)
+        t2 = K.gn_fwd(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"], True, h2)
         rc = f"{p}.residual_input_conv.{l}"
         y = out if out is not None else self._new(B * Pn, cout)
         # conv2(h2) + residual 1x1(x) in ONE GEMM: A = [im2col(h2) | x], B = [W2 | Wr]
@@ -563,9 +560,8 @@ class UNetEngine:
         N = h * w
         nk = f"{p}.cross_attention_norms.{l}" if cross else f"{p}.attention_norms.{l}"
         mk = f"{p}.cross_attentions.{l}" if cross else f"{p}.attentions.{l}"
-        tab = K.gn_stats(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"])
         a = self._new(B * N, C)
-        K.gn_apply(x, tab, B, N, C, False, a)
+        tab = K.gn_fwd(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"], False, a)
         Win = self.W(mk + ".in_proj_weight#f")
         bin_ = P[mk + ".in_proj_bias"]
         d = C // Hh

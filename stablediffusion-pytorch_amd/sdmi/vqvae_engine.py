@@ -131,15 +131,13 @@ class VQVAEEngine:
         P, G = self.P, self.L["G"]
         Pn = h * w
         a, b = f"{p}.resnet_conv_first.{l}", f"{p}.resnet_conv_second.{l}"
-        t1 = K.gn_stats(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"])
         h0 = self._new(B * Pn, cin)
-        K.gn_apply(x, t1, B, Pn, cin, True, h0)
+        t1 = K.gn_fwd(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"], True, h0)
         h1 = self._new(B * Pn, cout)
         K.conv_fwd(h0, B, h, w, cin, cin, self.W(a + ".2"), cout, 3, 3, 1, 1, h1, cout, bias=P[a + ".2.bias"])
         del h0
-        t2 = K.gn_stats(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"])
         h2 = self._new(B * Pn, cout)
-        K.gn_apply(h1, t2, B, Pn, cout, True, h2)
+        t2 = K.gn_fwd(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"], True, h2)
         del h1
         y = self._new(B * Pn, cout)
         K.conv_fwd(h2, B, h, w, cout, cout, self.W(f"{p}.res{l}#cat"), cout, 3, 3, 1, 1, y, cout,
@@ -150,9 +148,8 @@ class VQVAEEngine:
         P, G, Hh = self.P, self.L["G"], self.L["heads"]
         N = h * w
         nk, mk = f"{p}.attention_norms.{l}", f"{p}.attentions.{l}"
-        tab = K.gn_stats(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"])
         a = self._new(B * N, C)
-        K.gn_apply(x, tab, B, N, C, False, a)
+        tab = K.gn_fwd(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"], False, a)
         qkv = self._new(B * N, 3 * C)
         K.linear(a, self.W(mk + "#in"), qkv, bias=P[mk + ".in_proj_bias"])
         o = self._new(B * N, C)
@@ -170,9 +167,8 @@ class VQVAEEngine:
 
     def _head(self, key_norm, key_conv, x, B, h, w, C, n_store):
         P = self.P
-        tab = K.gn_stats(x, B, h * w, C, self.L["G"], P[key_norm + ".weight"], P[key_norm + ".bias"])
         hs = self._new(B * h * w, C)
-        K.gn_apply(x, tab, B, h * w, C, True, hs)
+        tab = K.gn_fwd(x, B, h * w, C, self.L["G"], P[key_norm + ".weight"], P[key_norm + ".bias"], True, hs)
         out = self._new(B * h * w, 8, torch.float32)
         K.conv_fwd(hs, B, h, w, C, C, self.W(key_conv), 8, 3, 3, 1, 1, out, 8, bias=P[key_conv + ".bias"],
                    n_store=n_store)

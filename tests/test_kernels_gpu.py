@@ -52,6 +52,16 @@ def test_groupnorm_fwd_bwd(B, H, C, G, silu):
     assert relerr(dx.view(B, P, C).permute(0, 2, 1), xr.grad) < 2e-2
     assert relerr(dg, gr.grad) < 1e-2
     assert relerr(db, br.grad) < 1e-2
+    # gn_fwd (single pass for P <= 256, stats + apply beyond): same output and table
+    y2 = torch.empty_like(x2)
+    tab2 = k.gn_fwd(x2, B, P, C, G, gamma, beta, silu, y2)
+    assert relerr(y2.view(B, P, C).permute(0, 2, 1), yr.detach()) < 1e-2
+    assert relerr(tab2, tab) < 1e-4
+    # in-place backward (dx aliases dy) with an addend, as the resnet blocks call it
+    add = bf(torch.randn(B * P, C, device="cuda"))
+    buf = dy.view(B * P, C).clone()
+    k.gn_bwd(x2, buf, buf, tab2, gamma, B, P, C, G, silu, None, None, addend=add)
+    assert relerr(buf.view(B, P, C).permute(0, 2, 1), xr.grad + add.float().view(B, P, C).permute(0, 2, 1)) < 2e-2
 
 
 @pytest.mark.parametrize("B,Hh,N,S,d", [(2, 16, 64, 64, 8), (2, 16, 256, 256, 24), (1, 16, 16, 77, 32),
