@@ -17,6 +17,8 @@
 //      -> conflict-free transposed reads.
 // Split-K (for the small-grid weight-gradient and deep low-resolution GEMMs) writes fp32 slabs that
 // a second kernel reduces while applying the same epilogue.
+#include <atomic>
+
 #include "common.h"
 #include "../../include/sdmi.h"
 #include <string.h>
@@ -970,17 +972,25 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, i
   return hipGetLastError();
 }
 
-__device__ unsigned g_splitk_counters[1 << 16];  // zero at load; every tile re-arms its own counter
+// Split-K arrival counters: SK_SLOTS regions of SK_SLOT_TILES, one region per launch, round-robin, so split
+// GEMMs in flight at the same time on different streams never share a counter. Zero at load; the last arriver
+// of every tile re-arms its counter (plan / graph replays included).
+constexpr int SK_SLOTS = 64, SK_SLOT_TILES = 4096;
+__device__ unsigned g_splitk_counters[SK_SLOTS * SK_SLOT_TILES];
 
-// per-device address of the split-K arrival counters, or null when SDMI_SPLITK_FUSED=0
-unsigned* splitk_counters() {
+// counter region for one launch of `tiles` output tiles, or null (separate reducer) when SDMI_SPLITK_FUSED=0
+// or the launch has more tiles than a region
+unsigned* splitk_counters(long long tiles) {
   static int fused = -1;
   static unsigned* addr[64] = {};
+  static std::atomic<unsigned> next{0};
   if (fused < 0) {
     const char* s = getenv("SDMI_SPLITK_FUSED");
-    fused = s ? atoi(s) != 0 : 0;  // measured slower than the separate reducer on the step's shapes
+    // off by default: the last arriver reads all of its tile's slabs alone (up to MiBs for the deep weight-gradient
+    // splits); measured 3.5 ms/step slower than the separate reducer launch
+    fused = s ? atoi(s) != 0 : 0;
   }
-  if (!fused) return nullptr;
+  if (!fused || tiles > SK_SLOT_TILES) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (!addr[dev]) {
@@ -988,7 +998,7 @@ unsigned* splitk_counters() {
     if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_splitk_counters)) != hipSuccess) return nullptr;
     addr[dev] = (unsigned*)p;
   }
-  return addr[dev];
+  return addr[dev] + (size_t)(next.fetch_add(1) % SK_SLOTS) * SK_SLOT_TILES;
 }
 
 int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
@@ -1111,7 +1121,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     run.ws = (const float*)workspace;
     run.nsplit = splits;
     run.split_stride = (long long)d->m * d->n;
-    if ((long long)grid.x * grid.y <= (1 << 16)) run.counters = splitk_counters();
+    run.counters = splitk_counters((long long)grid.x * grid.y);
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
