@@ -978,19 +978,19 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, i
 constexpr int SK_SLOTS = 64, SK_SLOT_TILES = 4096;
 __device__ unsigned g_splitk_counters[SK_SLOTS * SK_SLOT_TILES];
 
-// counter region for one launch of `tiles` output tiles, or null (separate reducer) when SDMI_SPLITK_FUSED=0
-// or the launch has more tiles than a region
-unsigned* splitk_counters(long long tiles) {
-  static int fused = -1;
+// counter region for one launch of `tiles` output tiles split `splits` ways, or null (separate reducer launch).
+// The in-launch combine is used up to SDMI_SPLITK_FUSED splits (default 0 = never): its last arriver reads all of
+// the tile's slabs alone; measured slower than the reducer launch on the cond-UNet step even for 2-way splits
+// (+0.2 ms/step at <= 2, +0.5 at <= 4, +3.5 at any).
+unsigned* splitk_counters(long long tiles, int splits) {
+  static int fused_max = -1;
   static unsigned* addr[64] = {};
   static std::atomic<unsigned> next{0};
-  if (fused < 0) {
+  if (fused_max < 0) {
     const char* s = getenv("SDMI_SPLITK_FUSED");
-    // off by default: the last arriver reads all of its tile's slabs alone (up to MiBs for the deep weight-gradient
-    // splits); measured 3.5 ms/step slower than the separate reducer launch
-    fused = s ? atoi(s) != 0 : 0;
+    fused_max = s ? atoi(s) : 0;
   }
-  if (!fused || tiles > SK_SLOT_TILES) return nullptr;
+  if (splits > fused_max || tiles > SK_SLOT_TILES) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (!addr[dev]) {
@@ -1121,7 +1121,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     run.ws = (const float*)workspace;
     run.nsplit = splits;
     run.split_stride = (long long)d->m * d->n;
-    run.counters = splitk_counters((long long)grid.x * grid.y);
+    run.counters = splitk_counters((long long)grid.x * grid.y, splits);
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
