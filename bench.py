@@ -10,6 +10,7 @@ all-reduce (N > 1), clip(1.0), Adam(1e-5), EMA(0.9999), bf16 weight repack. Prin
 """
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -38,9 +39,15 @@ PEAK_HBM = 8.0e12
 
 
 # GEMM mode tag -> kernel symbol (gemm.hip launch_t: DMA mainloop for row-major / conv A, register staging for col-major A)
-DOMINANT_KERNEL = {"gemm_a1b0": "gemm_dma_kernel<1, 0, 2>", "gemm_a0b0": "gemm_dma_kernel<0, 0, 2>",
-                   "gemm_a0b1": "gemm_dma_kernel<0, 1, 2>", "gemm_a2b1": "gemm_kernel<2, 1>",
-                   "gemm_a2b2": "gemm_kernel<2, 2>"}
+def kernel_name(tag, info):
+    """Kernel instantiation of a profiled sdmi_gemm launch (as rocprofv3 names it), from its mode tag
+    (gemm_a<A>b<B>) and the variant / tile_n the library reported (sdmi_gemm_kernel_info)."""
+    a, b = re.match(r"gemm_a(\d)b(\d)", tag).groups()
+    v = int(re.search(r"variant=(\d+)", info).group(1))
+    tn = int(re.search(r"tile_n=(\d+)", info).group(1))
+    if v == 0:
+        return f"gemm_kernel<{a}, {b}>"
+    return f"gemm_dma_kernel<{a}, {b}, {v}, {tn if v == 2 else 128}>"
 PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
 
 
@@ -312,7 +319,7 @@ def main():
         eager_step()
         torch.cuda.synchronize()
         prof, K.PROFILE = K.PROFILE, None
-        by = {}
+        by, per_kernel = {}, {}
         for tag, fl, e0, e1, sp in prof:
             if not tag.startswith("gemm"):
                 continue
@@ -321,21 +328,37 @@ def main():
             a[0] += fl
             a[1] += ms
             a[2] += 1
+            kern = kernel_name(tag, sp)
+            split = int(re.search(r"splits=(\d+)", sp).group(1)) > 1
+            k = per_kernel.setdefault(kern, {"fl": 0.0, "ms": 0.0, "n": 0, "fl1": 0.0, "ms1": 0.0, "n1": 0, "mode": tag})
+            k["fl"] += fl
+            k["ms"] += ms
+            k["n"] += 1
+            if not split:  # the event brackets the kernel alone (split launches add a reducer launch)
+                k["fl1"] += fl
+                k["ms1"] += ms
+                k["n1"] += 1
         tot_fl = sum(v[0] for v in by.values())
         tot_ms = sum(v[1] for v in by.values())
-        dom = max(by.items(), key=lambda kv: kv[1][1])
-        dfl, dms, dn = dom[1]
-        traffic = pmc_traffic(DOMINANT_KERNEL.get(dom[0]))
-        roof = {"bound": "mfma", "kernel": f"sdmi {DOMINANT_KERNEL.get(dom[0], dom[0])} ({dom[0]}: implicit-GEMM conv "
-                                           f"fwd/dgrad launches of one step)" if dom[0] == "gemm_a1b0" else dom[0],
+        dname, d = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
+        use1 = d["n1"] > 0
+        dfl, dms, dn = (d["fl1"], d["ms1"], d["n1"]) if use1 else (d["fl"], d["ms"], d["n"])
+        traffic = pmc_traffic(dname)
+        roof = {"bound": "mfma", "kernel": f"sdmi {dname} ({d['mode']}: implicit-GEMM conv fwd/dgrad)"
+                if d["mode"] == "gemm_a1b0" else f"sdmi {dname} ({d['mode']})",
                 "achieved": dfl / (dms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
-                "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic, "traffic_unit": "bytes/launch (HBM, PMC)",
-                "launches": dn, "avg_launch_us": dms * 1e3 / dn, "flop_per_launch": dfl / dn,
+                "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic,
+                "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, all launches of the kernel)",
+                "launches": dn, "launches_note": "unsplit launches of the kernel in one step (HIP events on its stream)"
+                if use1 else "all launches (each includes its split-K reducer launch)",
+                "avg_launch_us": dms * 1e3 / dn, "flop_per_launch": dfl / dn,
+                "kernel_ms_per_step": d["ms"], "kernel_launches_per_step": d["n"],
                 "all_gemm": {"tflops": tot_fl / (tot_ms * 1e-3) / 1e12, "ms_per_step": tot_ms,
                              "launches": sum(v[2] for v in by.values())},
                 "per_mode": {k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms": v[1], "launches": v[2]}
                              for k, v in by.items()},
-                "dominant_mode": dom[0]}
+                "per_kernel": {k: {"tflops": v["fl"] / (v["ms"] * 1e-3) / 1e12, "ms": v["ms"], "launches": v["n"]}
+                               for k, v in per_kernel.items()}}
 
     FLOP = wl["flop"]
     result = {

@@ -98,6 +98,9 @@ typedef struct sdmi_gemm_desc {
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */
+/* mainloop variant (0 register-staged, 2 / 3 LDS-DMA stages) and column-tile width (128 / 192) a launch of d
+ * uses; host-only, for profiling attribution */
+int sdmi_gemm_kernel_info(const sdmi_gemm_desc* d, int* variant, int* tile_n);
 int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* workspace_bytes);
 int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t workspace_bytes, sdmi_stream_t stream);
 

@@ -1089,6 +1089,16 @@ int plan_splits(const sdmi_gemm_desc* d) {
 
 }  // namespace
 
+// which mainloop / column-tile width a launch of this descriptor uses (variant: 0 register-staged, 2 / 3 LDS-DMA
+// ring stages; tile_n: 128 or 192) -- for profiling / roofline attribution
+extern "C" int sdmi_gemm_kernel_info(const sdmi_gemm_desc* d, int* variant, int* tile_n) {
+  if (!d) return -1;
+  const int v = pick_variant(d);
+  if (variant) *variant = v;
+  if (tile_n) *tile_n = pick_tbn(d, v);
+  return 0;
+}
+
 extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) {
   Args a;
   EpiArgs e;

@@ -65,6 +65,8 @@ class PackDesc(ctypes.Structure):
 SIGNATURES = {
     "sdmi_gemm_plan": ([ctypes.POINTER(GemmDesc), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_size_t)], _I),
     "sdmi_gemm": ([ctypes.POINTER(GemmDesc), _P, _SZ, _P], _I),
+    "sdmi_gemm_kernel_info": ([ctypes.POINTER(GemmDesc), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
+                              _I),
     "sdmi_attn_fwd": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _P], _I),
     "sdmi_attn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I,
                        _I, _I, _I, _I, _I, _P], _I),
@@ -135,7 +137,7 @@ class _Lib:
 
 
 # entry points that only answer host-side queries (never launch; not recorded)
-_HOST_ONLY = {"sdmi_gemm_plan", "sdmi_chan_reduce_workspace", "sdmi_mse_workspace", "sdmi_pack_chunk",
+_HOST_ONLY = {"sdmi_gemm_plan", "sdmi_gemm_kernel_info", "sdmi_chan_reduce_workspace", "sdmi_mse_workspace", "sdmi_pack_chunk",
               "sdmi_optim_workspace", "sdmi_ln_chunk_rows", "sdmi_vq_workspace"}
 
 

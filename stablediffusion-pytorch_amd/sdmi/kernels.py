@@ -122,7 +122,12 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     ws = None
     if ws_bytes.value:
         ws = torch.empty(ws_bytes.value // 4, dtype=torch.float32, device=c.device)
-    with _Prof(f"gemm_a{a_mode}b{b_mode}", 2.0 * m * n * k, f"M={m} N={n} K={k} splits={splits.value}"):
+    info = ""
+    if PROFILE is not None:  # attribute the launch to its kernel instantiation (roofline / profiles)
+        var, tn = ctypes.c_int(0), ctypes.c_int(0)
+        check(L.sdmi_gemm_kernel_info(ctypes.byref(d), ctypes.byref(var), ctypes.byref(tn)), "sdmi_gemm_kernel_info")
+        info = f" variant={var.value} tile_n={tn.value}"
+    with _Prof(f"gemm_a{a_mode}b{b_mode}", 2.0 * m * n * k, f"M={m} N={n} K={k} splits={splits.value}{info}"):
         check(L.sdmi_gemm(ctypes.byref(d), ws.data_ptr() if ws is not None else None, ws_bytes.value, _stream()),
               "sdmi_gemm")
     return c
