@@ -278,28 +278,6 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
-// delta[bh][q] = sum_d dO[q][h*d + .] * O[q][h*d + .]
-__global__ void attn_delta_kernel(AttnArgs a) {
-  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // (b, q, h)
-  long long total = (long long)a.B * a.N * a.H;
-  if (idx >= total) return;
-  int h = idx % a.H;
-  long long bq = idx / a.H;
-  int q = bq % a.N;
-  int b = bq / a.N;
-  const bf16_t* O = a.o + bq * a.ldo + h * a.d;
-  const bf16_t* dO = a.dout + bq * a.lddo + h * a.d;
-  float s = 0.f;
-  for (int j = 0; j < a.d; j += 8) {
-    float x[8], y[8];
-    unpack8(*(const uint4*)(O + j), x);
-    unpack8(*(const uint4*)(dO + j), y);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += x[e] * y[e];
-  }
-  ((float*)a.delta)[((long long)b * a.H + h) * a.N + q] = s;
-}
-
 // =============================================================================================
 // backward: dK, dV (keys on lanes, 128 keys per workgroup, query tiles streamed)
 // =============================================================================================
@@ -439,7 +417,23 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     row_frags<DP>(of[g], a.dout + (long long)b * a.N * a.lddo, a.lddo, myq[g], a.N, h * a.d, a.d, lane);
     const bool ok = myq[g] < a.N;
     const float L = ok ? -a.lse[(long long)bh * a.N + myq[g]] : -INFINITY;
-    const float D = ok ? -a.delta[(long long)bh * a.N + myq[g]] : 0.f;
+    // delta = rowsum(dO * O) of this query row: the four lane groups hold disjoint 8-column chunks of the row
+    float D = 0.f;
+    {
+      s16x8 orow[KS];
+      row_frags<DP>(orow, a.o + (long long)b * a.N * a.ldo, a.ldo, myq[g], a.N, h * a.d, a.d, lane);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float x[8], y[8];
+        unpack8(__builtin_bit_cast(uint4, orow[ks]), x);
+        unpack8(__builtin_bit_cast(uint4, of[g][ks]), y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) D = fmaf(x[e], y[e], D);
+      }
+      D = xsum4(D);
+      if (ok && (lane >> 4) == 0) ((float*)a.delta)[(long long)bh * a.N + myq[g]] = D;
+      D = -D;
+    }
     nlse[g] = (f32x2_t){L, L};
     ndlt[g] = (f32x2_t){D, D};
 #pragma unroll
@@ -567,15 +561,13 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
   int rc = check_args(a);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  long long rows = (long long)B * N * H;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, a);
-  SDMI_CHECK_LAUNCH();
+  // the dQ kernel also produces delta = rowsum(dO * O) (written to delta_ws) for the dK/dV kernel after it
   dim3 gk((S + ROWS - 1) / ROWS, B * H), gq((N + ROWS - 1) / ROWS, B * H);
   switch ((d + 15) / 16) {
 #define SDMI_ATTN_BWD(DT)                                            \
   case DT:                                                           \
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<DT>, gk, dim3(NT), 0, s, a); \
     hipLaunchKernelGGL(attn_bwd_dq_kernel<DT>, gq, dim3(NT), 0, s, a);  \
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<DT>, gk, dim3(NT), 0, s, a); \
     break;
     SDMI_ATTN_BWD(1)
     SDMI_ATTN_BWD(2)
