@@ -253,6 +253,20 @@ typedef struct sdmi_pack_desc {
 int sdmi_pack_chunk(void);
 int sdmi_pack_weights(const sdmi_pack_desc* descs_dev, const void* bmap_dev, int nblocks, sdmi_stream_t stream);
 
+/* Transposed weight layouts derived from already-packed bf16 ones (the dgrad layout of a conv is its forward
+ * layout transposed per tap with the taps flipped; sub-pixel phase layouts select 4 of 16 taps):
+ * dst[i*dst_ld + t*dst_tap + o] = src[o*src_ld + smap[t]*src_tap + i] for o < O, i < I, t < taps.
+ * Work split: one workgroup per 64 (o) x 64 (i) tile of one tap; bmap_dev holds one int4 (descriptor, first i,
+ * first o, tap) per workgroup. src / dst 16-byte aligned rows; I and O multiples of 8 within the padded views. */
+typedef struct sdmi_tpack_desc {
+  const void* src;
+  void* dst;
+  int O, I, taps;
+  int src_ld, src_tap, dst_ld, dst_tap;
+  signed char smap[16];
+} sdmi_tpack_desc;
+int sdmi_pack_transpose(const sdmi_tpack_desc* descs_dev, const void* bmap_dev, int nblocks, sdmi_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Optimizer step over flat fp32 buffers (train_ddpm_cond_celebhq_multi_gpu.py:362-378):
  * GradScaler.unscale_ + clip_grad_norm_(max_norm) + non-finite skip + scaler.update (state on device:

@@ -259,7 +259,47 @@ __global__ void pack_kernel(const sdmi_pack_desc* descs, const int2* bmap) {
     __syncthreads();
   }
 }
+// dst[i][t][o] = src[o][smap[t]][i] over 64 x 64 tiles staged in LDS: 16-byte loads of src rows, 16-byte stores of
+// dst rows (each gathered from one LDS column).
+__global__ __launch_bounds__(NT) void pack_transpose_kernel(const sdmi_tpack_desc* descs, const int4* bmap) {
+  __shared__ __attribute__((aligned(16))) bf16_t t[64][72];  // [o][i]
+  const int4 bm = bmap[blockIdx.x];
+  const sdmi_tpack_desc& d = descs[bm.x];
+  const int i0 = bm.y, o0 = bm.z, tap = bm.w;
+  const bf16_t* src = (const bf16_t*)d.src + (long long)d.smap[tap] * d.src_tap;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + k * NT;  // 64 rows x 8 chunks
+    const int r = q >> 3, c = (q & 7) * 8;
+    const int o = o0 + r, i = i0 + c;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (o < d.O && i < d.I) v = *(const uint4*)(src + (long long)o * d.src_ld + i);
+    *(uint4*)&t[r][c] = v;
+  }
+  __syncthreads();
+  bf16_t* dst = (bf16_t*)d.dst + (long long)tap * d.dst_tap;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int q = threadIdx.x + k * NT;  // 64 dst rows (i) x 8 chunks of o
+    const int r = q >> 3, c = (q & 7) * 8;
+    const int i = i0 + r, o = o0 + c;
+    if (i >= d.I || o >= d.O) continue;
+    bf16_t w[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e] = t[c + e][r];
+    *(uint4*)(dst + (long long)i * d.dst_ld + o) = *(const uint4*)w;
+  }
+}
 }  // namespace
+
+extern "C" int sdmi_pack_transpose(const sdmi_tpack_desc* descs_dev, const void* bmap_dev, int nblocks,
+                                   sdmi_stream_t stream) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(pack_transpose_kernel, dim3(nblocks), dim3(NT), 0, (hipStream_t)stream, descs_dev,
+                     (const int4*)bmap_dev);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int sdmi_prep_input(const float* x, int B, int cx, int H, int W, const float* mask, int cmi, int MH, int MW,
                                const float* wcond, int cmo, void* out, int cpad, const float* keep,

@@ -54,6 +54,11 @@ _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlon
 _SZ = ctypes.c_size_t
 
 
+class TPackDesc(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p)] + [(n, ctypes.c_int) for n in (
+        "O", "I", "taps", "src_ld", "src_tap", "dst_ld", "dst_tap")] + [("smap", ctypes.c_byte * 16)]
+
+
 class PackDesc(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p),
                 ("so", ctypes.c_longlong), ("si", ctypes.c_longlong), ("skh", ctypes.c_longlong),
@@ -88,6 +93,7 @@ SIGNATURES = {
     "sdmi_copy_slice": ([_P, _I, _P, _I, _L, _I, _I, _P], _I),
     "sdmi_pack_chunk": ([], _I),
     "sdmi_pack_weights": ([_P, _P, _I, _P], _I),
+    "sdmi_pack_transpose": ([_P, _P, _I, _P], _I),
     "sdmi_optim_workspace": ([], _SZ),
     "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
     "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P], _I),

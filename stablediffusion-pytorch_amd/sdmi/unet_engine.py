@@ -76,6 +76,7 @@ class PackPlan:
     def __init__(self, device):
         self.device = device
         self.items = []  # (name, src tensor, dims, shape of packed view)
+        self.titems = []  # layouts derived from packed views by per-tap transposes (add_transpose)
         self.total = 0
         self.views = {}
 
@@ -99,6 +100,19 @@ class PackPlan:
             assert width % 8 == 0 and (row0 * width + col0) % 8 == 0, "16-byte aligned pack destination"
         self.items.append(dict(src=src, dst_off=dst_off, O=O, I=I, Ipad=Ipad, KH=KH, KW=KW, so=so, si=si, skh=skh,
                                skw=skw, kh_off=kh_off, kh_mul=kh_mul, kw_off=kw_off, kw_mul=kw_mul, dst_ld=dst_ld))
+
+    def add_transpose(self, name, src_view, O, I, taps, smap, src_tap, src_col0=0, rows=None, opad=None):
+        """Derived layout from an already-packed view (run after the packs, bf16 -> bf16, per-tap transpose):
+        name[i][t][o] = src_view[o][src_col0 + smap[t] * src_tap + i] for o < O, i < I; the view is
+        [rows or I][taps * (opad or O)] (padding rows / columns stay zero)."""
+        Opad = opad or O
+        assert Opad % 8 == 0 and src_tap % 8 == 0 and src_col0 % 8 == 0 and len(smap) == taps <= 16
+        width = taps * Opad
+        off = self.total
+        self.total += ((rows or I) * width + 63) // 64 * 64
+        self.views[name] = (off, rows or I, width)
+        self.titems.append(dict(dst_off=off, src_view=src_view, src_col0=src_col0, O=O, I=I, taps=taps,
+                                smap=list(smap), src_tap=src_tap, dst_ld=width, dst_tap=Opad))
 
     def reserve(self, name, rows, width):
         off = self.total
@@ -124,6 +138,23 @@ class PackPlan:
         self.bmap_dev = torch.tensor(bmap, dtype=torch.int32).reshape(-1).to(self.device)
         self.nblocks = len(bmap)
         self.ptrs = [it["src"].data_ptr() for it in self.items]
+        tdescs = (_lib.TPackDesc * max(1, len(self.titems)))()
+        tmap = []
+        for j, it in enumerate(self.titems):
+            d = tdescs[j]
+            sbase, _, swidth = self.views[it["src_view"]]
+            d.src = self.buf.data_ptr() + 2 * (sbase + it["src_col0"])
+            d.dst = self.buf.data_ptr() + 2 * it["dst_off"]
+            d.O, d.I, d.taps = it["O"], it["I"], it["taps"]
+            d.src_ld, d.src_tap, d.dst_ld, d.dst_tap = swidth, it["src_tap"], it["dst_ld"], it["dst_tap"]
+            assert swidth % 8 == 0
+            for t, v in enumerate(it["smap"]):
+                d.smap[t] = v
+            tmap += [(j, i, o, t) for i in range(0, it["I"], 64) for o in range(0, it["O"], 64)
+                     for t in range(it["taps"])]
+        self.tdesc_dev = torch.frombuffer(bytearray(bytes(tdescs)), dtype=torch.uint8).to(self.device)
+        self.tmap_dev = torch.tensor(tmap or [(0, 0, 0, 0)], dtype=torch.int32).reshape(-1).to(self.device)
+        self.ntiles = len(tmap)
 
     def view(self, name):
         off, rows, width = self.views[name]
@@ -132,6 +163,8 @@ class PackPlan:
     def run(self):
         _lib.check(_lib.lib().sdmi_pack_weights(self.desc_dev.data_ptr(), self.bmap_dev.data_ptr(), self.nblocks,
                                                 K._stream()), "sdmi_pack_weights")
+        _lib.check(_lib.lib().sdmi_pack_transpose(self.tdesc_dev.data_ptr(), self.tmap_dev.data_ptr(), self.ntiles,
+                                                  K._stream()), "sdmi_pack_transpose")
 
     def stale(self):
         return any(it["src"].data_ptr() != p for it, p in zip(self.items, self.ptrs))
@@ -224,7 +257,10 @@ class UNetEngine:
             Ip = ipad or I
             if fwd:
                 pk.add(key + "#f", w, O, I, Ip, KH, KW, I * KH * KW, KH * KW, KW, 1, rows=opad)
-            if dgrad:  # stride-1 dgrad: [I][KH][KW][O] with flipped taps
+            if dgrad and fwd:  # stride-1 dgrad [I][KH][KW][O] with flipped taps = the forward layout transposed
+                pk.add_transpose(key + "#d", key + "#f", O, I, KH * KW, [KH * KW - 1 - t for t in range(KH * KW)], Ip,
+                                 rows=ipad, opad=opad)
+            elif dgrad:
                 pk.add(key + "#d", w, I, O, opad or O, KH, KW, KH * KW, I * KH * KW, KW, 1, KH - 1, -1, KW - 1, -1,
                        rows=ipad)
 
@@ -247,7 +283,6 @@ class UNetEngine:
             pk.add(None, w, cout, L["T"], L["T"], 1, 1, L["T"], 1, 0, 0, into="temb_all", row0=self.temb_off[(p, l)])
         for (p, l, cin, cout) in self.resnets:
             conv(f"{p}.resnet_conv_first.{l}.2")
-            conv(f"{p}.resnet_conv_second.{l}.2", fwd=False)
             # second conv and the 1x1 residual conv as one K-concatenated weight [cout][9*cout + cin]
             w2 = P[f"{p}.resnet_conv_second.{l}.2.weight"]
             wr = P[f"{p}.residual_input_conv.{l}.weight"]
@@ -255,6 +290,8 @@ class UNetEngine:
             pk.reserve(cat, cout, 9 * cout + cin)
             pk.add(None, w2, cout, cout, cout, 3, 3, cout * 9, 9, 3, 1, into=cat)
             pk.add(None, wr, cout, cin, cin, 1, 1, cin, 1, 0, 0, into=cat, col0=9 * cout)
+            # its dgrad layout: the conv part of the concatenated forward weight, transposed per (flipped) tap
+            pk.add_transpose(f"{p}.resnet_conv_second.{l}.2#d", cat, cout, cout, 9, [8 - t for t in range(9)], cout)
         nd = len(L["down"]) - 1
         for i in range(nd):
             p = f"downs.{i}"
@@ -272,8 +309,9 @@ class UNetEngine:
                 C = w.shape[0]
                 conv(key, dgrad=False)
                 for ph in range(2):
-                    for pw in range(2):  # dgrad phases: [ci][a][b][co] = W[co][ci][3-ph-2a][3-pw-2b]
-                        pk.add(f"{key}#d{ph}{pw}", w, C, C, C, 2, 2, 16, C * 16, 4, 1, 3 - ph, -2, 3 - pw, -2)
+                    for pw in range(2):  # dgrad phases: [ci][a][b][co] = W[co][ci][3-ph-2a][3-pw-2b] = #f[co][tap][ci]
+                        pk.add_transpose(f"{key}#d{ph}{pw}", key + "#f", C, C, 4,
+                                         [(3 - ph - 2 * a) * 4 + (3 - pw - 2 * b) for a in range(2) for b in range(2)], C)
         for i in range(len(L["mid"]) - 1):
             p = f"mids.{i}"
             for l in range(L["n_mid"]):
@@ -296,11 +334,13 @@ class UNetEngine:
                 key = f"{p}.up_sample_conv"
                 w = P[key + ".weight"]  # (Cx, Cy, 4, 4)
                 Cx, Cy = w.shape[0], w.shape[1]
-                for ph in range(2):
-                    for pw in range(2):  # fwd phases: [co][a][b][ci] = W[ci][co][3-ph-2a][3-pw-2b]
-                        pk.add(f"{key}#f{ph}{pw}", w, Cy, Cx, Cx, 2, 2, 16, Cy * 16, 4, 1, 3 - ph, -2, 3 - pw, -2)
                 # dgrad = stride-2 conv over dY: [ci][kh][kw][co] = W[ci][co][kh][kw]
                 pk.add(f"{key}#d", w, Cx, Cy, Cy, 4, 4, Cy * 16, 16, 4, 1)
+                for ph in range(2):
+                    for pw in range(2):  # fwd phases: [co][a][b][ci] = W[ci][co][3-ph-2a][3-pw-2b] = #d[ci][tap][co]
+                        pk.add_transpose(f"{key}#f{ph}{pw}", f"{key}#d", Cx, Cy, 4,
+                                         [(3 - ph - 2 * a) * 4 + (3 - pw - 2 * b) for a in range(2) for b in range(2)],
+                                         Cy)
         conv("conv_out", ipad=None, opad=8)
         pk.finalize()
         self.pack = pk
