@@ -90,14 +90,15 @@ class DIT(nn.Module):
     def forward(self, x, t, cond_input=None):
         if self.cond:
             assert cond_input is not None, "Model initialized with conditioning so cond_input cannot be None"
-        mask = text = None
+        mask = text = klass = None
         if self.image_cond:
             validate_image_conditional_input(cond_input, x)
             mask = cond_input["image"]
         if self.class_cond:
             validate_class_conditional_input(cond_input, x, self.num_classes)
+            klass = cond_input["class"]
         if self.text_cond:
             assert "text" in cond_input, \
                 "Model initialized with text conditioning but cond_input has no text information"
             text = cond_input["text"]
-        return run_denoiser(self, self._sdmi, x, t, text, mask)
+        return run_denoiser(self, self._sdmi, x, t, text, mask, klass)

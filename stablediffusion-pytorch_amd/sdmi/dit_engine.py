@@ -34,6 +34,8 @@ def dit_layout(cfg, im_channels=4):
         ic = cond["image_condition_config"]
         L["im_in"] = ic["image_condition_input_channels"]
         L["im_out"] = ic["image_condition_output_channels"]
+    if L["klass"]:
+        L["num_classes"] = cond["class_condition_config"]["num_classes"]
     L["patch_in"] = im_channels + (L["im_out"] if L["image"] else 0)
     L["mod_w"] = 6 * L["D"] * L["n_layers"] + 2 * L["D"]
     return L
@@ -83,8 +85,9 @@ class DiTEngine:
         self.cfg = cfg
         self.L = dit_layout(cfg, im_channels)
         L = self.L
-        if L["klass"]:
-            raise NotImplementedError("class conditioning is not wired into the HIP DiT engine yet")
+        # class conditioning (transformer.py:176-181): sinusoidal t_emb += class @ class_emb.weight before t_proj,
+        # one GEMM with the class count zero-padded to a multiple of 8
+        self.kpad = (L["num_classes"] + 7) // 8 * 8 if L["klass"] else 0
         if L["D"] % 8 or L["D"] > 512 or L["D"] % 4:
             raise ValueError("hidden_size must be a multiple of 8 and <= 512 for the row kernels")
         if L["A"] % 8 or L["head_dim"] % 8 or L["head_dim"] > 64:
@@ -116,6 +119,9 @@ class DiTEngine:
         pk.add("pe", w, D, ci, self.cpad, p, p, p * p * ci, 1, p * ci, ci)
         lin("t_proj.0.weight")
         lin("t_proj.2.weight")
+        if L["klass"]:  # [classes (zero rows up to kpad)][T]: B operand (k = class) of the class-embedding GEMM
+            pk.add("class_emb#kn", P["class_emb.weight"], L["num_classes"], L["T"], L["T"], 1, 1, L["T"], 1, 0, 0,
+                   rows=self.kpad)
         pk.reserve("ada", L["mod_w"], D)
         row = 0
         for k in ada_keys(L, "weight"):
@@ -187,8 +193,9 @@ class DiTEngine:
             K.ld_of(dv) if dv is not None else 0, K._p(pg), x.shape[0], x.shape[1], N, int(x.dtype == torch.float32),
             K._p(dx16), K.ld_of(dx16) if dx16 is not None else 0, K._stream()), "sdmi_ln_mod_bwd")
 
-    def forward(self, x, t, text=None, mask=None, need_backward=True, mask_keep=None):
-        """x: (B, C, H, W) fp32; t: int64 (B,), (1,) or 0-d; text (B, S, ctx); mask (B, cmi, MH, MW) fp32.
+    def forward(self, x, t, text=None, mask=None, need_backward=True, mask_keep=None, klass=None):
+        """x: (B, C, H, W) fp32; t: int64 (B,), (1,) or 0-d; text (B, S, ctx); mask (B, cmi, MH, MW) fp32;
+        klass (B, num_classes) fp32 for class-conditional configs.
         Returns (pred fp32 token-major [B*N, p*p*C], ctx for backward)."""
         L, P = self.L, self.P
         B, Cx, H, W = x.shape
@@ -228,6 +235,18 @@ class DiTEngine:
         e = self._new(B, L["T"])
         _lib.check(_lib.lib().sdmi_time_embedding(t.data_ptr(), 0 if t.numel() == 1 else 1, B, L["T"], e.data_ptr(),
                                                   L["T"], None, K._stream()), "sdmi_time_embedding")
+        cls = None
+        if L["klass"]:
+            if klass is None:
+                raise ValueError("class-conditional model: klass (B, num_classes) is required")
+            kl = plan.as_operand(klass)
+            if tuple(kl.shape) != (B, L["num_classes"]):
+                raise ValueError(f"klass must be (B, {L['num_classes']})")
+            cls = self._new(B, self.kpad)
+            _lib.check(_lib.lib().sdmi_nchw_to_nhwc_bf16(kl.data_ptr(), B, L["num_classes"], 1, cls.data_ptr(),
+                                                         self.kpad, K._stream()), "cast")
+            K.gemm(B, L["T"], self.kpad, cls, _lib.A_ROWMAJOR, self.kpad, self.W("class_emb#kn"), _lib.B_KN, L["T"],
+                   e, L["T"], resid=e, ldr=L["T"])  # e += class @ class_emb.weight
         h1 = self._new(B, D)
         K.linear(e, self.W("t_proj.0.weight"), h1, bias=P["t_proj.0.bias"], act=2)
         r = self._new(B, D)  # ReLU(t_emb): the only form in which t_emb is consumed (adaLN inputs)
@@ -235,7 +254,7 @@ class DiTEngine:
         mod = self._new(B, L["mod_w"])
         ada_b = contiguous_run(P, ada_keys(L, "bias"), (L["mod_w"],))
         K.linear(r, self.W("ada"), mod, bias=ada_b)
-        st.update(e=e, h1=h1, r=r, mod=mod)
+        st.update(e=e, h1=h1, r=r, mod=mod, cls=cls)
         ctx = None
         if L["text"]:
             txt = plan.as_operand(text)
@@ -450,6 +469,11 @@ class DiTEngine:
         K.linear_dgrad(dt, self.W("t_proj.2.weight"), dh1, relu_of=st["h1"])
         K.linear_wgrad(dh1, st["e"], self.g("t_proj.0.weight"))
         K.chan_sum(dh1, 1, B, D, per_c=self.g("t_proj.0.bias"))
+        if st.get("cls") is not None:  # d class_emb.weight = class^T @ d(t_emb), d(t_emb) = dh1 @ W(t_proj.0)
+            de = self._new(B, L["T"])
+            K.linear_dgrad(dh1, self.W("t_proj.0.weight"), de)
+            K.gemm(self.kpad, L["T"], B, st["cls"], _lib.A_COLMAJOR, self.kpad, de, _lib.B_KN, L["T"],
+                   self.g("class_emb.weight"), L["T"], m_store=L["num_classes"])
         # ---- patch embedding (a 2x2 stride-2 conv over the NHWC patch source) ----
         gh, gw = H // p, W // p
         xin = st["xin"]

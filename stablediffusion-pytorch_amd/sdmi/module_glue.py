@@ -48,11 +48,11 @@ class EngineHolder:
 
 class DenoiserFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, holder, x, t, text, mask, *params):
+    def forward(ctx, holder, x, t, text, mask, klass, *params):
         eng = holder.engine
         eng.refresh_weights()
         B, C, H, W = x.shape
-        pred, tape = eng.forward(x, t, text, mask, need_backward=True)
+        pred, tape = eng.forward(x, t, text, mask, need_backward=True, klass=klass)
         out = eng.pred_to_nchw(pred, B, H, W)
         ctx.holder = holder
         ctx.tape = tape
@@ -69,17 +69,17 @@ class DenoiserFunction(torch.autograd.Function):
         eng.backward(ctx.tape, dpred, grads=gviews)
         ctx.tape = None
         names = [k for k, _ in holder.module.named_parameters()]
-        return (None, None, None, None, None) + tuple(gviews[k] for k in names)
+        return (None, None, None, None, None, None) + tuple(gviews[k] for k in names)
 
 
 UNetFunction = DenoiserFunction
 
 
-def run_unet(module, holder, x, t, text=None, mask=None):
+def run_unet(module, holder, x, t, text=None, mask=None, klass=None):
     _require_gpu(x)
     holder.ensure(x.device)
     params = [p for _, p in module.named_parameters()]
-    return DenoiserFunction.apply(holder, x, t, text, mask, *params)
+    return DenoiserFunction.apply(holder, x, t, text, mask, klass, *params)
 
 
 run_denoiser = run_unet

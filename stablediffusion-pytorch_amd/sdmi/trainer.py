@@ -103,26 +103,26 @@ class DDPMTrainer:
         self.reducer.ready(upto)
 
     # ------------------------------------------------------------------------------------------
-    def step(self, x0, noise, t, text=None, mask=None, mask_keep=None):
+    def step(self, x0, noise, t, text=None, mask=None, mask_keep=None, klass=None):
         """One training step on device tensors: x0/noise (B,4,H,W) fp32, t (B,) int64, text (B,S,C) fp32,
         mask (B,18,MH,MW) fp32 (one-hot), mask_keep (B,) fp32 cond-drop multipliers or None.
         With SDMI_MAIN_PRIORITY=1 the step's critical path (forward + data-gradient chain + optimizer) runs on a
         high-priority stream, so the overlapped weight-gradient stream yields to it under contention."""
         if self.main_stream is None:
-            return self._step(x0, noise, t, text, mask, mask_keep)
+            return self._step(x0, noise, t, text, mask, mask_keep, klass)
         caller = torch.cuda.current_stream(self.device)
         plan.wait_stream(self.main_stream, caller)
         with torch.cuda.stream(self.main_stream):
-            r = self._step(x0, noise, t, text, mask, mask_keep)
+            r = self._step(x0, noise, t, text, mask, mask_keep, klass)
         plan.wait_stream(caller, self.main_stream)
         return r
 
-    def _step(self, x0, noise, t, text, mask, mask_keep):
+    def _step(self, x0, noise, t, text, mask, mask_keep, klass=None):
         eng, st = self.engine, self.store
         B, C, H, W = x0.shape
         xt = torch.empty_like(x0)
         K.add_noise(x0, noise, t, self.sqrt_abar, self.sqrt_1m_abar, xt)
-        pred, ctx = eng.forward(xt, t, text, mask, mask_keep=mask_keep)
+        pred, ctx = eng.forward(xt, t, text, mask, mask_keep=mask_keep, klass=klass)
         dpred = eng.new_dpred(B, H, W)
         eng.loss(pred, noise, dpred, self.state[S_LOSS:S_LOSS + 1], gscale_dev=self.state[S_SCALE:S_SCALE + 1])
         if self.reducer is not None and self.base == "dit":

@@ -230,8 +230,9 @@ class UNetEngine:
         self.im_channels = im_channels
         self.device = next(iter(params.values())).device
         L = self.L
-        if L["klass"]:
-            raise NotImplementedError("class conditioning is not wired into the HIP engine yet")
+        # class conditioning (unet_cond_base.py:152-155): t_emb += class @ class_emb.weight, as one GEMM whose K
+        # (the class count) is zero-padded to a multiple of 8
+        self.kpad = (L["num_classes"] + 7) // 8 * 8 if L["klass"] else 0
         self.resnets = resnet_list(L)
         self.temb_off = {}
         off = 0
@@ -276,6 +277,9 @@ class UNetEngine:
         conv(first, ipad=self.cin_pad)
         lin("t_proj.0")
         lin("t_proj.2")
+        if L["klass"]:  # [classes (zero rows up to kpad)][T]: the B operand (k = class) of the class-embedding GEMM
+            pk.add("class_emb#kn", P["class_emb.weight"], L["num_classes"], L["T"], L["T"], 1, 1, L["T"], 1, 0, 0,
+                   rows=self.kpad)
         # concatenated t_emb_layers weight [sum C][T]
         pk.reserve("temb_all", self.temb_total, L["T"])
         for (p, l, cin, cout) in self.resnets:
@@ -360,8 +364,9 @@ class UNetEngine:
     def g(self, key):
         return self.Gd[key] if self.Gd is not None else None
 
-    def forward(self, x, t, text=None, mask=None, need_backward=True, mask_keep=None):
-        """x: (B, C, H, W) fp32; t: int64 (B,), (1,) or 0-d; text: (B, S, ctx) ; mask: (B, cmi, MH, MW) fp32.
+    def forward(self, x, t, text=None, mask=None, need_backward=True, mask_keep=None, klass=None):
+        """x: (B, C, H, W) fp32; t: int64 (B,), (1,) or 0-d; text: (B, S, ctx) ; mask: (B, cmi, MH, MW) fp32;
+        klass: (B, num_classes) fp32 (one-hot, cond-drop already applied) for class-conditional configs.
         Returns (pred NHWC fp32 [B*H*W, 8] with the first im_channels valid, tape)."""
         L, P = self.L, self.P
         B, Cx, H, W = x.shape
@@ -420,6 +425,19 @@ class UNetEngine:
         _lib.check(_lib.lib().sdmi_silu(h1.data_ptr(), None, s1.data_ptr(), B * T, K._stream()), "sdmi_silu")
         temb = self._new(B, T)
         K.linear(s1, self.W("t_proj.2#f"), temb, bias=P["t_proj.2.bias"])
+        cls = None
+        if L["klass"]:
+            if klass is None:
+                raise ValueError("class-conditional model: klass (B, num_classes) is required")
+            kl = plan.as_operand(klass)
+            if tuple(kl.shape) != (B, L["num_classes"]):
+                raise ValueError(f"klass must be (B, {L['num_classes']})")
+            cls = self._new(B, self.kpad)
+            _lib.check(_lib.lib().sdmi_nchw_to_nhwc_bf16(kl.data_ptr(), B, L["num_classes"], 1, cls.data_ptr(),
+                                                         self.kpad, K._stream()), "cast")
+            # temb += class @ class_emb.weight (in-place residual epilogue)
+            K.gemm(B, T, self.kpad, cls, _lib.A_ROWMAJOR, self.kpad, self.W("class_emb#kn"), _lib.B_KN, T, temb, T,
+                   resid=temb, ldr=T)
         stemb = self._new(B, T)
         _lib.check(_lib.lib().sdmi_silu(temb.data_ptr(), None, stemb.data_ptr(), B * T, K._stream()), "sdmi_silu")
         temb_all = self._new(B, self.temb_total)
@@ -427,7 +445,7 @@ class UNetEngine:
         bias_all = self._temb_bias()
         K.linear(stemb, self.W("temb_all"), temb_all, bias=bias_all)
         self.dtemb_all = None
-        tape.append((self._bwd_time, dict(e=e, h1=h1, s1=s1, temb=temb, stemb=stemb, B=B)))
+        tape.append((self._bwd_time, dict(e=e, h1=h1, s1=s1, temb=temb, stemb=stemb, B=B, cls=cls)))
         st["temb_all"] = temb_all
 
         ctx = None
@@ -786,6 +804,9 @@ class UNetEngine:
         dtemb = self._new(B, T)
         lib = _lib.lib()
         _lib.check(lib.sdmi_silu(c["temb"].data_ptr(), dst.data_ptr(), dtemb.data_ptr(), B * T, K._stream()), "silu")
+        if c.get("cls") is not None:  # d class_emb.weight = class^T @ dtemb (A = the bf16 class rows, col-major)
+            K.gemm(self.kpad, T, B, c["cls"], _lib.A_COLMAJOR, self.kpad, dtemb, _lib.B_KN, T,
+                   self.g("class_emb.weight"), T, m_store=L["num_classes"])
         K.linear_wgrad(dtemb, c["s1"], self.g("t_proj.2.weight"))
         K.chan_sum(dtemb, 1, B, T, per_c=self.g("t_proj.2.bias"))
         ds1 = self._new(B, T)

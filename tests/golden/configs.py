@@ -68,3 +68,12 @@ def vqvae_celebhq_config():
 SMALL_VQVAE = {"z_channels": 4, "codebook_size": 512, "down_channels": [32, 64, 64], "mid_channels": [64, 64],
                "down_sample": [True, True], "attn_down": [False, True], "norm_channels": 16, "num_heads": 2,
                "num_down_layers": 1, "num_mid_layers": 1, "num_up_layers": 1}
+
+
+# class conditioning (unet_cond_base.py:152-155, transformer.py:176-181; tools/*class_cond*: MNIST, 10 classes)
+def _class_cond(n=10):
+    return {"condition_types": ["class"], "class_condition_config": {"num_classes": n, "cond_drop_prob": 0.1}}
+
+
+SMALL_CLASS_UNET = dict(SMALL_UNCOND, condition_config=_class_cond())
+SMALL_CLASS_DIT = dict(SMALL_DIT_UNCOND, condition_config=_class_cond())

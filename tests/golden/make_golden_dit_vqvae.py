@@ -2,7 +2,7 @@
 implementation (read-only at /root/reference) in THIS container. Only input/output tensors are
 committed (safetensors); weights regenerate from oracle.sd_oracle.deterministic_state.
 
-Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae] [sampler]
+Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae] [sampler] [class]
 
 The reference DIT zero-initialises adaptive_norm_layer and proj_out (models/transformer.py:147-151,
 transformer_layer.py:70-71), so a freshly built reference model outputs exactly 0; the fixtures load
@@ -201,14 +201,44 @@ def gen_sampler():
     save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, "samplers.safetensors"))
 
 
+def gen_class():
+    """Class-conditional small UNet and DiT (10 classes, soft + one-hot rows): forward, loss, gradients incl.
+    class_emb.weight."""
+    import models.unet_cond_base as ref_cond
+    from tests.golden.configs import SMALL_CLASS_UNET, SMALL_CLASS_DIT
+    from tests.golden.make_golden import make_model
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(2, 4, 32, 32, generator=g)
+    t = torch.randint(0, 1000, (2,), generator=g)
+    klass = torch.zeros(2, 10)
+    klass[0, 3] = 1.0
+    klass[1] = torch.rand(10, generator=g)  # soft row: the einsum takes any weights
+    noise = torch.randn(2, 4, 32, 32, generator=g)
+    for name, build in (("unet_class_small", lambda: make_model(ref_cond, SMALL_CLASS_UNET, seed=5)),
+                        ("dit_class_small", lambda: make_dit(SMALL_CLASS_DIT, seed=6))):
+        model, sd = build()
+        model.train()
+        model.zero_grad()
+        out = model(x, t, cond_input={"class": klass})
+        loss = torch.nn.functional.mse_loss(out, noise)
+        loss.backward()
+        f = {"x": x, "t": t, "class": klass, "noise": noise, "out": out.detach(), "loss": loss.detach().reshape(1)}
+        for k, p in model.named_parameters():
+            if k in ("class_emb.weight", "t_proj.0.weight", "t_proj.2.bias"):
+                f["grad." + k] = p.grad.detach().clone()
+        save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, f"{name}.safetensors"))
+
+
 def main():
-    what = sys.argv[1:] or ["dit", "vqvae", "sampler"]
+    what = sys.argv[1:] or ["dit", "vqvae", "sampler", "class"]
     if "dit" in what:
         gen_dit()
     if "vqvae" in what:
         gen_vqvae()
     if "sampler" in what:
         gen_sampler()
+    if "class" in what:
+        gen_class()
     print("fixtures written to", HERE)
 
 

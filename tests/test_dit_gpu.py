@@ -279,3 +279,19 @@ def test_dit_trainer_two_steps_match_reference():
             dk = (tr.store.view(p, key).reshape(-1)[:8192] - sd0[key].reshape(-1)[:8192])
             dr = f[k] - sd0[key].reshape(-1)[:8192]
             assert cos(dk, dr) >= 0.9, (key, cos(dk, dr))
+
+
+def test_class_conditional_dit_matches_golden():
+    from safetensors.torch import load_file
+    from tests.golden.configs import SMALL_CLASS_DIT
+    f = load_file(os.path.join(G, "dit_class_small.safetensors"))
+    model, _ = make(SMALL_CLASS_DIT, seed=6)
+    out = model(f["x"].cuda(), f["t"].cuda(), {"class": f["class"].cuda()})
+    loss = torch.nn.functional.mse_loss(out, f["noise"].cuda())
+    loss.backward()
+    torch.cuda.synchronize()
+    assert ((out.detach().cpu() - f["out"]) ** 2).mean().item() <= 1e-4
+    assert abs(loss.item() - f["loss"].item()) <= 0.02 * f["loss"].item()
+    p = dict(model.named_parameters())
+    for k in ("class_emb.weight", "t_proj.0.weight"):
+        assert cos(p[k].grad.cpu(), f["grad." + k]) >= 0.99, k

@@ -129,3 +129,23 @@ def test_sampler_steps_bit_exact():
             assert torch.equal(out, f[f"ddim_eta{eta:g}_{t}_{tp}"]), (eta, t, tp)
     for t in (999, 500, 0):
         assert torch.equal(O.ddpm_sampler_step((0.0001, 0.02), 1000, f["x"], f["eps"], f["noise"], t), f[f"ddpm_{t}"])
+
+
+def test_class_conditional_unet_and_dit_forward_and_grads():
+    """Class conditioning (unet_cond_base.py:152-155, transformer.py:176-181) pinned on the reference's own
+    outputs: one-hot and soft class rows, loss and the class_emb.weight gradient."""
+    from oracle import dit_oracle as DO
+    from tests.golden.configs import SMALL_CLASS_UNET, SMALL_CLASS_DIT
+    for name, cfg, shapes, fwd, seed in (
+            ("unet_class_small", SMALL_CLASS_UNET, O.unet_param_shapes(SMALL_CLASS_UNET), O.unet_forward, 5),
+            ("dit_class_small", SMALL_CLASS_DIT, DO.dit_param_shapes(SMALL_CLASS_DIT), DO.dit_forward, 6)):
+        f = fx(name)
+        sd = O.deterministic_state(shapes, seed=seed)
+        leaves = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+        out = fwd(leaves, cfg, f["x"], f["t"], {"class": f["class"]})
+        assert rel(out.detach(), f["out"]) < 1e-5, name
+        loss = torch.nn.functional.mse_loss(out, f["noise"])
+        loss.backward()
+        assert abs(loss.item() - f["loss"].item()) <= 1e-5 * abs(f["loss"].item())
+        for k in ("class_emb.weight", "t_proj.0.weight", "t_proj.2.bias"):
+            assert rel(leaves[k].grad, f["grad." + k]) < 1e-4, (name, k)

@@ -110,3 +110,21 @@ def test_scheduler_add_noise_bit_exact(name, b0, b1):
     s._dev = {}
     xt = s.add_noise(f["x0"].cuda(), f["eps"].cuda(), f["t"].cuda()).cpu()
     assert torch.equal(xt, f["xt"])
+
+
+def test_class_conditional_unet_matches_golden():
+    """Class-conditional UNet (class_emb GEMM into t_emb and its weight gradient) against the reference's
+    outputs (tests/golden/unet_class_small.safetensors)."""
+    from safetensors.torch import load_file
+    from tests.golden.configs import SMALL_CLASS_UNET
+    f = load_file(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "unet_class_small.safetensors"))
+    model, sd = make(SMALL_CLASS_UNET, True, seed=5)
+    out = model(f["x"].cuda(), f["t"].cuda(), {"class": f["class"].cuda()})
+    loss = torch.nn.functional.mse_loss(out, f["noise"].cuda())
+    loss.backward()
+    torch.cuda.synchronize()
+    assert ((out.detach().cpu() - f["out"]) ** 2).mean().item() <= 1e-4
+    assert abs(loss.item() - f["loss"].item()) <= 0.02 * f["loss"].item()
+    p = dict(model.named_parameters())
+    for k in ("class_emb.weight", "t_proj.0.weight"):
+        assert cos(p[k].grad.cpu(), f["grad." + k]) >= 0.99, k
