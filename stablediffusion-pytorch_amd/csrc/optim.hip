@@ -3,6 +3,8 @@
 // (train_ddpm_cond_celebhq_multi_gpu.py:362-378; torch.optim.Adam defaults, EMA decay 0.9999).
 // All control state (step, loss scale, growth tracker, found-inf) lives on the device so a whole
 // training step can be replayed as one hipGraph without host synchronisation.
+#include <cstdlib>
+
 #include "common.h"
 #include "../../include/sdmi.h"
 
@@ -107,8 +109,14 @@ extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm
 extern "C" int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n,
                              const float* state, float lr, float b1, float b2, float eps, float ema_decay,
                              sdmi_stream_t stream) {
+  static long long max_blocks = -1;  // grid cap (SDMI_ADAM_BLOCKS): a narrower grid leaves CUs to concurrent work
+  if (max_blocks < 0) {
+    const char* e = getenv("SDMI_ADAM_BLOCKS");
+    max_blocks = e ? atoll(e) : 8192;
+    if (max_blocks < 1) max_blocks = 8192;
+  }
   long long blocks = (n + NT - 1) / NT;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > max_blocks) blocks = max_blocks;
   hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v, ema,
                      n, state, lr, b1, b2, eps, ema_decay);
   SDMI_CHECK_LAUNCH();

@@ -75,6 +75,24 @@ class FlatStore:
         self.p = {k: self.view(self.params, k) for k in self.order}
         self.g = {k: self.view(self.grads, k) for k in self.order} if with_grads else None
 
+    def forward_chunks(self, n):
+        """~n contiguous ranges [lo, hi) of the flat buffer in FORWARD order (descending offsets: the backward
+        finalises the last layers first, so the flat order is roughly reverse forward order), split at parameter
+        starts; returns (ranges, chunk_of_key)."""
+        starts = sorted(off for off, _ in self.offsets.values())
+        target = max(1, self.numel // n)
+        cuts, hi = [], self.numel
+        for s in reversed(starts):  # walk from the top of the buffer down
+            if hi - s >= target and s > 0:
+                cuts.append((s, hi))
+                hi = s
+        cuts.append((0, hi))
+        ranges = [c for c in cuts if c[1] > c[0]]
+        chunk_of = {}
+        for k, (off, _) in self.offsets.items():
+            chunk_of[k] = next(i for i, (lo, hi) in enumerate(ranges) if lo <= off < hi)
+        return ranges, chunk_of
+
     def view(self, flat, k):
         off, n = self.offsets[k]
         return flat[off:off + n].view(self.shapes[k])

@@ -73,6 +73,16 @@ class DDPMTrainer:
         if self.device.type == "cuda" and os.environ.get("SDMI_MAIN_PRIORITY", "0") == "1":
             lo, hi = torch.cuda.Stream.priority_range()
             self.main_stream = torch.cuda.Stream(device=self.device, priority=hi)
+        # Optimizer + weight packing pipelined against the next step's forward: the flat buffer is cut into
+        # forward-ordered chunks; after the (global) clip, Adam + EMA + packing run chunk by chunk on the engine's
+        # side stream, each chunk ending in an event that the engine waits for only where the forward first reads
+        # one of that chunk's parameters or packed weights (UNet engine; SDMI_OPT_CHUNKS=1 disables it).
+        nchunks = int(os.environ.get("SDMI_OPT_CHUNKS", "6"))
+        self.opt_ranges = None
+        if nchunks > 1 and base != "dit" and getattr(self.engine, "side", None) is not None:
+            self.opt_ranges, key_chunk = self.store.forward_chunks(nchunks)
+            self.engine.set_chunks(key_chunk)
+            self.opt_events = [torch.cuda.Event() for _ in self.opt_ranges]
         self.engine.refresh_weights()
 
     # ------------------------------------------------------------------------------------------
@@ -142,10 +152,25 @@ class DDPMTrainer:
         hp = self.hp
         _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(), ws.data_ptr(),
                                        hp["growth"], 1, float(self.world), K._stream()), "sdmi_clip_unscale")
-        _lib.check(L.sdmi_adam_ema(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
-                                   K._p(self.ema), st.numel, self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"],
-                                   hp["eps"], hp["ema"] if hp["ema"] is not None else 0.0, K._stream()), "sdmi_adam_ema")
-        eng.refresh_weights()
+        ema_decay = hp["ema"] if hp["ema"] is not None else 0.0
+        if self.opt_ranges is None:
+            _lib.check(L.sdmi_adam_ema(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                                       K._p(self.ema), st.numel, self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"],
+                                       hp["eps"], ema_decay, K._stream()), "sdmi_adam_ema")
+            eng.refresh_weights()
+            return self.state
+        side = eng.side
+        plan.wait_stream(side, torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for c, (lo, hi) in enumerate(self.opt_ranges):
+                e = self.ema[lo:hi] if self.ema is not None else None
+                _lib.check(L.sdmi_adam_ema(st.params[lo:hi].data_ptr(), st.grads[lo:hi].data_ptr(),
+                                           self.m[lo:hi].data_ptr(), self.v[lo:hi].data_ptr(), K._p(e), hi - lo,
+                                           self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"], hp["eps"], ema_decay,
+                                           K._stream()), "sdmi_adam_ema")
+                eng.pack.run_chunk(c)
+                plan.record_event(self.opt_events[c], side)
+        eng._pending = {c: ev for c, ev in enumerate(self.opt_events)}
         return self.state
 
     def _on_progress_dit(self, i):
@@ -168,4 +193,12 @@ class DDPMTrainer:
     def ema_state_dict(self):
         if self.ema is None:
             raise RuntimeError("this trainer keeps no EMA copy (ema_decay=None)")
+        self.sync_optimizer()
         return {k: self.store.view(self.ema, k) for k in self.store.order}
+
+    def sync_optimizer(self):
+        """The current stream waits for the chunked optimizer step still in flight (parameters, EMA and packed
+        weights are final for stream-ordered readers afterwards)."""
+        need = getattr(self.engine, "_need_all", None)
+        if need is not None:
+            need()

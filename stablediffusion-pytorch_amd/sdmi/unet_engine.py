@@ -119,11 +119,40 @@ class PackPlan:
         self.total += (rows * width + 63) // 64 * 64
         self.views[name] = (off, rows, width)
 
+    def set_chunks(self, chunk_of_ptr):
+        """Split the packing into per-chunk launches: chunk_of_ptr(data_ptr) -> chunk index of a source parameter.
+        run_chunk(c) then packs only the views whose sources lie in chunk c (derived views after their source);
+        view_chunk[name] is the chunk after which a packed view is complete."""
+        self.chunk_of_ptr = chunk_of_ptr
+        self.finalize()
+
     def finalize(self):
         self.buf = torch.zeros(max(self.total, 64), dtype=torch.bfloat16, device=self.device)
         chunk = _lib.lib().sdmi_pack_chunk()
+        cof = getattr(self, "chunk_of_ptr", None)
+        item_chunk = [cof(it["src"].data_ptr()) if cof else 0 for it in self.items]
+        starts = sorted((off, name) for name, (off, rows, width) in self.views.items())
+        self.view_chunk = {}
+
+        def view_of(dst_off):
+            name = None
+            for off, nm in starts:
+                if off > dst_off:
+                    break
+                name = nm
+            return name
+
+        for j, it in enumerate(self.items):  # a view is complete after the latest chunk of the items writing it
+            nm = view_of(it["dst_off"])
+            self.view_chunk[nm] = max(self.view_chunk.get(nm, 0), item_chunk[j])
+        titem_chunk = []
+        for it in self.titems:  # a derived view is produced right after its source view
+            c = self.view_chunk.get(it["src_view"], 0)
+            titem_chunk.append(c)
+            self.view_chunk[view_of(it["dst_off"])] = c
+        self.nchunks = max(item_chunk + titem_chunk + [0]) + 1
         descs = (_lib.PackDesc * len(self.items))()
-        bmap = []
+        bmaps = [[] for _ in range(self.nchunks)]
         for j, it in enumerate(self.items):
             d = descs[j]
             d.src = it["src"].data_ptr()
@@ -132,14 +161,14 @@ class PackPlan:
             for f in ("O", "I", "Ipad", "KH", "KW", "kh_off", "kh_mul", "kw_off", "kw_mul", "dst_ld"):
                 setattr(d, f, it[f])
             row = it["KH"] * it["KW"] * it["Ipad"]
-            bmap += [(j, o) for o in range(0, it["O"], max(1, chunk // row))]
+            bmaps[item_chunk[j]] += [(j, o) for o in range(0, it["O"], max(1, chunk // row))]
         raw = bytes(descs)
         self.desc_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
-        self.bmap_dev = torch.tensor(bmap, dtype=torch.int32).reshape(-1).to(self.device)
-        self.nblocks = len(bmap)
+        self.bmap_dev = [torch.tensor(b or [(0, 0)], dtype=torch.int32).reshape(-1).to(self.device) for b in bmaps]
+        self.nblocks = [len(b) for b in bmaps]
         self.ptrs = [it["src"].data_ptr() for it in self.items]
         tdescs = (_lib.TPackDesc * max(1, len(self.titems)))()
-        tmap = []
+        tmaps = [[] for _ in range(self.nchunks)]
         for j, it in enumerate(self.titems):
             d = tdescs[j]
             sbase, _, swidth = self.views[it["src_view"]]
@@ -150,21 +179,27 @@ class PackPlan:
             assert swidth % 8 == 0
             for t, v in enumerate(it["smap"]):
                 d.smap[t] = v
-            tmap += [(j, i, o, t) for i in range(0, it["I"], 64) for o in range(0, it["O"], 64)
-                     for t in range(it["taps"])]
+            tmaps[titem_chunk[j]] += [(j, i, o, t) for i in range(0, it["I"], 64) for o in range(0, it["O"], 64)
+                                      for t in range(it["taps"])]
         self.tdesc_dev = torch.frombuffer(bytearray(bytes(tdescs)), dtype=torch.uint8).to(self.device)
-        self.tmap_dev = torch.tensor(tmap or [(0, 0, 0, 0)], dtype=torch.int32).reshape(-1).to(self.device)
-        self.ntiles = len(tmap)
+        self.tmap_dev = [torch.tensor(m or [(0, 0, 0, 0)], dtype=torch.int32).reshape(-1).to(self.device)
+                         for m in tmaps]
+        self.ntiles = [len(m) for m in tmaps]
 
     def view(self, name):
         off, rows, width = self.views[name]
         return self.buf[off:off + rows * width].view(rows, width)
 
     def run(self):
-        _lib.check(_lib.lib().sdmi_pack_weights(self.desc_dev.data_ptr(), self.bmap_dev.data_ptr(), self.nblocks,
+        for c in range(self.nchunks):
+            self.run_chunk(c)
+
+    def run_chunk(self, c):
+        """Pack the views of chunk c (no-op for a chunk without views)."""
+        _lib.check(_lib.lib().sdmi_pack_weights(self.desc_dev.data_ptr(), self.bmap_dev[c].data_ptr(), self.nblocks[c],
                                                 K._stream()), "sdmi_pack_weights")
-        _lib.check(_lib.lib().sdmi_pack_transpose(self.tdesc_dev.data_ptr(), self.tmap_dev.data_ptr(), self.ntiles,
-                                                  K._stream()), "sdmi_pack_transpose")
+        _lib.check(_lib.lib().sdmi_pack_transpose(self.tdesc_dev.data_ptr(), self.tmap_dev[c].data_ptr(),
+                                                  self.ntiles[c], K._stream()), "sdmi_pack_transpose")
 
     def stale(self):
         return any(it["src"].data_ptr() != p for it, p in zip(self.items, self.ptrs))
@@ -225,8 +260,12 @@ class UNetEngine:
         self.cfg = cfg
         self.L = layout(cfg)
         self.base = base or ("cond" if cfg.get("condition_config") else "uncond")
-        self.P = params
+        self.P = _WaitingParams(params, self)
         self.Gd = grads
+        # optimizer / pack pipeline: chunk -> event the current stream still has to wait for before it reads the
+        # chunk's parameters or packed weights (set by the trainer after it issues the chunked optimizer step)
+        self._pending = {}
+        self._key_chunk = {}
         self.im_channels = im_channels
         self.device = next(iter(params.values())).device
         L = self.L
@@ -350,7 +389,24 @@ class UNetEngine:
         self.pack = pk
 
     def W(self, name):
+        if self._pending:
+            self._need(self.pack.view_chunk.get(name, 0))
         return self.pack.view(name)
+
+    def set_chunks(self, key_chunk):
+        """Parameters are updated and repacked in forward-ordered chunks (trainer): key -> chunk index."""
+        self._key_chunk = dict(key_chunk)
+        ptr_chunk = {self.P.raw(k).data_ptr(): c for k, c in key_chunk.items()}
+        self.pack.set_chunks(lambda ptr: ptr_chunk.get(ptr, 0))
+
+    def _need(self, c):
+        ev = self._pending.pop(c, None)
+        if ev is not None:
+            plan.wait_event(torch.cuda.current_stream(self.device), ev)
+
+    def _need_all(self):
+        for c in sorted(self._pending):
+            self._need(c)
 
     def refresh_weights(self):
         if self.pack.stale():
@@ -882,6 +938,7 @@ class UNetEngine:
         self.temb_grad_all = self._temb_grad_view()
         grads = ctx["grads"]
         tape = ctx["tape"]
+        self._need_all()  # the optimizer chunks read the gradient buffers the backward is about to overwrite
         K.PHASE = "bwd"
         for k in range(len(tape) - 1, -1, -1):
             fn, c = tape[k]
@@ -897,6 +954,24 @@ class UNetEngine:
         """The t_emb_layers weight gradients are one contiguous [sum C][T] region of the flat store."""
         return contiguous_run(self.Gd, [f"{p}.t_emb_layers.{l}.1.weight" for (p, l, ci, co) in self.resnets],
                               (self.temb_total, self.L["T"]))
+
+
+class _WaitingParams(dict):
+    """The engine's parameter dict: reading a parameter first makes the current stream wait for the optimizer
+    chunk that updates it (when one is pending)."""
+
+    def __init__(self, params, eng):
+        super().__init__(params)
+        self._eng = eng
+
+    def __getitem__(self, k):
+        eng = self._eng
+        if eng._pending:
+            eng._need(eng._key_chunk.get(k, 0))
+        return dict.__getitem__(self, k)
+
+    def raw(self, k):
+        return dict.__getitem__(self, k)
 
 
 def contiguous_run(tensors, keys, shape):
