@@ -89,29 +89,41 @@ __device__ __forceinline__ void strip_reduce(const StripArgs& a, int b, long lon
 #pragma unroll
     for (int e = 0; e < 8; ++e) tb[e] = r < R ? a.tab[(long long)b * a.C + cc + e] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (r < R) {
-#pragma unroll 2
-    for (long long p = r; p < nrows; p += R) {
-      const long long row = row0 + p;
-      float xv[8], gv[8];
-      if (MODE == 0) {
-        unpack8(*(const uint4*)(a.x + row * a.ldx + cc), xv);
+  if (r < R && nrows > 0) {
+    // rows in batches of RB: the batch's loads are issued together from clamped (valid) rows and masked after, so
+    // each thread keeps RB (x2 in mode 1) 16-byte loads in flight instead of one row per round trip
+    constexpr int RB = MODE == 1 ? 4 : 8;
+    for (long long p0 = r; p0 < nrows; p0 += (long long)RB * R) {
+      uint4 rx[RB], rg[RB];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { u[e] += xv[e]; v[e] = fmaf(xv[e], xv[e], v[e]); }
-      } else if (MODE == 1) {
-        unpack8(*(const uint4*)(a.x + row * a.ldx + cc), xv);
-        unpack8(*(const uint4*)(a.dy + row * a.ldy + cc), gv);
+      for (int q = 0; q < RB; ++q) {
+        const long long row = row0 + min(p0 + (long long)q * R, nrows - 1);
+        if (MODE != 2) rx[q] = *(const uint4*)(a.x + row * a.ldx + cc);
+        if (MODE != 0) rg[q] = *(const uint4*)(a.dy + row * a.ldy + cc);
+      }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float dz = gv[e];
-          if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb[e].x, tb[e].y));
-          u[e] += dz;
-          v[e] = fmaf(dz, (xv[e] - tb[e].z) * tb[e].w, v[e]);
+      for (int q = 0; q < RB; ++q) {
+        if (p0 + (long long)q * R >= nrows) break;
+        float xv[8], gv[8];
+        if (MODE == 0) {
+          unpack8(rx[q], xv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { u[e] += xv[e]; v[e] = fmaf(xv[e], xv[e], v[e]); }
+        } else if (MODE == 1) {
+          unpack8(rx[q], xv);
+          unpack8(rg[q], gv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float dz = gv[e];
+            if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb[e].x, tb[e].y));
+            u[e] += dz;
+            v[e] = fmaf(dz, (xv[e] - tb[e].z) * tb[e].w, v[e]);
+          }
+        } else {
+          unpack8(rg[q], gv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) u[e] += gv[e];
         }
-      } else {
-        unpack8(*(const uint4*)(a.dy + row * a.ldy + cc), gv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) u[e] += gv[e];
       }
     }
   }
@@ -140,11 +152,24 @@ __device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, f
   const int ch = t % cw, bg = t / cw;
   float x1 = 0.f, x2 = 0.f;
   if (bg < nbg && t < nbg * cw) {
-#pragma unroll 4
-    for (int b = bg; b < a.nb; b += nbg) {
-      const float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
-      x1 += ld_coherent(rp);
-      x2 += ld_coherent(rp + 1);
+    // issue 8 rows' coherent loads before summing them: the sum then waits once per batch of loads instead of
+    // once per load (a dependent chain of cross-XCD round trips otherwise)
+    for (int b0 = bg; b0 < a.nb; b0 += 8 * nbg) {
+      float r1[8], r2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = min(b0 + u * nbg, a.nb - 1);
+        const float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
+        r1[u] = ld_coherent(rp);
+        r2[u] = ld_coherent(rp + 1);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (b0 + u * nbg < a.nb) {
+          x1 += r1[u];
+          x2 += r2[u];
+        }
+      }
     }
   }
   acc[t][0] = x1;
@@ -178,10 +203,19 @@ __device__ __forceinline__ bool combine_psplits(const StripArgs& a, int b, int c
   for (int ch = threadIdx.x; ch < cw; ch += NT) {
     float x1 = 0.f, x2 = 0.f;
     const float* pp = a.part + ((long long)b * nz * a.C + c0 + ch) * 2;
-#pragma unroll 4
-    for (int z = 0; z < nz; ++z) {
-      x1 += ld_coherent(pp + (long long)z * a.C * 2);
-      x2 += ld_coherent(pp + (long long)z * a.C * 2 + 1);
+    float r1[PS_MAX], r2[PS_MAX];  // all splits' loads in flight before the (fixed-order) sum
+#pragma unroll
+    for (int z = 0; z < PS_MAX; ++z) {
+      const int zz = min(z, nz - 1);
+      r1[z] = ld_coherent(pp + (long long)zz * a.C * 2);
+      r2[z] = ld_coherent(pp + (long long)zz * a.C * 2 + 1);
+    }
+#pragma unroll
+    for (int z = 0; z < PS_MAX; ++z) {
+      if (z < nz) {
+        x1 += r1[z];
+        x2 += r2[z];
+      }
     }
     s1[ch] = x1;
     s2[ch] = x2;
@@ -355,11 +389,18 @@ __global__ __launch_bounds__(NT) void gn_fwd_small_kernel(StripArgs a, bf16_t* y
 #pragma unroll
   for (int e = 0; e < 8; ++e) { u[e] = 0.f; v[e] = 0.f; }
   const bf16_t* X = a.x + (long long)b * a.P * a.ldx + cc;
+  // every row load issued first from a clamped (valid) row, masked afterwards: a guarded load per row would make
+  // the compiler wait for each one before the next
+  uint4 rx[SMALL_IT];
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
-    const int p = r + it * R;
-    if (act && p < a.P) {
-      unpack8(*(const uint4*)(X + (long long)p * a.ldx), xv[it]);
+    const int p = min(min(r, R - 1) + it * R, a.P - 1);
+    rx[it] = *(const uint4*)(X + (long long)p * a.ldx);
+  }
+#pragma unroll
+  for (int it = 0; it < SMALL_IT; ++it) {
+    unpack8(rx[it], xv[it]);
+    if (act && r + it * R < a.P) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { u[e] += xv[it][e]; v[e] = fmaf(xv[it][e], xv[it][e], v[e]); }
     }
@@ -425,12 +466,18 @@ __global__ __launch_bounds__(NT) void gn_bwd_small_kernel(StripArgs a, bf16_t* d
     tb[e] = act ? a.tab[(long long)b * a.C + cc + e] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const long long rb = (long long)b * a.P;
+  uint4 rx[SMALL_IT], rg[SMALL_IT];  // all row loads in flight first (see gn_fwd_small_kernel)
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
-    const int p = r + it * R;
-    if (act && p < a.P) {
-      unpack8(*(const uint4*)(a.x + (rb + p) * a.ldx + cc), xv[it]);
-      unpack8(*(const uint4*)(a.dy + (rb + p) * a.ldy + cc), dz[it]);
+    const int p = min(min(r, R - 1) + it * R, a.P - 1);
+    rx[it] = *(const uint4*)(a.x + (rb + p) * a.ldx + cc);
+    rg[it] = *(const uint4*)(a.dy + (rb + p) * a.ldy + cc);
+  }
+#pragma unroll
+  for (int it = 0; it < SMALL_IT; ++it) {
+    unpack8(rx[it], xv[it]);
+    unpack8(rg[it], dz[it]);
+    if (act && r + it * R < a.P) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         if (a.silu) dz[it][e] *= silu_grad_f(fmaf(xv[it][e], tb[e].x, tb[e].y));
