@@ -151,7 +151,7 @@ __device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, f
   const int nbg = max(1, NT / cw);
   const int ch = t % cw, bg = t / cw;
   float x1 = 0.f, x2 = 0.f;
-  if (bg < nbg && t < nbg * cw) {
+  if (t < NT && bg < nbg && t < nbg * cw) {
     // issue 8 rows' coherent loads before summing them: the sum then waits once per batch of loads instead of
     // once per load (a dependent chain of cross-XCD round trips otherwise)
     for (int b0 = bg; b0 < a.nb; b0 += 8 * nbg) {
@@ -172,8 +172,10 @@ __device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, f
       }
     }
   }
-  acc[t][0] = x1;
-  acc[t][1] = x2;
+  if (t < NT) {
+    acc[t][0] = x1;
+    acc[t][1] = x2;
+  }
   __syncthreads();
   if (t < cw) {
     float y1 = 0.f, y2 = 0.f;
@@ -336,33 +338,42 @@ __global__ __launch_bounds__(NT) void chan_sum_kernel(StripArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Single-pass GroupNorm for small images (P <= SMALL_IT * rows per iteration, i.e. the 16x16 and smaller
-// levels): one workgroup owns a (batch row, channel strip of whole groups), keeps its P x strip slab in
-// registers, reduces, and applies -- one launch and one read of x (and dy) instead of a statistics pass, a
-// cross-workgroup combine and a second elementwise pass.
+// Single-pass GroupNorm: one workgroup (NTH = 256 or 1024 threads) owns a (batch row, channel strip of whole
+// groups), keeps its P x strip slab in registers as packed bf16 (SMALL_IT rows per thread), reduces, and applies
+// -- one launch and one read of x (and dy) instead of a statistics pass, a cross-workgroup combine and a second
+// elementwise pass. 256 threads cover P <= 256 (16x16 and smaller levels), 1024 threads P <= 1024 (32x32).
 // ---------------------------------------------------------------------------------------------
-constexpr int SMALL_IT = 10;  // pixel rows per thread: P <= 10 * (256 / (strip/8)), >= 256 for 64/72-wide strips
+constexpr int SMALL_IT = 10;  // pixel rows per thread: P <= 10 * (NTH / (strip/8))
 
-__host__ __device__ __forceinline__ int small_rows(int cw) { return NT / (cw >> 3); }
+__host__ __device__ __forceinline__ int small_rows(int cw, int nth = NT) { return nth / (cw >> 3); }
 
-// host: single-pass kernels enabled (SDMI_GN_SMALL=0 disables them for A/B runs)
-bool gn_small_enabled() {
-  static int on = -1;
-  if (on < 0) {
+// host: single-pass kernels enabled (SDMI_GN_SMALL=0 disables them for A/B runs; =1 keeps only the 256-thread one)
+int gn_small_mode() {
+  static int mode = -1;
+  if (mode < 0) {
     const char* e = getenv("SDMI_GN_SMALL");
-    on = e ? atoi(e) != 0 : 1;
+    mode = e ? atoi(e) : 2;
   }
-  return on != 0;
+  return mode;
 }
 
-// per-channel sums of u (and v) over the workgroup's rows -> s1/s2[cw] in LDS (red: [NT][17] scratch)
+// threads per workgroup of the single-pass kernels for a P x cw slab, or 0 (multi-pass path)
+int gn_pass_threads(int P, int cw) {
+  const int mode = gn_small_mode();
+  if (mode >= 1 && cw <= NT && P <= SMALL_IT * small_rows(cw, 256)) return 256;
+  if (mode >= 2 && cw <= NT && P <= SMALL_IT * small_rows(cw, 1024)) return 1024;
+  return 0;
+}
+
+// per-channel sums of u (and v) over the workgroup's rows -> s1/s2[cw] in LDS (red: [NTH][17] scratch)
+template <int NTH>
 __device__ __forceinline__ void small_reduce(const float* u, const float* v, int cw, float (*red)[17], float* s1,
                                              float* s2) {
-  const int t = threadIdx.x, L = cw >> 3, R = NT / L;
+  const int t = threadIdx.x, L = cw >> 3, R = NTH / L;
 #pragma unroll
   for (int e = 0; e < 8; ++e) { red[t][e] = u[e]; red[t][8 + e] = v[e]; }
   __syncthreads();
-  for (int ch = t; ch < cw; ch += NT) {
+  for (int ch = t; ch < cw; ch += NTH) {
     const int l = ch >> 3, e = ch & 7;
     float x1 = 0.f, x2 = 0.f;
     for (int rr = 0; rr < R; ++rr) {
@@ -376,15 +387,15 @@ __device__ __forceinline__ void small_reduce(const float* u, const float* v, int
 }
 
 // grid (nchunks, B): y = act(GroupNorm(x)), and the forward table for the backward pass
-__global__ __launch_bounds__(NT) void gn_fwd_small_kernel(StripArgs a, bf16_t* y, int ldy) {
-  __shared__ float red[NT][17];
+template <int NTH>
+__global__ __launch_bounds__(NTH) void gn_fwd_pass_kernel(StripArgs a, bf16_t* y, int ldy) {
+  __shared__ float red[NTH][17];
   __shared__ float s1[NT], s2[NT];
   __shared__ float2 grp[NT];
   const int b = blockIdx.y, c0 = blockIdx.x * a.CW, cw = min(a.CW, a.C - c0);
-  const int L = cw >> 3, R = NT / L, t = threadIdx.x, lane = t % L, r = t / L;
+  const int L = cw >> 3, R = NTH / L, t = threadIdx.x, lane = t % L, r = t / L;
   const int cc = c0 + lane * 8, Cg = a.C / a.G;
   const bool act = r < R;
-  float xv[SMALL_IT][8];
   float u[8], v[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { u[e] = 0.f; v[e] = 0.f; }
@@ -399,13 +410,14 @@ __global__ __launch_bounds__(NT) void gn_fwd_small_kernel(StripArgs a, bf16_t* y
   }
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
-    unpack8(rx[it], xv[it]);
+    float xv[8];
+    unpack8(rx[it], xv);
     if (act && r + it * R < a.P) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { u[e] += xv[it][e]; v[e] = fmaf(xv[it][e], xv[it][e], v[e]); }
+      for (int e = 0; e < 8; ++e) { u[e] += xv[e]; v[e] = fmaf(xv[e], xv[e], v[e]); }
     }
   }
-  small_reduce(u, v, cw, red, s1, s2);
+  small_reduce<NTH>(u, v, cw, red, s1, s2);
   const int ng = cw / Cg;
   if (t < ng) {
     double m1 = 0, m2 = 0;
@@ -416,7 +428,7 @@ __global__ __launch_bounds__(NT) void gn_fwd_small_kernel(StripArgs a, bf16_t* y
     grp[t] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)a.eps)));
   }
   __syncthreads();
-  for (int ch = t; ch < cw; ch += NT) {
+  for (int ch = t; ch < cw; ch += NTH) {
     const int c = c0 + ch;
     const float2 mr = grp[ch / Cg];
     const float sc = mr.y * a.gamma[c];
@@ -435,10 +447,11 @@ __global__ __launch_bounds__(NT) void gn_fwd_small_kernel(StripArgs a, bf16_t* y
   for (int it = 0; it < SMALL_IT; ++it) {
     const int p = r + it * R;
     if (p < a.P) {
-      float o[8];
+      float xv[8], o[8];
+      unpack8(rx[it], xv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float z = fmaf(xv[it][e], ta[e], ts[e]);
+        const float z = fmaf(xv[e], ta[e], ts[e]);
         o[e] = a.silu ? silu_f(z) : z;
       }
       *(uint4*)(Y + (long long)p * ldy) = pack8(o);
@@ -446,47 +459,50 @@ __global__ __launch_bounds__(NT) void gn_fwd_small_kernel(StripArgs a, bf16_t* y
   }
 }
 
-// grid (nchunks, B): GroupNorm (+SiLU) backward in one pass; dgamma/dbeta by the batch tail
-__global__ __launch_bounds__(NT) void gn_bwd_small_kernel(StripArgs a, bf16_t* dx, int lddx, const bf16_t* add,
+// grid (nchunks, B): GroupNorm (+SiLU) backward in one pass; dgamma/dbeta by the batch tail. x (and, for the
+// 256-thread form, dy) stay packed in registers; the 1024-thread form re-reads dy in the apply pass (an L2 hit:
+// the workgroup read it moments before) to stay within 128 VGPRs; dz = dy * SiLU'(...) is recomputed there.
+template <int NTH>
+__global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* dx, int lddx, const bf16_t* add,
                                                           int ldadd) {
-  __shared__ float red[NT][17];
+  __shared__ float red[NTH][17];
   __shared__ float s1[NT], s2[NT];
   __shared__ float2 grp[NT];
+  __shared__ float4 stb[NT];  // forward table of the strip
   const int b = blockIdx.y, c0 = blockIdx.x * a.CW, cw = min(a.CW, a.C - c0);
-  const int L = cw >> 3, R = NT / L, t = threadIdx.x, lane = t % L, r = t / L;
+  const int L = cw >> 3, R = NTH / L, t = threadIdx.x, lane = t % L, r = t / L;
   const int cc = c0 + lane * 8, Cg = a.C / a.G;
   const bool act = r < R;
-  float xv[SMALL_IT][8], dz[SMALL_IT][8];
-  float u[8], v[8];
-  float4 tb[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    u[e] = 0.f;
-    v[e] = 0.f;
-    tb[e] = act ? a.tab[(long long)b * a.C + cc + e] : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
   const long long rb = (long long)b * a.P;
-  uint4 rx[SMALL_IT], rg[SMALL_IT];  // all row loads in flight first (see gn_fwd_small_kernel)
+  uint4 rx[SMALL_IT], rg[SMALL_IT];  // all row loads in flight first
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
     const int p = min(min(r, R - 1) + it * R, a.P - 1);
     rx[it] = *(const uint4*)(a.x + (rb + p) * a.ldx + cc);
     rg[it] = *(const uint4*)(a.dy + (rb + p) * a.ldy + cc);
   }
+  for (int ch = t; ch < cw; ch += NTH) stb[ch] = a.tab[(long long)b * a.C + c0 + ch];
+  __syncthreads();
+  float u[8], v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { u[e] = 0.f; v[e] = 0.f; }
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
-    unpack8(rx[it], xv[it]);
-    unpack8(rg[it], dz[it]);
+    float xv[8], gv[8];
+    unpack8(rx[it], xv);
+    unpack8(rg[it], gv);
     if (act && r + it * R < a.P) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        if (a.silu) dz[it][e] *= silu_grad_f(fmaf(xv[it][e], tb[e].x, tb[e].y));
-        u[e] += dz[it][e];
-        v[e] = fmaf(dz[it][e], (xv[it][e] - tb[e].z) * tb[e].w, v[e]);
+        const float4 tb = stb[lane * 8 + e];
+        float dz = gv[e];
+        if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb.x, tb.y));
+        u[e] += dz;
+        v[e] = fmaf(dz, (xv[e] - tb.z) * tb.w, v[e]);
       }
     }
   }
-  small_reduce(u, v, cw, red, s1, s2);
+  small_reduce<NTH>(u, v, cw, red, s1, s2);
   const int ng = cw / Cg;
   const float inv_n = 1.0f / ((float)a.P * Cg);
   if (t < ng) {
@@ -495,12 +511,12 @@ __global__ __launch_bounds__(NT) void gn_bwd_small_kernel(StripArgs a, bf16_t* d
       A += a.gamma[c0 + ch] * s1[ch];
       Bc += a.gamma[c0 + ch] * s2[ch];
     }
-    const float4 tt = a.tab[(long long)b * a.C + c0 + t * Cg];
+    const float4 tt = stb[t * Cg];
     const float rs = tt.w, mu = tt.z;
     grp[t] = make_float2(-rs * rs * Bc * inv_n, rs * rs * mu * Bc * inv_n - rs * A * inv_n);
   }
   if (a.sum1) {
-    for (int ch = t; ch < cw; ch += NT) {
+    for (int ch = t; ch < cw; ch += NTH) {
       float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
       st_coherent(rp, s1[ch]);
       st_coherent(rp + 1, s2[ch]);
@@ -508,18 +524,14 @@ __global__ __launch_bounds__(NT) void gn_bwd_small_kernel(StripArgs a, bf16_t* d
   }
   __syncthreads();
   if (act) {
-    float q[8], o[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float2 qo = grp[(lane * 8 + e) / Cg];
-      q[e] = qo.x;
-      o[e] = qo.y;
-    }
 #pragma unroll
     for (int it = 0; it < SMALL_IT; ++it) {
       const int p = r + it * R;
       if (p < a.P) {
-        float av[8], ov[8];
+        float xv[8], gv[8], av[8], ov[8];
+        unpack8(rx[it], xv);
+        if (NTH == 256) unpack8(rg[it], gv);
+        else unpack8(*(const uint4*)(a.dy + (rb + p) * a.ldy + cc), gv);
         if (add) {
           unpack8(*(const uint4*)(add + (rb + p) * ldadd + cc), av);
         } else {
@@ -527,7 +539,13 @@ __global__ __launch_bounds__(NT) void gn_bwd_small_kernel(StripArgs a, bf16_t* d
           for (int e = 0; e < 8; ++e) av[e] = 0.f;
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ov[e] = av[e] + fmaf(tb[e].x, dz[it][e], fmaf(q[e], xv[it][e], o[e]));
+        for (int e = 0; e < 8; ++e) {
+          const float4 tb = stb[lane * 8 + e];
+          const float2 qo = grp[(lane * 8 + e) / Cg];
+          float dz = gv[e];
+          if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb.x, tb.y));
+          ov[e] = av[e] + fmaf(tb.x, dz, fmaf(qo.x, xv[e], qo.y));
+        }
         *(uint4*)(dx + (rb + p) * lddx + cc) = pack8(ov);
       }
     }
@@ -697,12 +715,16 @@ extern "C" int sdmi_gn_fwd(const void* x, int ldx, void* y, int ldy, int B, int 
                            const float* gamma, const float* beta, int silu, float* ws, float* table, sdmi_stream_t stream) {
   if (C % 8 || G <= 0 || C % G) return -1;
   const int cw = strip_width(C, C / G);
-  if (cw <= NT && P <= SMALL_IT * small_rows(cw) && gn_small_enabled()) {
+  const int nth = gn_pass_threads(P, cw);
+  if (nth) {
     StripArgs a = {};
     a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.eps = eps; a.silu = silu;
     a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table; a.CW = cw;
-    hipLaunchKernelGGL(gn_fwd_small_kernel, dim3((C + cw - 1) / cw, B), dim3(NT), 0, (hipStream_t)stream, a, (bf16_t*)y,
-                       ldy);
+    const dim3 grid((C + cw - 1) / cw, B);
+    if (nth == 256)
+      hipLaunchKernelGGL(gn_fwd_pass_kernel<256>, grid, dim3(256), 0, (hipStream_t)stream, a, (bf16_t*)y, ldy);
+    else
+      hipLaunchKernelGGL(gn_fwd_pass_kernel<1024>, grid, dim3(1024), 0, (hipStream_t)stream, a, (bf16_t*)y, ldy);
     SDMI_CHECK_LAUNCH();
     return 0;
   }
@@ -736,10 +758,14 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   const int nch = (C + r.CW - 1) / r.CW;
   if (r.CW > NT || nch > BATCH_CTR) return -2;
   r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
-  if (P <= SMALL_IT * small_rows(r.CW) && gn_small_enabled()) {  // single pass
+  if (const int nth = gn_pass_threads(P, r.CW)) {  // single pass
     if (dgamma && !(r.ctr = counter_slot())) return -4;
-    hipLaunchKernelGGL(gn_bwd_small_kernel, dim3(nch, B), dim3(NT), 0, s, r, (bf16_t*)dx, lddx, (const bf16_t*)addend,
-                       ldadd);
+    if (nth == 256)
+      hipLaunchKernelGGL(gn_bwd_pass_kernel<256>, dim3(nch, B), dim3(256), 0, s, r, (bf16_t*)dx, lddx,
+                         (const bf16_t*)addend, ldadd);
+    else
+      hipLaunchKernelGGL(gn_bwd_pass_kernel<1024>, dim3(nch, B), dim3(1024), 0, s, r, (bf16_t*)dx, lddx,
+                         (const bf16_t*)addend, ldadd);
     SDMI_CHECK_LAUNCH();
     return 0;
   }
