@@ -13,6 +13,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "stablediffusion-pytorch_amd"), REPO]
+os.environ["SDMI_WG_STREAM"] = "0"  # single stream (no side-stream optimizer chunks) for isolated timing
 import torch  # noqa: E402
 
 import bench  # noqa: E402
@@ -68,7 +69,6 @@ def main():
     step = lambda: tr.step(x0, noise, t, text, mask, mask_keep=keep)  # noqa: E731
     for _ in range(2):
         step()
-    tr.engine.side = None if hasattr(tr.engine, "side") else None  # single stream for isolated timing
     plan = StepPlan(step, dev)
     L = _lib.lib()
     ws = torch.empty(1 << 28, dtype=torch.float32, device=dev)  # 1 GiB split-K slabs

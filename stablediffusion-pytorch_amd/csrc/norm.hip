@@ -339,11 +339,13 @@ __global__ __launch_bounds__(NT) void chan_sum_kernel(StripArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // Single-pass GroupNorm: one workgroup (NTH = 256 or 1024 threads) owns a (batch row, channel strip of whole
-// groups), keeps its P x strip slab in registers as packed bf16 (SMALL_IT rows per thread), reduces, and applies
+// groups), keeps its P x strip slab in registers as packed bf16 (small_it(NTH) rows per thread), reduces, and applies
 // -- one launch and one read of x (and dy) instead of a statistics pass, a cross-workgroup combine and a second
 // elementwise pass. 256 threads cover P <= 256 (16x16 and smaller levels), 1024 threads P <= 1024 (32x32).
 // ---------------------------------------------------------------------------------------------
-constexpr int SMALL_IT = 10;  // pixel rows per thread: P <= 10 * (NTH / (strip/8))
+// pixel rows per thread: P <= small_it(NTH) * (NTH / (strip/8)); 8 for the 1024-thread form keeps its x and dy
+// slabs (64 VGPRs) within the 128 VGPRs a 16-wave workgroup allows (32x32 levels with 64-channel strips)
+__host__ __device__ constexpr int small_it(int nth) { return nth == 1024 ? 8 : 10; }
 
 __host__ __device__ __forceinline__ int small_rows(int cw, int nth = NT) { return nth / (cw >> 3); }
 
@@ -360,8 +362,8 @@ int gn_small_mode() {
 // threads per workgroup of the single-pass kernels for a P x cw slab, or 0 (multi-pass path)
 int gn_pass_threads(int P, int cw) {
   const int mode = gn_small_mode();
-  if (mode >= 1 && cw <= NT && P <= SMALL_IT * small_rows(cw, 256)) return 256;
-  if (mode >= 2 && cw <= NT && P <= SMALL_IT * small_rows(cw, 1024)) return 1024;
+  if (mode >= 1 && cw <= NT && P <= small_it(256) * small_rows(cw, 256)) return 256;
+  if (mode >= 2 && cw <= NT && P <= small_it(1024) * small_rows(cw, 1024)) return 1024;
   return 0;
 }
 
@@ -402,6 +404,7 @@ __global__ __launch_bounds__(NTH) void gn_fwd_pass_kernel(StripArgs a, bf16_t* y
   const bf16_t* X = a.x + (long long)b * a.P * a.ldx + cc;
   // every row load issued first from a clamped (valid) row, masked afterwards: a guarded load per row would make
   // the compiler wait for each one before the next
+  constexpr int SMALL_IT = small_it(NTH);
   uint4 rx[SMALL_IT];
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
@@ -474,6 +477,7 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
   const int cc = c0 + lane * 8, Cg = a.C / a.G;
   const bool act = r < R;
   const long long rb = (long long)b * a.P;
+  constexpr int SMALL_IT = small_it(NTH);
   uint4 rx[SMALL_IT], rg[SMALL_IT];  // all row loads in flight first
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {

@@ -13,6 +13,8 @@ HIP kernels of libsdmi.so, planned for MI355X:
   * self attention (9 heads x 32) and the optional text cross attention use the fused flash kernels.
 Parameters are referenced by the reference's state-dict keys; gradients go to caller-owned fp32 views.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -100,6 +102,7 @@ class DiTEngine:
         self.device = next(iter(params.values())).device
         self.cpad = (L["patch_in"] + 7) // 8 * 8
         self._pos = {}
+        self.dgrad_t = os.environ.get("SDMI_DGRAD_T", "1") != "0"  # linear data gradients from transposed packs
         self._build_pack()
 
     # ------------------------------------------------------------------------------------------
@@ -108,10 +111,12 @@ class DiTEngine:
         D, p = L["D"], L["p"]
         pk = PackPlan(self.device)
 
-        def lin(key, name=None):
+        def lin(key, name=None, t=False):
             w = P[key]
             N, Kd = w.shape
             pk.add(name or key, w, N, Kd, Kd, 1, 1, Kd, 1, 0, 0)
+            if t and self.dgrad_t:  # [Kd][N] for the data gradient (B_NK GEMM)
+                pk.add_transpose((name or key) + "#t", name or key, N, Kd, 1, [0], 8)
 
         # patch embedding Linear (D, (ph pw c)) as a 2x2 stride-2 conv weight [D][ph][pw][cpad]
         w = P["patch_embed_layer.patch_embed.0.weight"]
@@ -130,21 +135,30 @@ class DiTEngine:
             row += wk.shape[0]
         for i in range(L["n_layers"]):
             q = f"transformer_layers.{i}."
-            lin(q + "attn_block.qkv_proj.weight")
-            lin(q + "attn_block.output_proj.0.weight")
-            lin(q + "mlp_block.0.weight")
-            lin(q + "mlp_block.2.weight")
+            lin(q + "attn_block.qkv_proj.weight", t=True)
+            lin(q + "attn_block.output_proj.0.weight", t=True)
+            lin(q + "mlp_block.0.weight", t=True)
+            lin(q + "mlp_block.2.weight", t=True)
             if L["text"]:
-                lin(q + "cross_attn_block.q_proj.weight")
-                lin(q + "cross_attn_block.out_proj.weight")
+                lin(q + "cross_attn_block.q_proj.weight", t=True)
+                lin(q + "cross_attn_block.out_proj.weight", t=True)
                 lin(q + "context_proj.weight")
                 pk.reserve(q + "kv", 2 * D, D)
                 pk.add(None, P[q + "cross_attn_block.k_proj.weight"], D, D, D, 1, 1, D, 1, 0, 0, into=q + "kv")
                 pk.add(None, P[q + "cross_attn_block.v_proj.weight"], D, D, D, 1, 1, D, 1, 0, 0, into=q + "kv",
                        row0=D)
+                if self.dgrad_t:
+                    pk.add_transpose(q + "kv#t", q + "kv", 2 * D, D, 1, [0], 8)
         lin("proj_out.weight")
         pk.finalize()
         self.pack = pk
+
+    def _dgrad(self, dy, key, out, **kw):
+        """Data gradient of the packed linear `key` ([N][K]): from its transposed copy key#t when packed."""
+        if self.dgrad_t:
+            K.linear_dgrad_t(dy, self.W(key + "#t"), out, **kw)
+        else:
+            K.linear_dgrad(dy, self.W(key), out, **kw)
 
     def kv_bias(self, i):
         """k_proj.bias | v_proj.bias of layer i: adjacent in the flat store (dit_flat_order)."""
@@ -397,11 +411,11 @@ class DiTEngine:
             K.linear_wgrad(dv2, c["h"], self.g(q + "mlp_block.2.weight"))
             K.chan_sum(dv2, 1, M, D, per_c=self.g(q + "mlp_block.2.bias"))
             dh = self._new(M, 4 * D)
-            K.linear_dgrad(dv2, self.W(q + "mlp_block.2.weight"), dh, relu_of=c["h"])
+            self._dgrad(dv2, q + "mlp_block.2.weight", dh, relu_of=c["h"])
             K.linear_wgrad(dh, c["y2"], self.g(q + "mlp_block.0.weight"))
             K.chan_sum(dh, 1, M, 4 * D, per_c=self.g(q + "mlp_block.0.bias"))
             dy2 = self._new(M, D)
-            K.linear_dgrad(dh, self.W(q + "mlp_block.0.weight"), dy2)
+            self._dgrad(dh, q + "mlp_block.0.weight", dy2)
             dv1 = self._new(M, D)
             if L["text"]:
                 # x2 = xc + cross(LN(xc)) ; y2 = LNmod(x2)
@@ -412,7 +426,7 @@ class DiTEngine:
                 K.linear_wgrad(dvc, c["co"], self.g(q + "cross_attn_block.out_proj.weight"))
                 K.chan_sum(dvc, 1, M, D, per_c=self.g(q + "cross_attn_block.out_proj.bias"))
                 dco = self._new(M, D)
-                K.linear_dgrad(dvc, self.W(q + "cross_attn_block.out_proj.weight"), dco)
+                self._dgrad(dvc, q + "cross_attn_block.out_proj.weight", dco)
                 dcq, dckv = self._new(M, D), self._new(B * S, 2 * D)
                 K.attn_bwd(c["cq"], c["ckv"][:, :D], c["ckv"][:, D:], c["co"], dco, c["clse"], dcq, dckv[:, :D],
                            dckv[:, D:], B, Hh, N, S, D // Hh)
@@ -423,11 +437,11 @@ class DiTEngine:
                 K.linear_wgrad(dckv[:, D:], c["cp"], self.g(q + "cross_attn_block.v_proj.weight"))
                 K.chan_sum(dckv[:, D:], 1, B * S, D, per_c=self.g(q + "cross_attn_block.v_proj.bias"))
                 dcp = self._new(B * S, D)
-                K.linear_dgrad(dckv, self.W(q + "kv"), dcp)
+                self._dgrad(dckv, q + "kv", dcp)
                 K.linear_wgrad(dcp, st["ctx"], self.g(q + "context_proj.weight"))
                 K.chan_sum(dcp, 1, B * S, D, per_c=self.g(q + "context_proj.bias"))
                 dyc = self._new(M, D)
-                K.linear_dgrad(dcq, self.W(q + "cross_attn_block.q_proj.weight"), dyc)
+                self._dgrad(dcq, q + "cross_attn_block.q_proj.weight", dyc)
                 self._ln_bwd(c["xc"], c["mc"], c["rc"], dyc, dxs, dres=dxs, gate=mcol(mod, i, 2), v=c["v1"], dv=dv1,
                              pg=mcol(ws, i, 2), N=N)
             else:
@@ -437,7 +451,7 @@ class DiTEngine:
             K.linear_wgrad(dv1, c["o"], self.g(q + "attn_block.output_proj.0.weight"))
             K.chan_sum(dv1, 1, M, D, per_c=self.g(q + "attn_block.output_proj.0.bias"))
             do = self._new(M, A)
-            K.linear_dgrad(dv1, self.W(q + "attn_block.output_proj.0.weight"), do)
+            self._dgrad(dv1, q + "attn_block.output_proj.0.weight", do)
             qkv = c["qkv"]
             dqkv = self._new(M, 3 * A)
             K.attn_bwd(qkv[:, :A], qkv[:, A:2 * A], qkv[:, 2 * A:], c["o"], do, c["lse"], dqkv[:, :A],
@@ -445,7 +459,7 @@ class DiTEngine:
             K.linear_wgrad(dqkv, c["y1"], self.g(q + "attn_block.qkv_proj.weight"))
             K.chan_sum(dqkv, 1, M, 3 * A, per_c=self.g(q + "attn_block.qkv_proj.bias"))
             dy1 = self._new(M, D)
-            K.linear_dgrad(dqkv, self.W(q + "attn_block.qkv_proj.weight"), dy1)
+            self._dgrad(dqkv, q + "attn_block.qkv_proj.weight", dy1)
             prev = st["layers"][i - 1] if i > 0 else None
             dv2 = self._new(M, D) if prev is not None else None
             dtok = self._new(M, D) if prev is None else None  # bf16 d(tokens): patch-embedding GEMM operand

@@ -224,6 +224,15 @@ def linear_dgrad(dy, w, out, *, resid=None, relu_of=None):
                 ldr=ld_of(resid) if resid is not None else 0, act=3 if relu_of is not None else 0, aux=relu_of)
 
 
+def linear_dgrad_t(dy, wt, out, *, resid=None, relu_of=None):
+    """linear_dgrad from the transposed weight: out[m][k] = sum_n dy[m][n] wt[k][n] (+ resid, ReLU mask as
+    linear_dgrad); wt [K,N] bf16 rows (B_NK), which takes the wider N tiles of the forward GEMM."""
+    M, N = dy.shape
+    K = wt.shape[0]
+    return gemm(M, K, N, dy, _lib.A_ROWMAJOR, ld_of(dy), wt, _lib.B_NK, ld_of(wt), out, ld_of(out), resid=resid,
+                ldr=ld_of(resid) if resid is not None else 0, act=3 if relu_of is not None else 0, aux=relu_of)
+
+
 def linear_wgrad(dy, x, out):
     """out[n][k] = sum_m dy[m][n] x[m][k]  (fp32 weight gradient, out [N,K] contiguous rows)."""
     M, N = dy.shape

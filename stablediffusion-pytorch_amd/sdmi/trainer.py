@@ -83,6 +83,7 @@ class DDPMTrainer:
             self.opt_ranges, key_chunk = self.store.forward_chunks(nchunks)
             self.engine.set_chunks(key_chunk)
             self.opt_events = [torch.cuda.Event() for _ in self.opt_ranges]
+            self.late_event = torch.cuda.Event()
         self.engine.refresh_weights()
 
     # ------------------------------------------------------------------------------------------
@@ -170,7 +171,13 @@ class DDPMTrainer:
                                            K._stream()), "sdmi_adam_ema")
                 eng.pack.run_chunk(c)
                 plan.record_event(self.opt_events[c], side)
+            late = eng.pack.late_chunk
+            if late is not None:  # backward-only layouts, behind every forward chunk
+                eng.pack.run_chunk(late)
+                plan.record_event(self.late_event, side)
         eng._pending = {c: ev for c, ev in enumerate(self.opt_events)}
+        if late is not None:
+            eng._pending[late] = self.late_event
         return self.state
 
     def _on_progress_dit(self, i):

@@ -111,19 +111,22 @@ class PackPlan:
         off = self.total
         self.total += ((rows or I) * width + 63) // 64 * 64
         self.views[name] = (off, rows or I, width)
+        # data-gradient layouts (#d, #t) are read only by the backward: packed after every forward chunk
         self.titems.append(dict(dst_off=off, src_view=src_view, src_col0=src_col0, O=O, I=I, taps=taps,
-                                smap=list(smap), src_tap=src_tap, dst_ld=width, dst_tap=Opad))
+                                smap=list(smap), src_tap=src_tap, dst_ld=width, dst_tap=Opad, late="#f" not in name))
 
     def reserve(self, name, rows, width):
         off = self.total
         self.total += (rows * width + 63) // 64 * 64
         self.views[name] = (off, rows, width)
 
-    def set_chunks(self, chunk_of_ptr):
-        """Split the packing into per-chunk launches: chunk_of_ptr(data_ptr) -> chunk index of a source parameter.
-        run_chunk(c) then packs only the views whose sources lie in chunk c (derived views after their source);
-        view_chunk[name] is the chunk after which a packed view is complete."""
+    def set_chunks(self, chunk_of_ptr, n):
+        """Split the packing into per-chunk launches: chunk_of_ptr(data_ptr) -> chunk index (< n) of a source
+        parameter. run_chunk(c) then packs only the views whose sources lie in chunk c (derived views after their
+        source) and run_chunk(late_chunk) the backward-only derived views; view_chunk[name] is the chunk after
+        which a packed view is complete."""
         self.chunk_of_ptr = chunk_of_ptr
+        self.n_declared = n
         self.finalize()
 
     def finalize(self):
@@ -150,7 +153,19 @@ class PackPlan:
             c = self.view_chunk.get(it["src_view"], 0)
             titem_chunk.append(c)
             self.view_chunk[view_of(it["dst_off"])] = c
-        self.nchunks = max(item_chunk + titem_chunk + [0]) + 1
+        nreg = max(item_chunk + titem_chunk + [getattr(self, "n_declared", 1) - 1]) + 1
+        self.late_chunk = None
+        if any(it["late"] for it in self.titems):
+            self.late_chunk = nreg
+            for j, it in enumerate(self.titems):
+                if it["late"]:
+                    assert self.view_chunk[it["src_view"]] < nreg
+                    titem_chunk[j] = nreg
+                    self.view_chunk[view_of(it["dst_off"])] = nreg
+        late_views = {view_of(it["dst_off"]) for it in self.titems if it["late"]}
+        assert not any(not it["late"] and it["src_view"] in late_views for it in self.titems), \
+            "a forward view derived from a backward-only view"
+        self.nchunks = nreg + (self.late_chunk is not None)
         descs = (_lib.PackDesc * len(self.items))()
         bmaps = [[] for _ in range(self.nchunks)]
         for j, it in enumerate(self.items):
@@ -284,6 +299,10 @@ class UNetEngine:
         use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
         self.side = torch.cuda.Stream(device=self.device) if use_side else None
         self._keep = []
+        # linear data gradients from transposed packed weights (B_NK: the forward GEMM's wider tiles). Off by
+        # default here: the data-gradient GEMMs gain 0.2 ms in isolation but the overlapped step measures
+        # +0.04 ms (same-box A/B); the DiT engine, without a weight-gradient stream, gains 3.5 %.
+        self.dgrad_t = os.environ.get("SDMI_DGRAD_T", "0") != "0"
         self._build_pack()
 
     # ------------------------------------------------------------------------------------------
@@ -308,6 +327,8 @@ class UNetEngine:
             w = P[key + ".weight"] if key + ".weight" in P else P[key]
             N, Kd = w.shape
             pk.add(key + "#f", w, N, Kd, Kd, 1, 1, Kd, 1, 0, 0)
+            if self.dgrad_t:  # [Kd][N] for the data gradient (B_NK GEMM)
+                pk.add_transpose(key + "#t", key + "#f", N, Kd, 1, [0], 8)
 
         cin_img = self.im_channels + (L["im_out"] if L["image"] else 0)
         self.cin_pad = (cin_img + 7) // 8 * 8
@@ -335,6 +356,8 @@ class UNetEngine:
             pk.add(None, wr, cout, cin, cin, 1, 1, cin, 1, 0, 0, into=cat, col0=9 * cout)
             # its dgrad layout: the conv part of the concatenated forward weight, transposed per (flipped) tap
             pk.add_transpose(f"{p}.resnet_conv_second.{l}.2#d", cat, cout, cout, 9, [8 - t for t in range(9)], cout)
+            if self.dgrad_t:  # the 1x1 residual conv's weight transposed [cin][cout] for its data gradient
+                pk.add_transpose(f"{p}.res{l}#t", cat, cout, cin, 1, [0], 8, src_col0=9 * cout)
         nd = len(L["down"]) - 1
         for i in range(nd):
             p = f"downs.{i}"
@@ -393,11 +416,18 @@ class UNetEngine:
             self._need(self.pack.view_chunk.get(name, 0))
         return self.pack.view(name)
 
+    def _dgrad(self, dy, key, out, **kw):
+        """Data gradient of the packed linear `key` (#f [N][K]): from its transposed copy #t when packed."""
+        if self.dgrad_t:
+            K.linear_dgrad_t(dy, self.W(key + "#t"), out, **kw)
+        else:
+            K.linear_dgrad(dy, self.W(key + "#f"), out, **kw)
+
     def set_chunks(self, key_chunk):
         """Parameters are updated and repacked in forward-ordered chunks (trainer): key -> chunk index."""
         self._key_chunk = dict(key_chunk)
         ptr_chunk = {self.P.raw(k).data_ptr(): c for k, c in key_chunk.items()}
-        self.pack.set_chunks(lambda ptr: ptr_chunk.get(ptr, 0))
+        self.pack.set_chunks(lambda ptr: ptr_chunk.get(ptr, 0), max(key_chunk.values()) + 1)
 
     def _need(self, c):
         ev = self._pending.pop(c, None)
@@ -655,7 +685,10 @@ class UNetEngine:
         dh2 = self._new(B * Pn, cout)
         K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout)
         dx, fresh = grads.get(c["xn"])
-        K.linear_dgrad(dy, self.W(f"{p}.res{l}#cat")[:, 9 * cout:], dx, resid=None if fresh else dx)
+        if self.dgrad_t:
+            K.linear_dgrad_t(dy, self.W(f"{p}.res{l}#t"), dx, resid=None if fresh else dx)
+        else:
+            K.linear_dgrad(dy, self.W(f"{p}.res{l}#cat")[:, 9 * cout:], dx, resid=None if fresh else dx)
         K.gn_bwd(c["h1"], dh2, dh2, c["t2"], P[b + ".0.weight"], B, Pn, cout, G, True,
                  self.g(b + ".0.weight"), self.g(b + ".0.bias"))
         off = self.temb_off[(p, l)]
@@ -713,8 +746,9 @@ class UNetEngine:
             K.chan_sum(dy, 1, B * N, C, per_c=self.g(mk + ".out_proj.bias"))
         dy_read = self.wg_event if self.side is not None else None
         do = self._new(B * N, C)
-        K.linear_dgrad(dy, self.W(mk + ".out_proj#f"), do)
+        self._dgrad(dy, mk + ".out_proj", do)
         Win = self.W(mk + ".in_proj_weight#f")
+        WinT = self.W(mk + ".in_proj_weight#t") if self.dgrad_t else None
         gW = self.g(mk + ".in_proj_weight")
         gb = self.g(mk + ".in_proj_bias")
         da = self._new(B * N, C)
@@ -726,7 +760,10 @@ class UNetEngine:
             with self._wg(dqkv):
                 K.linear_wgrad(dqkv, c["a"], gW)
                 K.chan_sum(dqkv, 1, B * N, 3 * C, per_c=gb)
-            K.linear_dgrad(dqkv, Win, da)
+            if WinT is not None:
+                K.linear_dgrad_t(dqkv, WinT, da)
+            else:
+                K.linear_dgrad(dqkv, Win, da)
         else:
             S, kv = c["S"], c["kv"]
             dq = self._new(B * N, C)
@@ -738,11 +775,17 @@ class UNetEngine:
                 K.linear_wgrad(dkv, c["cp"], gW[C:])
                 K.chan_sum(dkv, 1, B * S, 2 * C, per_c=gb[C:])
             dcp = self._new(B * S, C)
-            K.linear_dgrad(dkv, Win[C:], dcp)
+            if WinT is not None:
+                K.linear_dgrad_t(dkv, WinT[:, C:], dcp)
+            else:
+                K.linear_dgrad(dkv, Win[C:], dcp)
             with self._wg(dcp):
                 K.linear_wgrad(dcp, c["ctx"], self.g(c["ck"] + ".weight"))
                 K.chan_sum(dcp, 1, B * S, C, per_c=self.g(c["ck"] + ".bias"))
-            K.linear_dgrad(dq, Win[:C], da)
+            if WinT is not None:
+                K.linear_dgrad_t(dq, WinT[:, :C], da)
+            else:
+                K.linear_dgrad(dq, Win[:C], da)
         # x receives dy (residual) + GroupNorm-branch gradient
         key, off, _ = grads.groups[c["xn"]]
         if not grads.init.get(c["xn"], False) and dy.is_contiguous() and K.ld_of(dy) == C and \
