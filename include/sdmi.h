@@ -150,6 +150,9 @@ int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, float* ws, void
  *                      (no bias) in channels cx..cx+cmo-1; keep[b] (optional) = cond-drop multiplier
  *                      (utils/diffusion_utils.py:31-37) applied at gather time.
  *  sdmi_cond_wgrad   : gradient of cond_conv_in.weight.
+ *  sdmi_prep_input_cmap / sdmi_cond_wgrad_cmap : the same with the mask given as a uint8 class map
+ *                      (B,MH,MW) instead of the (B,cmi,MH,MW) fp32 one-hot that dataset/celeb_dataset.py:164-175
+ *                      builds (clamp(0,cmi) -> one_hot(cmi+1) -> drop background); bit-identical results.
  *  sdmi_add_noise    : scheduler/linear_noise_scheduler.py:26-48 (bit-exact fp32 mul/mul/add).
  *  sdmi_mse          : nn.MSELoss (train_ddpm_cond_celebhq_multi_gpu.py:267,346) + its gradient times
  *                      the loss scale (gscale or *gscale_dev, GradScaler :269,362).
@@ -159,6 +162,11 @@ int sdmi_prep_input(const float* x, int B, int cx, int H, int W, const float* ma
                     const float* wcond, int cmo, void* out, int cpad, const float* keep, sdmi_stream_t stream);
 int sdmi_cond_wgrad(const void* dxin, int ld, int cx, int B, int H, int W, const float* mask, int cmi, int MH, int MW,
                     int cmo, float* dw, const float* keep, sdmi_stream_t stream);
+int sdmi_prep_input_cmap(const float* x, int B, int cx, int H, int W, const unsigned char* cmap, int cmi, int MH,
+                         int MW, const float* wcond, int cmo, void* out, int cpad, const float* keep,
+                         sdmi_stream_t stream);
+int sdmi_cond_wgrad_cmap(const void* dxin, int ld, int cx, int B, int H, int W, const unsigned char* cmap, int cmi,
+                         int MH, int MW, int cmo, float* dw, const float* keep, sdmi_stream_t stream);
 int sdmi_nhwc_to_nchw(const void* src, int src_f32, int ld, int B, int C, int HW, float* dst, sdmi_stream_t stream);
 int sdmi_nchw_to_nhwc_bf16(const float* src, int B, int C, int HW, void* dst, int ld, sdmi_stream_t stream);
 int sdmi_add_noise(const float* x0, const float* eps, const long long* t, const float* sqrt_abar,

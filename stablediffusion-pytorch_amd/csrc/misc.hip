@@ -17,7 +17,11 @@ int grid_for(long long work) {
 // channels cx .. cx+cmo-1 = 1x1 conv (no bias) of the nearest-resized mask (B,cmi,MH,MW) fp32
 // (F.interpolate default 'nearest': src = min(floor(dst * (in/out)), in-1)), rest zero.
 // ---------------------------------------------------------------------------------------------
-__global__ void prep_input_kernel(const float* x, int B, int cx, int H, int W, const float* mask, int cmi, int MH,
+// CMAP: the mask is a uint8 class map (B,MH,MW) -- the reference's one-hot (celeb_dataset.py:164-175:
+// clamp(0, cmi), one_hot(cmi + 1), background channel dropped) is never materialised: class c >= 1 selects
+// weight column c-1 (min(c, cmi), the clamp), class 0 gives 0 -- the one-hot sum's exact value.
+template <bool CMAP>
+__global__ void prep_input_kernel(const float* x, int B, int cx, int H, int W, const void* mask, int cmi, int MH,
                                   int MW, const float* wcond, int cmo, bf16_t* out, int cpad, const float* keep) {
   long long total = (long long)B * H * W;
   float sh = (float)MH / (float)H, sw = (float)MW / (float)W;
@@ -30,10 +34,16 @@ __global__ void prep_input_kernel(const float* x, int B, int cx, int H, int W, c
     for (int c = 0; c < cx; ++c) v[c] = x[(((long long)b * cx + c) * H + y) * W + xx];
     if (mask) {
       int sy = min((int)floorf((float)y * sh), MH - 1), sx = min((int)floorf((float)xx * sw), MW - 1);
+      int cls = 0;
+      if (CMAP) cls = min((int)((const unsigned char*)mask)[((long long)b * MH + sy) * MW + sx], cmi);
       for (int o = 0; o < cmo; ++o) {
         float acc = 0.f;
-        for (int i = 0; i < cmi; ++i)
-          acc += wcond[o * cmi + i] * mask[(((long long)b * cmi + i) * MH + sy) * MW + sx];
+        if (CMAP) {
+          acc = cls > 0 ? wcond[o * cmi + cls - 1] : 0.f;
+        } else {
+          const float* m = (const float*)mask;
+          for (int i = 0; i < cmi; ++i) acc += wcond[o * cmi + i] * m[(((long long)b * cmi + i) * MH + sy) * MW + sx];
+        }
         v[cx + o] = keep ? acc * keep[b] : acc;
       }
     }
@@ -43,7 +53,8 @@ __global__ void prep_input_kernel(const float* x, int B, int cx, int H, int W, c
 }
 
 // d wcond[o][i] = sum_{b,p} dxin[p][cx + o] * mask_resized[b][i][p]    (one block per (o, i))
-__global__ void cond_wgrad_kernel(const bf16_t* dxin, int ld, int cx, int B, int H, int W, const float* mask, int cmi,
+template <bool CMAP>
+__global__ void cond_wgrad_kernel(const bf16_t* dxin, int ld, int cx, int B, int H, int W, const void* mask, int cmi,
                                   int MH, int MW, float* dw, const float* keep) {
   int o = blockIdx.x / cmi, i = blockIdx.x - o * cmi;
   float sh = (float)MH / (float)H, sw = (float)MW / (float)W;
@@ -54,7 +65,9 @@ __global__ void cond_wgrad_kernel(const bf16_t* dxin, int ld, int cx, int B, int
     int yx = (int)(p - (long long)b * H * W);
     int y = yx / W, xx = yx - y * W;
     int sy = min((int)floorf((float)y * sh), MH - 1), sx = min((int)floorf((float)xx * sw), MW - 1);
-    float mv = mask[(((long long)b * cmi + i) * MH + sy) * MW + sx];
+    float mv;
+    if (CMAP) mv = min((int)((const unsigned char*)mask)[((long long)b * MH + sy) * MW + sx], cmi) == i + 1 ? 1.f : 0.f;
+    else mv = ((const float*)mask)[(((long long)b * cmi + i) * MH + sy) * MW + sx];
     acc += bf2f(dxin[p * ld + cx + o]) * (keep ? mv * keep[b] : mv);
   }
   __shared__ float red[NT / 64];
@@ -305,16 +318,36 @@ extern "C" int sdmi_prep_input(const float* x, int B, int cx, int H, int W, cons
                                const float* wcond, int cmo, void* out, int cpad, const float* keep,
                                sdmi_stream_t stream) {
   if (cpad % 8 || cx + (mask ? cmo : 0) > cpad || cpad > 16) return -1;
-  hipLaunchKernelGGL(prep_input_kernel, dim3(grid_for((long long)B * H * W)), dim3(NT), 0, (hipStream_t)stream, x, B, cx,
-                     H, W, mask, cmi, MH, MW, wcond, cmo, (bf16_t*)out, cpad, keep);
+  hipLaunchKernelGGL(prep_input_kernel<false>, dim3(grid_for((long long)B * H * W)), dim3(NT), 0, (hipStream_t)stream, x,
+                     B, cx, H, W, mask, cmi, MH, MW, wcond, cmo, (bf16_t*)out, cpad, keep);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_prep_input_cmap(const float* x, int B, int cx, int H, int W, const unsigned char* cmap, int cmi,
+                                    int MH, int MW, const float* wcond, int cmo, void* out, int cpad, const float* keep,
+                                    sdmi_stream_t stream) {
+  if (cpad % 8 || cx + (cmap ? cmo : 0) > cpad || cpad > 16 || cmi < 1 || cmi > 255) return -1;
+  hipLaunchKernelGGL(prep_input_kernel<true>, dim3(grid_for((long long)B * H * W)), dim3(NT), 0, (hipStream_t)stream, x,
+                     B, cx, H, W, cmap, cmi, MH, MW, wcond, cmo, (bf16_t*)out, cpad, keep);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int sdmi_cond_wgrad(const void* dxin, int ld, int cx, int B, int H, int W, const float* mask, int cmi,
                                int MH, int MW, int cmo, float* dw, const float* keep, sdmi_stream_t stream) {
-  hipLaunchKernelGGL(cond_wgrad_kernel, dim3(cmo * cmi), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)dxin, ld, cx,
-                     B, H, W, mask, cmi, MH, MW, dw, keep);
+  hipLaunchKernelGGL(cond_wgrad_kernel<false>, dim3(cmo * cmi), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)dxin, ld,
+                     cx, B, H, W, mask, cmi, MH, MW, dw, keep);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_cond_wgrad_cmap(const void* dxin, int ld, int cx, int B, int H, int W, const unsigned char* cmap,
+                                    int cmi, int MH, int MW, int cmo, float* dw, const float* keep,
+                                    sdmi_stream_t stream) {
+  if (cmi < 1 || cmi > 255) return -1;
+  hipLaunchKernelGGL(cond_wgrad_kernel<true>, dim3(cmo * cmi), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)dxin, ld,
+                     cx, B, H, W, cmap, cmi, MH, MW, dw, keep);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -224,16 +224,10 @@ class DiTEngine:
         st = dict(B=B, H=H, W=W, N=N, M=M)
         # ---- patch source (transformer.py:180-188) + patch embedding (patch_embed.py:75-96) ----
         xin = self._new(B * H * W, self.cpad)
-        if L["image"]:
-            m = plan.as_operand(mask)
-            _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, m.data_ptr(), L["im_in"], m.shape[2],
-                                                  m.shape[3], P["cond_conv_in.weight"].data_ptr(), L["im_out"],
-                                                  xin.data_ptr(), self.cpad, K._p(mask_keep), K._stream()),
-                       "sdmi_prep_input")
-        else:
-            m = None
-            _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, None, 0, 1, 1, None, 0, xin.data_ptr(),
-                                                  self.cpad, None, K._stream()), "sdmi_prep_input")
+        m = (plan.as_operand(mask, torch.uint8 if K.is_class_map(mask) else torch.float32) if L["image"] else None)
+        K.prep_input(x, B, Cx, H, W, m, L.get("im_in", 0), P["cond_conv_in.weight"] if m is not None else None,
+                     L.get("im_out", 0),
+                     xin, self.cpad, mask_keep)
         st.update(xin=xin, mask=m, keep=mask_keep)
         # the residual stream is kept in fp32 (the reference's autocast stream is bf16; fp32 is strictly closer
         # to its fp32 forward and costs only row-kernel bandwidth -- the stream is never a GEMM operand)
@@ -504,9 +498,6 @@ class DiTEngine:
                     remap = (K._log2(gh), K._log2(gw), H, W, p, p, ph, pw)
                     K.gemm(M, self.cpad, D, dtok, _lib.A_ROWMAJOR, D, wpe[:, tap * self.cpad:], _lib.B_KN,
                            p * p * self.cpad, dxin, self.cpad, remap=remap)
-            m = st["mask"]
-            _lib.check(_lib.lib().sdmi_cond_wgrad(dxin.data_ptr(), self.cpad, self.im_channels, B, H, W, m.data_ptr(),
-                                                  L["im_in"], m.shape[2], m.shape[3], L["im_out"],
-                                                  self.g("cond_conv_in.weight").data_ptr(), K._p(st["keep"]),
-                                                  K._stream()), "sdmi_cond_wgrad")
+            K.cond_wgrad(dxin, self.cpad, self.im_channels, B, H, W, st["mask"], L["im_in"], L["im_out"],
+                         self.g("cond_conv_in.weight"), st["keep"])
         self.ws = None

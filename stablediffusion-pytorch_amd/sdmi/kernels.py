@@ -335,3 +335,36 @@ def copy_slice(src, dst, accumulate=False):
     P, C = src.shape
     check(_lib.lib().sdmi_copy_slice(_p(src), ld_of(src), _p(dst), ld_of(dst), P, C, 1 if accumulate else 0,
                                      _stream()), "sdmi_copy_slice")
+
+
+def is_class_map(mask):
+    """A (B, MH, MW) uint8 class map (sdmi.latents mask shards) instead of the reference's (B, cmi, MH, MW) fp32
+    one-hot (dataset/celeb_dataset.py:164-175)."""
+    return mask is not None and mask.dtype == torch.uint8 and mask.dim() == 3
+
+
+def prep_input(x, B, cx, H, W, mask, cmi, wcond, cmo, out, cpad, keep):
+    """Network input staging (unet_cond_base.py:131-140 / transformer.py:180-188): x NCHW fp32 -> NHWC bf16 with
+    the nearest-resized mask through the 1x1 cond conv; the mask is a one-hot fp32 tensor or a uint8 class map."""
+    L = _lib.lib()
+    if mask is None:
+        _lib.check(L.sdmi_prep_input(_ptr(x), B, cx, H, W, None, 0, 1, 1, None, 0, _ptr(out), cpad, None, _stream()),
+                   "sdmi_prep_input")
+    elif is_class_map(mask):
+        _lib.check(L.sdmi_prep_input_cmap(_ptr(x), B, cx, H, W, _ptr(mask), cmi, mask.shape[1], mask.shape[2],
+                                          _ptr(wcond), cmo, _ptr(out), cpad, _p(keep), _stream()),
+                   "sdmi_prep_input_cmap")
+    else:
+        _lib.check(L.sdmi_prep_input(_ptr(x), B, cx, H, W, _ptr(mask), cmi, mask.shape[2], mask.shape[3],
+                                     _ptr(wcond), cmo, _ptr(out), cpad, _p(keep), _stream()), "sdmi_prep_input")
+
+
+def cond_wgrad(dxin, ld, cx, B, H, W, mask, cmi, cmo, dw, keep):
+    """Gradient of cond_conv_in.weight from the staged-input gradient (one-hot or class-map mask)."""
+    L = _lib.lib()
+    if is_class_map(mask):
+        _lib.check(L.sdmi_cond_wgrad_cmap(_ptr(dxin), ld, cx, B, H, W, _ptr(mask), cmi, mask.shape[1],
+                                          mask.shape[2], cmo, _ptr(dw), _p(keep), _stream()), "sdmi_cond_wgrad_cmap")
+    else:
+        _lib.check(L.sdmi_cond_wgrad(_ptr(dxin), ld, cx, B, H, W, _ptr(mask), cmi, mask.shape[2], mask.shape[3], cmo,
+                                     _ptr(dw), _p(keep), _stream()), "sdmi_cond_wgrad")

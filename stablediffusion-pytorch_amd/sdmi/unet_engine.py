@@ -481,16 +481,10 @@ class UNetEngine:
 
         # ---- input staging + first conv (unet_cond_base.py:131-140) ----
         xin = self._new(B * H * W, self.cin_pad)
-        if L["image"]:
-            m = plan.as_operand(mask)
-            _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, m.data_ptr(), L["im_in"], m.shape[2],
-                                                  m.shape[3], P["cond_conv_in.weight"].data_ptr(), L["im_out"],
-                                                  xin.data_ptr(), self.cin_pad, K._p(mask_keep), K._stream()),
-                       "sdmi_prep_input")
-        else:
-            m = None
-            _lib.check(_lib.lib().sdmi_prep_input(x.data_ptr(), B, Cx, H, W, None, 0, 1, 1, None, 0, xin.data_ptr(),
-                                                  self.cin_pad, None, K._stream()), "sdmi_prep_input")
+        m = (plan.as_operand(mask, torch.uint8 if K.is_class_map(mask) else torch.float32) if L["image"] else None)
+        K.prep_input(x, B, Cx, H, W, m, L.get("im_in", 0), P["cond_conv_in.weight"] if m is not None else None,
+                     L.get("im_out", 0),
+                     xin, self.cin_pad, mask_keep)
         skip0 = cats[0][:, L["down"][0]:]
         K.conv_fwd(xin, B, H, W, self.cin_pad, self.cin_pad, self.W(self.first + "#f"), L["down"][0], 3, 3, 1, 1,
                    skip0, K.ld_of(skip0), bias=P[self.first + ".bias"])
@@ -884,12 +878,8 @@ class UNetEngine:
         if L["image"]:
             dxin = self._new(B * H * W, self.cin_pad)
             K.conv_fwd(dy, B, H, W, C0, ldy, self.W(self.first + "#d"), self.cin_pad, 3, 3, 1, 1, dxin, self.cin_pad)
-            m = c["mask"]
-            _lib.check(_lib.lib().sdmi_cond_wgrad(dxin.data_ptr(), self.cin_pad, self.im_channels, B, H, W,
-                                                  m.data_ptr(), L["im_in"], m.shape[2], m.shape[3], L["im_out"],
-                                                  self.g("cond_conv_in.weight").data_ptr(), K._p(c["keep"]),
-                                                  K._stream()),
-                       "sdmi_cond_wgrad")
+            K.cond_wgrad(dxin, self.cin_pad, self.im_channels, B, H, W, c["mask"], L["im_in"], L["im_out"],
+                         self.g("cond_conv_in.weight"), c["keep"])
 
     def _bwd_time(self, c, grads):
         P, L = self.P, self.L

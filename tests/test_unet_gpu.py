@@ -128,3 +128,39 @@ def test_class_conditional_unet_matches_golden():
     p = dict(model.named_parameters())
     for k in ("class_emb.weight", "t_proj.0.weight"):
         assert cos(p[k].grad.cpu(), f["grad." + k]) >= 0.99, k
+
+
+def test_class_map_mask_matches_one_hot_bitwise():
+    """uint8 class-map masks (sdmi.latents mask shards) through sdmi_prep_input_cmap / sdmi_cond_wgrad_cmap give
+    bit-identical outputs and gradients to the reference's one-hot fp32 mask (incl. values > 18: the clamp)."""
+    import ctypes
+    from sdmi import kernels as K
+    cfg = SMALL_COND
+    model, _ = make(cfg, True)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 4, 32, 32, generator=g).cuda()
+    t = torch.randint(0, 1000, (2,), generator=g).cuda()
+    ctx = cfg["condition_config"]["text_condition_config"]["text_embed_dim"]
+    text = torch.randn(2, 77, ctx, generator=g).cuda()
+    cmap = torch.randint(0, 21, (2, 96, 96), generator=g).to(torch.uint8)
+    outs, grads = [], []
+    for mask in (one_hot(cmap).cuda(), cmap.cuda()):
+        model.zero_grad(set_to_none=True)
+        out = model(x, t, {"text": text, "image": mask})
+        (out.float() ** 2).mean().backward()
+        torch.cuda.synchronize()
+        outs.append(out.detach().cpu())
+        grads.append({k: p.grad.detach().cpu().clone() for k, p in model.named_parameters()})
+    assert torch.equal(outs[0], outs[1])
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+    # cond-drop multipliers folded in at gather time (diffusion_utils.py:31-37)
+    w = torch.randn(3, 18, generator=g).cuda()
+    keep = torch.tensor([1.0, 0.0]).cuda()
+    a = torch.empty(2 * 32 * 32, 8, dtype=torch.bfloat16, device="cuda")
+    b = torch.empty_like(a)
+    K.prep_input(x, 2, 4, 32, 32, one_hot(cmap).contiguous().cuda(), 18, w, 3, a, 8, keep)
+    K.prep_input(x, 2, 4, 32, 32, cmap.cuda(), 18, w, 3, b, 8, keep)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert torch.count_nonzero(b[1024:, 4:7]) == 0 and torch.count_nonzero(b[:1024, 4:7]) > 0
