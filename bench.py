@@ -49,16 +49,27 @@ def kernel_name(tag, info):
         return f"gemm_kernel<{a}, {b}>"
     return f"gemm_dma_kernel<{a}, {b}, {v}, {tn if v == 2 else 128}>"
 PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+ROOF_FILE = os.path.join(REPO, "profiles", "r01_roofline_evidence.json")
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` (read x2-corrected FETCH_SIZE + WRITE_SIZE) from the committed rocprofv3
-    --pmc passes of this same bench command (scripts/gpu_pmc.sh -> profiles/*_pmc_traffic.json), or None."""
+def pmc_traffic(kernel, unsplit):
+    """(HBM bytes per launch of `kernel` -- read x2-corrected FETCH_SIZE + WRITE_SIZE -- from the committed rocprofv3
+    --pmc passes of this same bench command, unit note) or (None, None). `unsplit`: the bench times only the unsplit
+    launches, so the per-dispatch figure over those launches (scripts/roofline_evidence.py ->
+    profiles/r01_roofline_evidence.json) is preferred; otherwise the all-launch average (profiles/*_pmc_traffic.json)."""
+    try:
+        d = json.load(open(ROOF_FILE))
+        if unsplit and d.get("kernel") == kernel and d.get("traffic_bytes_per_launch"):
+            return d["traffic_bytes_per_launch"], ("bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, the kernel's "
+                                                   "unsplit launches: the ones timed here)")
+    except (OSError, KeyError, TypeError, ValueError):
+        pass
     try:
         d = json.load(open(PMC_FILE))[kernel]
-        return d["read_bytes_per_launch"] + d["write_bytes_per_launch"]
+        return (d["read_bytes_per_launch"] + d["write_bytes_per_launch"],
+                "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, all launches of the kernel)")
     except (OSError, KeyError, TypeError, ValueError):
-        return None
+        return None, None
 
 
 def cond_config():
@@ -351,12 +362,12 @@ def main():
         dname, d = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
         use1 = d["n1"] > 0
         dfl, dms, dn = (d["fl1"], d["ms1"], d["n1"]) if use1 else (d["fl"], d["ms"], d["n"])
-        traffic = pmc_traffic(dname)
+        traffic, traffic_unit = pmc_traffic(dname, use1)
         roof = {"bound": "mfma", "kernel": f"sdmi {dname} ({d['mode']}: implicit-GEMM conv fwd/dgrad)"
                 if d["mode"] == "gemm_a1b0" else f"sdmi {dname} ({d['mode']})",
                 "achieved": dfl / (dms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
                 "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic,
-                "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, all launches of the kernel)",
+                "traffic_unit": traffic_unit,
                 "launches": dn, "launches_note": "unsplit launches of the kernel in one step (HIP events on its stream)"
                 if use1 else "all launches (each includes its split-K reducer launch)",
                 "avg_launch_us": dms * 1e3 / dn, "flop_per_launch": dfl / dn,

@@ -5,7 +5,8 @@ set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=${TAG:-r01}
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_${TAG}_$C -o run -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --issue eager > gpurun_out/pmc_${TAG}_$C.log 2>&1 || { tail -5 gpurun_out/pmc_${TAG}_$C.log; exit 1; }
+  timeout -s KILL 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_${TAG}_$C -o run -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --issue eager > gpurun_out/pmc_${TAG}_$C.log 2>&1 || { tail -5 gpurun_out/pmc_${TAG}_$C.log; exit 1; }
 done
 python3 scripts/pmc_summary.py gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE --json gpurun_out/pmc_${TAG}_traffic.json > gpurun_out/pmc_${TAG}.txt
 head -30 gpurun_out/pmc_${TAG}.txt
+python3 scripts/roofline_evidence.py gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE "${ROOF_KERNEL:-gemm_dma_kernel<1, 0, 2, 128>}" --json gpurun_out/pmc_${TAG}_roofline.json

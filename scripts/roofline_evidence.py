@@ -1,0 +1,54 @@
+"""rocprofv3 evidence for bench.py's `roofline` kernel, restricted to the launches the bench's HIP events time:
+the UNSPLIT launches (grid z == 1; split-K launches are excluded there because their event also brackets the
+reducer). From a --kernel-trace CSV (or a directory holding one): average duration of those launches; from the
+--pmc FETCH_SIZE / WRITE_SIZE passes (each run with --kernel-trace as well, so every counter row joins its own
+dispatch's per-axis grid by Dispatch_Id): HBM bytes per unsplit launch (FETCH_SIZE x2, the gfx950 correction of
+MI355X_MICROARCH.md's HBM section; both counters in KiB).
+
+Usage: python scripts/roofline_evidence.py <kernel_trace.csv|dir> <fetch_dir> <write_dir> "<kernel>" [--json out]"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def _trace_csv(p):
+    if os.path.isdir(p):
+        return glob.glob(os.path.join(p, "**", "*kernel_trace.csv"), recursive=True)[0]
+    return p
+
+
+def _grid_z(d):
+    """Dispatch_Id -> grid z of the pass's own kernel trace"""
+    return {r["Dispatch_Id"]: int(r["Grid_Size_Z"]) for r in csv.DictReader(open(_trace_csv(d)))}
+
+
+def main():
+    trace, fdir, wdir, kernel = sys.argv[1:5]
+    durs = []
+    for r in csv.DictReader(open(_trace_csv(trace))):
+        if kernel not in r["Kernel_Name"]:
+            continue
+        if int(r["Grid_Size_Z"]) == 1:
+            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = {"kernel": kernel, "trace_unsplit_launches": len(durs),
+           "trace_avg_us": sum(durs) / len(durs) if durs else None}
+    for d, cname, mul in ((fdir, "FETCH_SIZE", 2.0), (wdir, "WRITE_SIZE", 1.0)):
+        vals = []
+        gz = _grid_z(d)
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] == cname and kernel in r["Kernel_Name"] and gz.get(r["Dispatch_Id"]) == 1:
+                    vals.append(float(r["Counter_Value"]) * 1024 * mul)
+        out[cname.lower() + "_bytes_per_launch"] = sum(vals) / len(vals) if vals else None
+        out[cname.lower() + "_launches"] = len(vals)
+    if out["fetch_size_bytes_per_launch"] is not None and out["write_size_bytes_per_launch"] is not None:
+        out["traffic_bytes_per_launch"] = out["fetch_size_bytes_per_launch"] + out["write_size_bytes_per_launch"]
+    print(json.dumps(out, indent=1))
+    if "--json" in sys.argv:
+        json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
