@@ -30,6 +30,9 @@ FLOP_PER_STEP = 3.8815e12      # cond-UNet fwd+bwd at B=32 (Flop
 WORKLOADS = {
     "cond-unet": dict(metric=METRIC, flop=FLOP_PER_STEP),
     "dit": dict(metric="DDPM train steps/sec (DiT-12L image-cond, CelebHQ-256 latents, B=32) on MI355X", flop=6.759e11),
+    # BASELINE config 3: config/celebhq.yaml unconditional UNet (tools/train_ddpm_vqvae.py step: Adam, no clip / EMA)
+    "uncond-unet": dict(metric="DDPM train steps/sec (uncond-UNet celebhq.yaml, CelebHQ-256 latents, B=32) on MI355X",
+                        flop=3.4814e12),
     # VQVAE encode + decode (no grad) of a batch of 8 CelebHQ-256 images: 2.9497e11 FLOP per image
     "vqvae": dict(metric="VQVAE encode+decode steps/sec (celebhq.yaml autoencoder, 256x256, B=8) on MI355X",
                   flop=8 * 2.9497e11),
@@ -70,6 +73,11 @@ def pmc_traffic(kernel, unsplit):
                 "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, all launches of the kernel)")
     except (OSError, KeyError, TypeError, ValueError):
         return None, None
+
+
+def uncond_config():
+    from tests.golden.configs import full_uncond_config
+    return full_uncond_config()
 
 
 def cond_config():
@@ -142,15 +150,15 @@ def cpu_baseline_vqvae(cfg, B=8):
                        f"torch CPU {torch.__version__} with {threads} threads")
 
 
-def cpu_baseline(cfg, B=32):
+def cpu_baseline(cfg, B=32, uncond=False):
     """The oracle (CPU fp32 restatement of the reference step) on the host cores; bounded sample."""
     from oracle import sd_oracle as O
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    sd = O.deterministic_state(O.unet_param_shapes(cfg), seed=0)
+    sd = O.deterministic_state(O.unet_param_shapes(cfg, base="uncond" if uncond else None), seed=0)
     ema = {k: v.clone() for k, v in sd.items()}
     opt = O.AdamState(sd)
-    sched = O.SchedulerTables(1000, 0.00085, 0.012)
+    sched = O.SchedulerTables(1000, 0.0015, 0.0195) if uncond else O.SchedulerTables(1000, 0.00085, 0.012)
     g = torch.Generator().manual_seed(1111)
     x0 = torch.randn(B, 4, 32, 32, generator=g)
     text = torch.randn(B, 77, 512, generator=g)
@@ -161,10 +169,14 @@ def cpu_baseline(cfg, B=32):
         noise = torch.randn(x0.shape, generator=g)
         t = torch.randint(0, 1000, (B,), generator=g)
         t0 = time.perf_counter()
-        O.train_step(sd, ema, opt, cfg, sched, x0, noise, t, {"text": text, "image": mask})
+        if uncond:  # tools/train_ddpm_vqvae.py: no clip (inf), no EMA (decay 0: a copy, negligible)
+            O.train_step(sd, ema, opt, cfg, sched, x0, noise, t, None, lr=5e-6, clip=float("inf"), ema_decay=0.0)
+        else:
+            O.train_step(sd, ema, opt, cfg, sched, x0, noise, t, {"text": text, "image": mask})
         times.append(time.perf_counter() - t0)
+    what = "fwd+bwd+Adam" if uncond else "fwd+bwd+clip+Adam+EMA"
     return dict(value=1.0 / times[-1], unit="steps/s", cores=threads, kind="port",
-                sample=f"oracle fp32 train step (fwd+bwd+clip+Adam+EMA), B={B}, 1 warm-up + 1 timed step, "
+                sample=f"oracle fp32 train step ({what}), B={B}, 1 warm-up + 1 timed step, "
                        f"{times[-1]:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
 
 
@@ -232,7 +244,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="cond-unet", choices=sorted(WORKLOADS),
-                    help="cond-unet (the headline metric, default) or dit (DiT-12L training step)")
+                    help="cond-unet (the headline metric, default), uncond-unet (celebhq.yaml), dit (DiT-12L training "
+                         "step) or vqvae (encode + decode)")
     ap.add_argument("--profile-gemm", action="store_true", default=True)
     ap.add_argument("--issue", default="plan", choices=("plan", "eager", "graph"),
                     help="plan (default): the step recorded once and its native calls replayed (sdmi.plan); eager: "
@@ -263,9 +276,10 @@ def main():
 
     wl = WORKLOADS[args.workload]
     is_dit = args.workload == "dit"
+    is_uncond = args.workload == "uncond-unet"
     if args.workload == "vqvae":
         return main_vqvae(args, wl, world, rank, device)
-    cfg = dit_config() if is_dit else cond_config()
+    cfg = dit_config() if is_dit else (uncond_config() if is_uncond else cond_config())
     torch.manual_seed(1111)  # identical initial weights on every rank (DDP broadcasts rank 0's)
     group = dist.group.WORLD if world > 1 else None
     if is_dit:
@@ -275,6 +289,11 @@ def main():
             if v.abs().max() == 0:  # the timed step runs on non-trivial data (zeros clock higher, MI355X DVFS)
                 v.normal_(0.0, 0.02)
         trainer = DDPMTrainer(cfg, init, device, base="dit", lr=1e-4, ema_decay=None, group=group)
+    elif is_uncond:  # tools/train_ddpm_vqvae.py:76-104: Adam(ldm_lr 5e-6, celebhq.yaml:54), no clip, no EMA
+        import models.unet_base as mu
+        init = mu.Unet(4, cfg).state_dict()
+        trainer = DDPMTrainer(cfg, init, device, base="uncond", lr=5e-6, ema_decay=None, max_grad_norm=float("inf"),
+                              sched=(1000, 0.0015, 0.0195), group=group)
     else:
         init = mc.Unet(4, cfg).state_dict()
         trainer = DDPMTrainer(cfg, init, device, group=group)
@@ -287,6 +306,9 @@ def main():
     def eager_step():
         noise = torch.randn(x0.shape, device=device, generator=gen)
         t = torch.randint(0, 1000, (B,), device=device, generator=gen)
+        if is_uncond:
+            trainer.step(x0, noise, t)
+            return
         if is_dit:  # image-only conditioning, drop prob 0.9 (Model_DiT_12L_config.py ldm_image_condition_cond_drop_prob)
             keep = (torch.rand(B, device=device, generator=gen) > 0.9).float()
             trainer.step(x0, noise, t, None, mask, mask_keep=keep)
@@ -303,7 +325,8 @@ def main():
         from sdmi.graph import CapturedTrainStep
         if issue == "graph" and not is_dit:
             trainer.engine.side = None  # single-stream capture
-        cap = CapturedTrainStep(trainer, x0, None if is_dit else text, empty, mask, B, generator=gen, drop_p=drop_p,
+        cap = CapturedTrainStep(trainer, x0, None if (is_dit or is_uncond) else text, empty, None if is_uncond else mask,
+                                B, generator=gen, drop_p=drop_p,
                                 mode=issue)
         one_step = cap.step
     else:
@@ -388,6 +411,9 @@ def main():
         "config": ({"workload": "DiT-12L Model_DiT_12L_config training step (image cond, no EMA, lr 1e-4)",
                     "model": "DiT-12L 18.3M", "global_batch": B * world, "per_gpu_batch": B, "latent": [4, 32, 32],
                     "mask": [18, 512, 512], "parallelism": f"dp{world}"} if is_dit else
+                   {"workload": "uncond-UNet celebhq.yaml training step (Adam lr 5e-6, no clip / EMA)",
+                    "model": "uncond-UNet 103.5M", "global_batch": B * world, "per_gpu_batch": B,
+                    "latent": [4, 32, 32], "parallelism": f"dp{world}"} if is_uncond else
                    {"workload": "cond-UNet celebhq_text_image_cond training step", "model": "cond-UNet 118.5M",
                     "global_batch": B * world, "per_gpu_batch": B, "latent": [4, 32, 32],
                     "text": [77, 512], "mask": [18, 512, 512], "parallelism": f"dp{world}"}),
@@ -398,7 +424,7 @@ def main():
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline_dit(cfg) if is_dit else cpu_baseline(cfg)
+        result["cpu_baseline"] = cpu_baseline_dit(cfg) if is_dit else cpu_baseline(cfg, uncond=is_uncond)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
