@@ -164,3 +164,35 @@ def test_class_map_mask_matches_one_hot_bitwise():
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert torch.count_nonzero(b[1024:, 4:7]) == 0 and torch.count_nonzero(b[:1024, 4:7]) > 0
+
+
+def test_uncond_trainer_two_steps_match_oracle():
+    """DDPMTrainer(base="uncond") with the tools/train_ddpm_vqvae.py step (Adam lr 5e-6, no clip, no EMA; celebhq.yaml
+    schedule 0.0015 -> 0.0195) vs the fp32 oracle step: loss within 1 %, gradient norm within 5 %, parameter-update
+    cosine >= 0.95 (Adam's first steps are ~sign(g) * lr, so bf16 noise on near-zero gradients flips a few)."""
+    from sdmi.trainer import DDPMTrainer, S_LOSS, S_NORM
+    cfg = SMALL_UNCOND
+    sd0 = O.deterministic_state(O.unet_param_shapes(cfg, base="uncond"), 7)
+    tr = DDPMTrainer(cfg, sd0, "cuda", base="uncond", lr=5e-6, ema_decay=None, max_grad_norm=float("inf"),
+                     sched=(1000, 0.0015, 0.0195))
+    assert tr.ema is None
+    ref = {k: v.clone() for k, v in sd0.items()}
+    ema = {k: v.clone() for k, v in sd0.items()}
+    opt = O.AdamState(ref)
+    sched = O.SchedulerTables(1000, 0.0015, 0.0195)
+    g = torch.Generator().manual_seed(21)
+    for _ in range(2):
+        x0 = torch.randn(2, 4, 32, 32, generator=g)
+        noise = torch.randn(2, 4, 32, 32, generator=g)
+        t = torch.randint(0, 1000, (2,), generator=g)
+        tr.step(x0.cuda(), noise.cuda(), t.cuda())
+        rl, rn, _ = O.train_step(ref, ema, opt, cfg, sched, x0, noise, t, None, lr=5e-6, clip=float("inf"),
+                                 ema_decay=0.0)
+        torch.cuda.synchronize()
+        loss, norm = tr.state[S_LOSS].item(), tr.state[S_NORM].item()
+        assert abs(loss - rl.item()) <= 1e-2 * rl.item(), (loss, rl.item())
+        assert abs(norm - rn.item()) <= 5e-2 * rn.item(), (norm, rn.item())
+    p = tr.store.params.cpu()
+    d_hip = torch.cat([(tr.store.view(p, k) - sd0[k]).flatten() for k in tr.store.order])
+    d_ref = torch.cat([(ref[k] - sd0[k]).flatten() for k in tr.store.order])
+    assert cos(d_hip, d_ref) >= 0.95, cos(d_hip, d_ref)
