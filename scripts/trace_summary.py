@@ -20,9 +20,10 @@ def main():
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if "adam_ema_kernel" in r["Kernel_Name"]]
+    # one gradient-norm launch per step (the optimizer itself runs in chunks pipelined into the next forward)
+    marks = [i for i, r in enumerate(rows) if "sumsq_kernel" in r["Kernel_Name"]]
     if len(marks) < 2:
-        raise SystemExit("need >= 2 optimizer launches in the trace")
+        raise SystemExit("need >= 2 gradient-norm launches in the trace")
     step = rows[marks[-2] + 1: marks[-1] + 1]
     t0 = int(step[0]["Start_Timestamp"])
     t1 = int(step[-1]["End_Timestamp"])
@@ -47,15 +48,16 @@ def main():
             ce = max(ce, e0)
     union += ce - cs
     print(f"  GPU busy (any stream) {union / 1e6:.3f} ms")
-    # phases on the issuing stream: forward = before the loss kernel, backward, optimizer = from sumsq on
+    # phases: from the previous step's gradient norm to the loss = optimizer chunks + packing (side stream) and the
+    # forward; from the loss to this step's gradient norm = backward (+ weight gradients on the side stream)
     names = [r["Kernel_Name"] for r in step]
     i_mse = next((i for i, n in enumerate(names) if "mse_kernel" in n), None)
-    i_opt = next((i for i, n in enumerate(names) if "sumsq_kernel" in n), None)
-    if i_mse is not None and i_opt is not None:
-        def span_busy(a, b):
-            return sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in step[a:b])
-        print(f"  phases (kernel busy): forward {span_busy(0, i_mse) / 1e6:.3f} ms, "
-              f"backward {span_busy(i_mse, i_opt) / 1e6:.3f} ms, optimizer+pack {span_busy(i_opt, len(step)) / 1e6:.3f} ms")
+    if i_mse is not None:
+        def busy_of(rs, pred=lambda n: True):
+            return sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rs if pred(r["Kernel_Name"]))
+        opt = lambda n: "adam_ema" in n or "pack" in n  # noqa: E731
+        print(f"  phases (kernel busy): forward {busy_of(step[:i_mse], lambda n: not opt(n)) / 1e6:.3f} ms, "
+              f"optimizer+pack {busy_of(step, opt) / 1e6:.3f} ms, backward {busy_of(step[i_mse:]) / 1e6:.3f} ms")
     groups = {}
     for r in step:
         wg = int(r["Workgroup_Size_X"])

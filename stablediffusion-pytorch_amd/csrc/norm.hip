@@ -367,6 +367,23 @@ int gn_pass_threads(int P, int cw) {
   return 0;
 }
 
+// the 1024-thread single pass puts one workgroup on a CU per (strip, batch row): below SDMI_GN_PASS_MIN_WG such
+// workgroups (narrow C at B = 32: C = 128 -> 64 workgroups) the chip is mostly idle and the two-pass path
+// (pixel-split reductions, >= 512 workgroups) is used instead. 0 (default) keeps the single pass everywhere.
+int gn_pass_min_wg() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SDMI_GN_PASS_MIN_WG");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
+int gn_pass_threads_for(int P, int cw, int nch, int B) {
+  const int nth = gn_pass_threads(P, cw);
+  return (nth == 1024 && (long long)nch * B < gn_pass_min_wg()) ? 0 : nth;
+}
+
 // per-channel sums of u (and v) over the workgroup's rows -> s1/s2[cw] in LDS (red: [NTH][17] scratch)
 template <int NTH>
 __device__ __forceinline__ void small_reduce(const float* u, const float* v, int cw, float (*red)[17], float* s1,
@@ -719,7 +736,7 @@ extern "C" int sdmi_gn_fwd(const void* x, int ldx, void* y, int ldy, int B, int 
                            const float* gamma, const float* beta, int silu, float* ws, float* table, sdmi_stream_t stream) {
   if (C % 8 || G <= 0 || C % G) return -1;
   const int cw = strip_width(C, C / G);
-  const int nth = gn_pass_threads(P, cw);
+  const int nth = gn_pass_threads_for(P, cw, (C + cw - 1) / cw, B);
   if (nth) {
     StripArgs a = {};
     a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.eps = eps; a.silu = silu;
@@ -762,7 +779,7 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   const int nch = (C + r.CW - 1) / r.CW;
   if (r.CW > NT || nch > BATCH_CTR) return -2;
   r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
-  if (const int nth = gn_pass_threads(P, r.CW)) {  // single pass
+  if (const int nth = gn_pass_threads_for(P, r.CW, nch, B)) {  // single pass
     if (dgamma && !(r.ctr = counter_slot())) return -4;
     if (nth == 256)
       hipLaunchKernelGGL(gn_bwd_pass_kernel<256>, dim3(nch, B), dim3(256), 0, s, r, (bf16_t*)dx, lddx,
