@@ -287,6 +287,11 @@ int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* st
 int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n, const float* state,
                   float lr, float b1, float b2, float eps, float ema_decay, sdmi_stream_t stream);
 
+/* Streams restricted to a share of the CUs (hipExtStreamCreateWithCUMask): keep_num of every keep_den CUs.
+ * Used for the engine's weight-gradient side stream (SDMI_SIDE_CU=num/den), no reference counterpart. */
+int sdmi_stream_create_cu_share(int keep_num, int keep_den, sdmi_stream_t* out);
+int sdmi_stream_destroy(sdmi_stream_t s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -83,6 +83,8 @@ SIGNATURES = {
     "sdmi_chan_sum": ([_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _I, _P], _I),
     "sdmi_prep_input": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),
     "sdmi_cond_wgrad": ([_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P], _I),
+    "sdmi_stream_create_cu_share": ([_I, _I, ctypes.POINTER(ctypes.c_void_p)], _I),
+    "sdmi_stream_destroy": ([_P], _I),
     "sdmi_prep_input_cmap": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),
     "sdmi_cond_wgrad_cmap": ([_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P], _I),
     "sdmi_nhwc_to_nchw": ([_P, _I, _I, _I, _I, _I, _P, _P], _I),

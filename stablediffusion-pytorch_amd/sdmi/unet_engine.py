@@ -269,6 +269,27 @@ class Tape(list):
         super().append(item)
 
 
+_SIDE_STREAMS = {}
+
+
+def side_stream(device):
+    """The weight-gradient side stream. SDMI_SIDE_CU=num/den restricts it to num of every den CUs
+    (sdmi_stream_create_cu_share) so its wide GEMMs leave CUs free for the critical-path data-gradient chain;
+    unset: an ordinary stream."""
+    share = os.environ.get("SDMI_SIDE_CU", "")
+    if not share:
+        return torch.cuda.Stream(device=device)
+    num, den = (int(v) for v in share.split("/"))
+    key = (str(device), num, den)
+    if key not in _SIDE_STREAMS:  # one per process and device (never destroyed: streams live as long as the engine)
+        import ctypes
+        with torch.cuda.device(device):
+            h = ctypes.c_void_p()
+            _lib.check(_lib.lib().sdmi_stream_create_cu_share(num, den, ctypes.byref(h)), "sdmi_stream_create_cu_share")
+            _SIDE_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=device)
+    return _SIDE_STREAMS[key]
+
+
 class UNetEngine:
     def __init__(self, cfg, params, grads=None, base=None, im_channels=4):
         """params / grads: {state-dict key: fp32 CUDA tensor}; grads may be None (inference)."""
@@ -297,7 +318,7 @@ class UNetEngine:
         # weight-gradient work (wgrad GEMMs, bias sums) runs on a side stream, overlapped with the
         # data-gradient chain of the backward on the current stream
         use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
-        self.side = torch.cuda.Stream(device=self.device) if use_side else None
+        self.side = side_stream(self.device) if use_side else None
         self._keep = []
         # linear data gradients from transposed packed weights (B_NK: the forward GEMM's wider tiles). Off by
         # default here: the data-gradient GEMMs gain 0.2 ms in isolation but the overlapped step measures
