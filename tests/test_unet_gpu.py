@@ -196,3 +196,35 @@ def test_uncond_trainer_two_steps_match_oracle():
     d_hip = torch.cat([(tr.store.view(p, k) - sd0[k]).flatten() for k in tr.store.order])
     d_ref = torch.cat([(ref[k] - sd0[k]).flatten() for k in tr.store.order])
     assert cos(d_hip, d_ref) >= 0.95, cos(d_hip, d_ref)
+
+
+def test_edge_shapes_batch1_nonsquare_and_broadcast_t():
+    """Edge cases of the reference call surface: B = 1, a non-square latent (32 x 16: the reference only needs
+    H, W divisible by the down-sampling), a (1,)-shaped timestep broadcast over the batch (tools/sample_ddpm_*.py
+    pass `torch.as_tensor(i).unsqueeze(0)`), and a 0-d timestep. Same forward bound as the main test."""
+    cfg = SMALL_COND
+    model, sd = make(cfg, True)
+    leaves = {k: v.clone() for k, v in sd.items()}
+    g = torch.Generator().manual_seed(17)
+    ctx = cfg["condition_config"]["text_condition_config"]["text_embed_dim"]
+    for (B, H, W, tshape) in ((1, 32, 32, "0d"), (2, 32, 16, "1"), (3, 16, 32, "B")):
+        x = torch.randn(B, 4, H, W, generator=g)
+        tv = int(torch.randint(0, 1000, (1,), generator=g))
+        t = {"0d": torch.tensor(tv), "1": torch.tensor([tv]), "B": torch.full((B,), tv)}[tshape]
+        c = {"text": torch.randn(B, 77, ctx, generator=g),
+             "image": one_hot(torch.randint(0, 19, (B, 2 * H, 2 * W), generator=g)).contiguous()}
+        with torch.no_grad():
+            ref = O.unet_forward(leaves, cfg, x, torch.full((B,), tv), c)
+            out = model(x.cuda(), t.cuda(), {k: v.cuda() for k, v in c.items()}).cpu()
+        assert out.shape == ref.shape
+        mse = ((out - ref) ** 2).mean().item()
+        assert mse <= 1e-4, (B, H, W, tshape, mse)
+
+
+def test_unsupported_spatial_size_fails_loudly():
+    """Spatial sizes the implicit-GEMM geometry cannot encode (non power of two) raise on the host, before any
+    convolution is launched -- never a silent fallback."""
+    model, _ = make(SMALL_UNCOND, False)
+    with pytest.raises(ValueError):
+        model(torch.randn(1, 4, 24, 24).cuda(), torch.tensor([3]).cuda())
+    torch.cuda.synchronize()
