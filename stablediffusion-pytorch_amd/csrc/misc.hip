@@ -1,6 +1,7 @@
 // Small fused kernels around the denoiser: input staging (mask gather + 1x1 mask projection),
 // output layout, scheduler add_noise, MSE loss, time embedding, SiLU, channel-slice copies and
 // bf16 weight packing.
+#include <atomic>
 #include <hip/hip_ext.h>
 
 #include "common.h"
@@ -8,6 +9,14 @@
 
 namespace {
 constexpr int NT = 256;
+
+// input staging: one pixel per thread with up to 18 scattered mask reads each -- latency-bound, so small
+// workgroups (4x the workgroups of NT-thread blocks: a 32768-pixel batch covers 512 CUs' worth of slots)
+constexpr int PREP_NT = 64;
+int prep_grid(long long work) {
+  long long g = (work + PREP_NT - 1) / PREP_NT;
+  return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
 
 int grid_for(long long work) {
   long long g = (work + NT - 1) / NT;
@@ -27,7 +36,7 @@ __global__ void prep_input_kernel(const float* x, int B, int cx, int H, int W, c
                                   int MW, const float* wcond, int cmo, bf16_t* out, int cpad, const float* keep) {
   long long total = (long long)B * H * W;
   float sh = (float)MH / (float)H, sw = (float)MW / (float)W;
-  for (long long p = (long long)blockIdx.x * NT + threadIdx.x; p < total; p += (long long)gridDim.x * NT) {
+  for (long long p = (long long)blockIdx.x * PREP_NT + threadIdx.x; p < total; p += (long long)gridDim.x * PREP_NT) {
     int b = (int)(p / (H * W));
     int yx = (int)(p - (long long)b * H * W);
     int y = yx / W, xx = yx - y * W;
@@ -55,14 +64,25 @@ __global__ void prep_input_kernel(const float* x, int B, int cx, int H, int W, c
 }
 
 // d wcond[o][i] = sum_{b,p} dxin[p][cx + o] * mask_resized[b][i][p]    (one block per (o, i))
+// Pixel-split form: block (oi, z) sums pixels [z * chunk, (z + 1) * chunk) into part[z][oi] (one block per (o, i)
+// left 54 workgroups looping over every pixel: ~90 us at the end of the backward); cond_wgrad_finish_kernel adds the
+// CW_SPLITS partials in a fixed order, so the result is deterministic (and identical between the one-hot and the
+// class-map forms, which differ only in how mv is read).
+constexpr int CW_SPLITS = 32;
+constexpr int CW_SLOTS = 8;                  // partial buffers, one per launch round-robin (concurrent engines)
+constexpr int CW_MAX = 16 * 255;             // cmo <= 16 (cpad), cmi <= 255
+__device__ float g_cw_part[CW_SLOTS][CW_SPLITS][CW_MAX];
+
 template <bool CMAP>
 __global__ void cond_wgrad_kernel(const bf16_t* dxin, int ld, int cx, int B, int H, int W, const void* mask, int cmi,
-                                  int MH, int MW, float* dw, const float* keep) {
-  int o = blockIdx.x / cmi, i = blockIdx.x - o * cmi;
+                                  int MH, int MW, int slot, const float* keep) {
+  const int oi = blockIdx.x, o = oi / cmi, i = oi - o * cmi;
   float sh = (float)MH / (float)H, sw = (float)MW / (float)W;
-  long long total = (long long)B * H * W;
+  const long long total = (long long)B * H * W;
+  const long long chunk = (total + CW_SPLITS - 1) / CW_SPLITS;
+  const long long p0 = blockIdx.y * chunk, p1 = min(total, p0 + chunk);
   float acc = 0.f;
-  for (long long p = threadIdx.x; p < total; p += NT) {
+  for (long long p = p0 + threadIdx.x; p < p1; p += NT) {
     int b = (int)(p / (H * W));
     int yx = (int)(p - (long long)b * H * W);
     int y = yx / W, xx = yx - y * W;
@@ -79,8 +99,34 @@ __global__ void cond_wgrad_kernel(const bf16_t* dxin, int ld, int cx, int B, int
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int w = 0; w < NT / 64; ++w) s += red[w];
-    dw[o * cmi + i] = s;
+    g_cw_part[slot][blockIdx.y][oi] = s;
   }
+}
+
+__global__ void cond_wgrad_finish_kernel(int n, int slot, float* dw) {
+  for (int oi = blockIdx.x * NT + threadIdx.x; oi < n; oi += gridDim.x * NT) {
+    float s = 0.f;
+    for (int z = 0; z < CW_SPLITS; ++z) s += g_cw_part[slot][z][oi];
+    dw[oi] = s;
+  }
+}
+
+int cw_slot() {
+  static std::atomic<unsigned> next{0};
+  return (int)(next.fetch_add(1) % CW_SLOTS);
+}
+
+template <bool CMAP>
+int launch_cond_wgrad(const void* dxin, int ld, int cx, int B, int H, int W, const void* mask, int cmi, int MH, int MW,
+                      int cmo, float* dw, const float* keep, hipStream_t s) {
+  if (cmo < 1 || cmo > 16 || cmi < 1 || cmi > 255) return -1;
+  const int slot = cw_slot();
+  hipLaunchKernelGGL(cond_wgrad_kernel<CMAP>, dim3(cmo * cmi, CW_SPLITS), dim3(NT), 0, s, (const bf16_t*)dxin, ld, cx,
+                     B, H, W, mask, cmi, MH, MW, slot, keep);
+  SDMI_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cond_wgrad_finish_kernel, dim3((cmo * cmi + NT - 1) / NT), dim3(NT), 0, s, cmo * cmi, slot, dw);
+  SDMI_CHECK_LAUNCH();
+  return 0;
 }
 
 // NHWC (fp32 or bf16, row stride ld) -> NCHW fp32 (first C channels), and the reverse for gradients
@@ -320,7 +366,7 @@ extern "C" int sdmi_prep_input(const float* x, int B, int cx, int H, int W, cons
                                const float* wcond, int cmo, void* out, int cpad, const float* keep,
                                sdmi_stream_t stream) {
   if (cpad % 8 || cx + (mask ? cmo : 0) > cpad || cpad > 16) return -1;
-  hipLaunchKernelGGL(prep_input_kernel<false>, dim3(grid_for((long long)B * H * W)), dim3(NT), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(prep_input_kernel<false>, dim3(prep_grid((long long)B * H * W)), dim3(PREP_NT), 0, (hipStream_t)stream, x,
                      B, cx, H, W, mask, cmi, MH, MW, wcond, cmo, (bf16_t*)out, cpad, keep);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -330,7 +376,7 @@ extern "C" int sdmi_prep_input_cmap(const float* x, int B, int cx, int H, int W,
                                     int MH, int MW, const float* wcond, int cmo, void* out, int cpad, const float* keep,
                                     sdmi_stream_t stream) {
   if (cpad % 8 || cx + (cmap ? cmo : 0) > cpad || cpad > 16 || cmi < 1 || cmi > 255) return -1;
-  hipLaunchKernelGGL(prep_input_kernel<true>, dim3(grid_for((long long)B * H * W)), dim3(NT), 0, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(prep_input_kernel<true>, dim3(prep_grid((long long)B * H * W)), dim3(PREP_NT), 0, (hipStream_t)stream, x,
                      B, cx, H, W, cmap, cmi, MH, MW, wcond, cmo, (bf16_t*)out, cpad, keep);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -338,20 +384,13 @@ extern "C" int sdmi_prep_input_cmap(const float* x, int B, int cx, int H, int W,
 
 extern "C" int sdmi_cond_wgrad(const void* dxin, int ld, int cx, int B, int H, int W, const float* mask, int cmi,
                                int MH, int MW, int cmo, float* dw, const float* keep, sdmi_stream_t stream) {
-  hipLaunchKernelGGL(cond_wgrad_kernel<false>, dim3(cmo * cmi), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)dxin, ld,
-                     cx, B, H, W, mask, cmi, MH, MW, dw, keep);
-  SDMI_CHECK_LAUNCH();
-  return 0;
+  return launch_cond_wgrad<false>(dxin, ld, cx, B, H, W, mask, cmi, MH, MW, cmo, dw, keep, (hipStream_t)stream);
 }
 
 extern "C" int sdmi_cond_wgrad_cmap(const void* dxin, int ld, int cx, int B, int H, int W, const unsigned char* cmap,
                                     int cmi, int MH, int MW, int cmo, float* dw, const float* keep,
                                     sdmi_stream_t stream) {
-  if (cmi < 1 || cmi > 255) return -1;
-  hipLaunchKernelGGL(cond_wgrad_kernel<true>, dim3(cmo * cmi), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)dxin, ld,
-                     cx, B, H, W, cmap, cmi, MH, MW, dw, keep);
-  SDMI_CHECK_LAUNCH();
-  return 0;
+  return launch_cond_wgrad<true>(dxin, ld, cx, B, H, W, cmap, cmi, MH, MW, cmo, dw, keep, (hipStream_t)stream);
 }
 
 extern "C" int sdmi_nhwc_to_nchw(const void* src, int src_f32, int ld, int B, int C, int HW, float* dst,
