@@ -27,7 +27,7 @@ constexpr int NT = 256;
 constexpr int NSLOTS = 2048;      // counter slots, one per launch, round-robin
 constexpr int SLOT_CTRS = 2048;   // [0, 1024): per (strip, b) pixel-split counters, [1024, 2048): per strip
 constexpr int BATCH_CTR = 1024;
-constexpr int PS_MAX = 8;         // pixel splits per (strip, b)
+constexpr int PS_MAX = 32;        // pixel splits per (strip, b) (small batches of large images: VQVAE B = 8 at 256^2)
 __device__ unsigned g_norm_counters[NSLOTS * SLOT_CTRS];  // zero at load; the last arriver re-arms
 
 struct StripArgs {
@@ -205,18 +205,21 @@ __device__ __forceinline__ bool combine_psplits(const StripArgs& a, int b, int c
   for (int ch = threadIdx.x; ch < cw; ch += NT) {
     float x1 = 0.f, x2 = 0.f;
     const float* pp = a.part + ((long long)b * nz * a.C + c0 + ch) * 2;
-    float r1[PS_MAX], r2[PS_MAX];  // all splits' loads in flight before the (fixed-order) sum
+    // splits in batches of 8: a batch's loads are in flight together, the sum stays in split order (deterministic)
+    for (int z0 = 0; z0 < nz; z0 += 8) {
+      float r1[8], r2[8];
 #pragma unroll
-    for (int z = 0; z < PS_MAX; ++z) {
-      const int zz = min(z, nz - 1);
-      r1[z] = ld_coherent(pp + (long long)zz * a.C * 2);
-      r2[z] = ld_coherent(pp + (long long)zz * a.C * 2 + 1);
-    }
+      for (int z = 0; z < 8; ++z) {
+        const int zz = min(z0 + z, nz - 1);
+        r1[z] = ld_coherent(pp + (long long)zz * a.C * 2);
+        r2[z] = ld_coherent(pp + (long long)zz * a.C * 2 + 1);
+      }
 #pragma unroll
-    for (int z = 0; z < PS_MAX; ++z) {
-      if (z < nz) {
-        x1 += r1[z];
-        x2 += r2[z];
+      for (int z = 0; z < 8; ++z) {
+        if (z0 + z < nz) {
+          x1 += r1[z];
+          x2 += r2[z];
+        }
       }
     }
     s1[ch] = x1;
