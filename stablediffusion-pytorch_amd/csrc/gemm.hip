@@ -613,7 +613,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_
 // and N = 384 outputs split into 2 (not 3) column tiles, so a 32768 x 384 conv is exactly 512 tiles = one round
 template <int AM, int BMODE, int STAGES, int TBN = BN>
 __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(const Args g, const EpiArgs e) {
-  static_assert(TBN == BN || (TBN == 192 && BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR), "192-column tiles: B_NK");
+  static_assert(TBN == BN || ((TBN == 192 || TBN == 64) && BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR),
+                "64 / 192-column tiles: B_NK");
   constexpr int NJ = TBN / 32;                       // 16-column MFMA tiles per wave
   constexpr int B_BYTES = TBN * BK * 2;              // B tile bytes
   constexpr int STAGE_BYTES = TILE_BYTES + B_BYTES;  // A | B
@@ -797,7 +798,8 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
       // tile t landed for this thread: at most (tiles issued after t) x (4 + NJ) DMA instructions outstanding
       const int after = min(STAGES - 2, nt - 1 - t);
       if (after >= 1) {
-        if constexpr (NJ == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        if constexpr (NJ == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if constexpr (NJ == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
       }
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -947,7 +949,16 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
     const char* s = getenv("SDMI_GEMM_TBN");
     force = s ? atoi(s) : -1;
   }
-  if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR || d->n % 192) return BN;
+  if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR) return BN;
+  // narrow outputs (N <= 64: the VQVAE's 64-channel convs at 256^2, 4-channel heads, DiT proj_out): a 128-column
+  // tile would spend half (or more) of its MFMAs on zero-padded columns (SDMI_GEMM_TBN64=0 disables)
+  static int tbn64 = -1;
+  if (tbn64 < 0) {
+    const char* s = getenv("SDMI_GEMM_TBN64");
+    tbn64 = s ? atoi(s) : 1;
+  }
+  if (tbn64 && d->n <= 64 && force != 128) return 64;
+  if (d->n % 192) return BN;
   if (force == 128 || force == 192) return force;
   if (d->tile_n_hint == 128 || d->tile_n_hint == 192) return d->tile_n_hint;
   const long long mt = (d->m + BM - 1) / BM;
@@ -964,8 +975,11 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, i
   } else if (tbn == BN) {
     hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2>), grid, dim3(NT), 2 * 2 * TILE_BYTES, s, a, e);
   } else if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR) {
-    hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2, 192>), grid, dim3(NT), 2 * (TILE_BYTES + 192 * BK * 2), s, a,
-                       e);
+    if (tbn == 64)
+      hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2, 64>), grid, dim3(NT), 2 * (TILE_BYTES + 64 * BK * 2), s, a, e);
+    else
+      hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2, 192>), grid, dim3(NT), 2 * (TILE_BYTES + 192 * BK * 2), s, a,
+                         e);
   } else {
     return hipErrorInvalidValue;
   }
