@@ -353,12 +353,14 @@ def main():
     steps_per_s = args.steps / elapsed
     state = trainer.state.tolist()
 
-    # dominant-kernel roofline: the implicit-GEMM conv/linear launches of one extra (untimed) step, timed
-    # with HIP events on the stream they run on
+    # dominant-kernel roofline: the implicit-GEMM conv/linear launches of PROF_STEPS extra (untimed) steps, timed
+    # with HIP events on the stream they run on (averaged over the steps: one step's concurrency noise is ~10 %)
     roof = None
     if args.profile_gemm:
+        PROF_STEPS = 3
         K.PROFILE = []
-        eager_step()
+        for _ in range(PROF_STEPS):
+            eager_step()
         torch.cuda.synchronize()
         prof, K.PROFILE = K.PROFILE, None
         by, per_kernel = {}, {}
@@ -391,16 +393,17 @@ def main():
                 "achieved": dfl / (dms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
                 "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic,
                 "traffic_unit": traffic_unit,
-                "launches": dn, "launches_note": "unsplit launches of the kernel in one step (HIP events on its stream)"
-                if use1 else "all launches (each includes its split-K reducer launch)",
+                "launches": dn // PROF_STEPS,
+                "launches_note": f"unsplit launches of the kernel per step (HIP events on its stream, {PROF_STEPS} "
+                                 "profiled steps averaged)" if use1 else "all launches (each includes its split-K reducer)",
                 "avg_launch_us": dms * 1e3 / dn, "flop_per_launch": dfl / dn,
-                "kernel_ms_per_step": d["ms"], "kernel_launches_per_step": d["n"],
-                "all_gemm": {"tflops": tot_fl / (tot_ms * 1e-3) / 1e12, "ms_per_step": tot_ms,
-                             "launches": sum(v[2] for v in by.values())},
-                "per_mode": {k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms": v[1], "launches": v[2]}
-                             for k, v in by.items()},
-                "per_kernel": {k: {"tflops": v["fl"] / (v["ms"] * 1e-3) / 1e12, "ms": v["ms"], "launches": v["n"]}
-                               for k, v in per_kernel.items()}}
+                "kernel_ms_per_step": d["ms"] / PROF_STEPS, "kernel_launches_per_step": d["n"] // PROF_STEPS,
+                "all_gemm": {"tflops": tot_fl / (tot_ms * 1e-3) / 1e12, "ms_per_step": tot_ms / PROF_STEPS,
+                             "launches": sum(v[2] for v in by.values()) // PROF_STEPS},
+                "per_mode": {k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms": v[1] / PROF_STEPS,
+                                 "launches": v[2] // PROF_STEPS} for k, v in by.items()},
+                "per_kernel": {k: {"tflops": v["fl"] / (v["ms"] * 1e-3) / 1e12, "ms": v["ms"] / PROF_STEPS,
+                                   "launches": v["n"] // PROF_STEPS} for k, v in per_kernel.items()}}
 
     FLOP = wl["flop"]
     result = {
