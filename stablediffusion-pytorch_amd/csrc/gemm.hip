@@ -951,13 +951,15 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
   }
   if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR) return BN;
   // narrow outputs (N <= 64: the VQVAE's 64-channel convs at 256^2, 4-channel heads, DiT proj_out): a 128-column
-  // tile would spend half (or more) of its MFMAs on zero-padded columns (SDMI_GEMM_TBN64=0 disables)
+  // tile would spend half (or more) of its MFMAs on zero-padded columns. SDMI_GEMM_TBN64 = the largest N given
+  // 64-column tiles (default 64; 0 disables)
   static int tbn64 = -1;
   if (tbn64 < 0) {
     const char* s = getenv("SDMI_GEMM_TBN64");
-    tbn64 = s ? atoi(s) : 1;
+    tbn64 = s ? atoi(s) : 64;
+    if (tbn64 < 0) tbn64 = 64;
   }
-  if (tbn64 && d->n <= 64 && force != 128) return 64;
+  if (d->n <= tbn64 && force != 128) return 64;
   if (d->n % 192) return BN;
   if (force == 128 || force == 192) return force;
   if (d->tile_n_hint == 128 || d->tile_n_hint == 192) return d->tile_n_hint;
