@@ -960,6 +960,14 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
     if (tbn64 < 0) tbn64 = 64;
   }
   if (d->n <= tbn64 && force != 128) return 64;
+  // ragged N whose last 128-column tile would be at most half used (DiT hidden size 288: 3 x 128 = 384 columns,
+  // 25 % padding; 5 x 64 = 320, 10 %). SDMI_GEMM_TBN64_RAGGED=0 disables.
+  static int ragged = -1;
+  if (ragged < 0) {
+    const char* s = getenv("SDMI_GEMM_TBN64_RAGGED");
+    ragged = s ? atoi(s) : 1;
+  }
+  if (ragged && force != 128 && d->tile_n_hint != 128 && d->n % 128 && d->n % 128 <= 64 && d->n % 192) return 64;
   if (d->n % 192) return BN;
   if (force == 128 || force == 192) return force;
   if (d->tile_n_hint == 128 || d->tile_n_hint == 192) return d->tile_n_hint;
