@@ -50,7 +50,7 @@ typedef struct sdmi_conv_geom {
   /* gathered NHWC input: pixel (b, iy, ix) channel c at x[((b*ih + iy)*iw + ix)*ldx + c] */
   int ih, iw, cin, ldx;
   int kh, kw;           /* taps */
-  int oh_log2, ow_log2; /* GEMM pixel grid (power-of-two) used to decompose a pixel index  */
+  int oh, ow;           /* GEMM pixel grid (any size) used to decompose a pixel index m   */
   int sy, sx, oy0, ox0; /* iy = oy*sy + ty + oy0, ix = ox*sx + tx + ox0 (zero outside)      */
 } sdmi_conv_geom;
 
@@ -60,18 +60,18 @@ typedef struct sdmi_gemm_desc {
   const void* a; int lda; /* bf16 */
   const void* b; int ldb; /* bf16 */
   sdmi_conv_geom geom;    /* used by SDMI_A_CONV / SDMI_B_KN_CONV */
-  /* epilogue: v = alpha*acc + bias[n] + rowbias[(m >> rb_shift)*rb_ld + n] + resid[orow*ldr + n];
+  /* epilogue: v = alpha*acc + bias[n] + rowbias[(m / rb_div)*rb_ld + n] + resid[orow*ldr + n];
    *           v = act(v); C[orow*ldc + ocol] = v   (orow = row remap of m, ocol = col permute of n) */
   void* c; int ldc; int c_f32;
   const float* bias;          /* fp32 [n] or NULL      */
   const void* rowbias;        /* bf16 or NULL           */
-  int rb_ld, rb_shift;
+  int rb_ld, rb_div;          /* rb_div 0 or 1: one rowbias row per output row */
   const void* resid; int ldr; /* bf16 or NULL           */
   float alpha;
   int act;                    /* 0 none, 1 SiLU, 2 ReLU, 3 ReLU-gradient mask (aux) */
   /* row remap (stride-2 sub-pixel phases of a transposed conv): m -> (b, oy, ox) on a
-   * (2^r_gh_log2 x 2^r_gw_log2) grid, orow = (b*r_oh + oy*r_sy + r_oy)*r_ow + ox*r_sx + r_ox */
-  int remap, r_gh_log2, r_gw_log2, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
+   * (r_gh x r_gw) grid, orow = (b*r_oh + oy*r_sy + r_oy)*r_ow + ox*r_sx + r_ox */
+  int remap, r_gh, r_gw, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
   /* column permute (weight-gradient layouts): n = tap*p_cin + c  ->  ocol = c*p_taps + tap (perm 1, torch
    * conv weight layout) or tap*p_cvalid + c (perm 2, tap-major Linear layout of a patch embedding), stored
    * only for c < p_cvalid (0 = all): gradients of zero-padded input channels are dropped */
@@ -83,7 +83,7 @@ typedef struct sdmi_gemm_desc {
    * same pixel grid) -- fuses a 1x1 conv of another tensor into the same GEMM by K-concatenation */
   const void* a2; int lda2; int k_split;
   const float* bias2; /* second fp32 [n] bias added in the epilogue, or NULL */
-  /* rowbias row index = (m >> rb_shift) % rb_mod when rb_mod > 0: a per-token table shared by every
+  /* rowbias row index = (m / rb_div) % rb_mod when rb_mod > 0: a per-token table shared by every
    * sample (the DiT patch position embedding, models/patch_embed.py:93-95) */
   int rb_mod;
   /* act 3 (ReLU backward, models/transformer_layer.py:38-42 / transformer.py:107-111): v is kept where
@@ -291,6 +291,26 @@ int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* 
  * Used for the engine's weight-gradient side stream (SDMI_SIDE_CU=num/den), no reference counterpart. */
 int sdmi_stream_create_cu_share(int keep_num, int keep_den, sdmi_stream_t* out);
 int sdmi_stream_destroy(sdmi_stream_t s);
+
+/* ---------------------------------------------------------------------------------------------
+ * Launch plans (host side of a training / sampling step, no reference counterpart: the reference issues every
+ * aten op from Python per step, train_ddpm_cond_celebhq_multi_gpu.py:299-378). Between sdmi_plan_begin and
+ * sdmi_plan_end every kernel launch of this library executes AND is recorded (kernel, grid, LDS bytes, stream,
+ * a copy of its arguments); the caller notes the event record / stream wait edges it issues itself and numbered
+ * callouts (work outside the library: RCCL collectives, torch copies). sdmi_plan_replay re-issues the recorded
+ * ops from op index `start` until the next callout (*callout = its id, *next = the op after it) or the end
+ * (*callout = -1). Pointers, grids and streams are replayed verbatim: the caller keeps every recorded buffer,
+ * stream and event alive and refills inputs in place. One recorder per process (not re-entrant).
+ * ------------------------------------------------------------------------------------------- */
+int sdmi_plan_begin(void);
+int sdmi_plan_end(void** plan);
+int sdmi_plan_recording(void);
+int sdmi_plan_note_event(void* event, sdmi_stream_t stream);
+int sdmi_plan_note_wait(sdmi_stream_t stream, void* event);
+int sdmi_plan_note_callout(int id);
+int sdmi_plan_info(const void* plan, int* ops, int* launches);
+int sdmi_plan_replay(void* plan, int start, int* callout, int* next);
+int sdmi_plan_destroy(void* plan);
 
 #ifdef __cplusplus
 }

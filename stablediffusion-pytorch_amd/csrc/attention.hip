@@ -539,10 +539,10 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
   dim3 grid((N + ROWS - 1) / ROWS, B * H);
   hipStream_t s = (hipStream_t)stream;
   switch ((d + 15) / 16) {
-    case 1: hipLaunchKernelGGL(attn_fwd_kernel<1>, grid, dim3(NT), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(NT), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(attn_fwd_kernel<3>, grid, dim3(NT), 0, s, a); break;
-    default: hipLaunchKernelGGL(attn_fwd_kernel<4>, grid, dim3(NT), 0, s, a); break;
+    case 1: sdmi_rt::launch(attn_fwd_kernel<1>, grid, dim3(NT), 0, s, a); break;
+    case 2: sdmi_rt::launch(attn_fwd_kernel<2>, grid, dim3(NT), 0, s, a); break;
+    case 3: sdmi_rt::launch(attn_fwd_kernel<3>, grid, dim3(NT), 0, s, a); break;
+    default: sdmi_rt::launch(attn_fwd_kernel<4>, grid, dim3(NT), 0, s, a); break;
   }
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -566,8 +566,8 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
   switch ((d + 15) / 16) {
 #define SDMI_ATTN_BWD(DT)                                            \
   case DT:                                                           \
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<DT>, gq, dim3(NT), 0, s, a);  \
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<DT>, gk, dim3(NT), 0, s, a); \
+    sdmi_rt::launch(attn_bwd_dq_kernel<DT>, gq, dim3(NT), 0, s, a);  \
+    sdmi_rt::launch(attn_bwd_dkv_kernel<DT>, gk, dim3(NT), 0, s, a); \
     break;
     SDMI_ATTN_BWD(1)
     SDMI_ATTN_BWD(2)

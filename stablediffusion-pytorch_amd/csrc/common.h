@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "launch.h"
+
 typedef uint16_t bf16_t;
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -83,6 +85,31 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+
+// Division of a non-negative int (< 2^31) by a runtime constant d >= 1 with one multiply-high and a shift:
+// m = ceil(2^(31+s) / d), s = ceil(log2 d) -> n / d = umulhi(n, m) >> (s - 1) exactly for every n < 2^31
+// (m * d - 2^(31+s) < d and 2^-s <= 1/d bound the error below one); d == 1 is m = 0 (identity).
+// Conv pixel grids of any size (the reference only requires H, W divisible by the down-sampling,
+// utils/config_utils.py:30-31: MNIST's 28x28 -> 7x7 latents) decompose without a hardware divide.
+struct FastDiv {
+  unsigned m;    // 0: d == 1
+  unsigned dsh;  // d | (s - 1) << 24  (d < 2^24)
+  __device__ __forceinline__ unsigned div(unsigned n) const { return m ? (__umulhi(n, m) >> (dsh >> 24)) : n; }
+  __host__ __device__ __forceinline__ int d() const { return (int)(dsh & 0xFFFFFFu); }
+  static FastDiv make(int d) {
+    FastDiv f;
+    if (d <= 1) {
+      f.m = 0;
+      f.dsh = 1;
+      return f;
+    }
+    int s = 0;
+    while ((1LL << s) < d) ++s;
+    f.m = (unsigned)(((1ULL << (31 + s)) + (unsigned long long)d - 1) / (unsigned long long)d);
+    f.dsh = (unsigned)d | ((unsigned)(s - 1) << 24);
+    return f;
+  }
+};
 
 #define SDMI_CHECK_LAUNCH()                                  \
   do {                                                       \

@@ -361,9 +361,9 @@ extern "C" int sdmi_ln_mod_fwd(const void* x, int ldx, const void* v, int ldv, c
   a.rpw = rpw;
   const int per = WAVES * rpw;
   if (x_f32)
-    hipLaunchKernelGGL(ln_mod_fwd_kernel<true>, dim3((rows + per - 1) / per), dim3(NT), 0, (hipStream_t)stream, a);
+    sdmi_rt::launch(ln_mod_fwd_kernel<true>, dim3((rows + per - 1) / per), dim3(NT), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(ln_mod_fwd_kernel<false>, dim3((rows + per - 1) / per), dim3(NT), 0, (hipStream_t)stream, a);
+    sdmi_rt::launch(ln_mod_fwd_kernel<false>, dim3((rows + per - 1) / per), dim3(NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -388,9 +388,9 @@ extern "C" int sdmi_ln_mod_bwd(const void* x, int ldx, const float* mean, const 
   a.pg = gate ? pg : nullptr;
   a.rows = rows; a.C = C; a.N = N; a.R = sdmi_ln_chunk_rows(N);
   if (x_f32)
-    hipLaunchKernelGGL(ln_mod_bwd_kernel<true>, dim3(rows / a.R), dim3(NT), 0, (hipStream_t)stream, a);
+    sdmi_rt::launch(ln_mod_bwd_kernel<true>, dim3(rows / a.R), dim3(NT), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(ln_mod_bwd_kernel<false>, dim3(rows / a.R), dim3(NT), 0, (hipStream_t)stream, a);
+    sdmi_rt::launch(ln_mod_bwd_kernel<false>, dim3(rows / a.R), dim3(NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -398,7 +398,7 @@ extern "C" int sdmi_ln_mod_bwd(const void* x, int ldx, const float* mean, const 
 extern "C" int sdmi_mod_finalize(const float* ws, int B, int chunks, int ws_ld, int W, void* out, int ldo,
                                  sdmi_stream_t stream) {
   if (B <= 0 || chunks <= 0 || W <= 0 || ws_ld < W || ldo < W) return -1;
-  hipLaunchKernelGGL(mod_finalize_kernel, dim3(grid_for((long long)B * W)), dim3(256), 0, (hipStream_t)stream, ws, B,
+  sdmi_rt::launch(mod_finalize_kernel, dim3(grid_for((long long)B * W)), dim3(256), 0, (hipStream_t)stream, ws, B,
                      chunks, ws_ld, W, (bf16_t*)out, ldo);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -408,7 +408,7 @@ extern "C" int sdmi_tokens_to_nchw(const void* src, int src_f32, int ld, int B, 
                                    sdmi_stream_t stream) {
   if (B <= 0 || C <= 0 || p <= 0 || H % p || W % p || ld < p * p * C) return -1;
   const long long total = (long long)B * H * W * C;
-  hipLaunchKernelGGL(tokens_to_nchw_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, src_f32, ld,
+  sdmi_rt::launch(tokens_to_nchw_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, src_f32, ld,
                      B, C, H, W, p, dst);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -418,7 +418,7 @@ extern "C" int sdmi_nchw_to_tokens_bf16(const float* src, int B, int C, int H, i
                                         sdmi_stream_t stream) {
   if (B <= 0 || C <= 0 || p <= 0 || H % p || W % p || ld < p * p * C) return -1;
   const long long total = (long long)B * (H / p) * (W / p) * ld;
-  hipLaunchKernelGGL(nchw_to_tokens_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, B, C, H, W,
+  sdmi_rt::launch(nchw_to_tokens_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, src, B, C, H, W,
                      p, (bf16_t*)dst, ld);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -430,10 +430,10 @@ extern "C" int sdmi_mse_patch(const float* pred, int ld, const float* target, in
   if (B <= 0 || C <= 0 || p <= 0 || H % p || W % p || ld < p * p * C) return -1;
   const long long total = (long long)B * (H / p) * (W / p) * ld;
   const int blocks = (int)std::min<long long>((total + NT - 1) / NT, 1024);  // ws: sdmi_mse_workspace() floats
-  hipLaunchKernelGGL(mse_patch_kernel, dim3(blocks), dim3(NT), 0, (hipStream_t)stream, pred, ld, target, B, C, H, W, p,
+  sdmi_rt::launch(mse_patch_kernel, dim3(blocks), dim3(NT), 0, (hipStream_t)stream, pred, ld, target, B, C, H, W, p,
                      gscale, gscale_dev, (bf16_t*)grad, ws);
   SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(NT), 0, (hipStream_t)stream, ws, blocks,
+  sdmi_rt::launch(sum_rows_kernel, dim3(1), dim3(NT), 0, (hipStream_t)stream, ws, blocks,
                      1.0f / (float)((long long)B * C * H * W), loss);
   SDMI_CHECK_LAUNCH();
   return 0;

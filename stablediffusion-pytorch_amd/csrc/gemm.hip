@@ -35,19 +35,30 @@ struct Args {
   const bf16_t* A; int lda;
   const bf16_t* B; int ldb;
   // gather geometry
-  int ih, iw, cin, ldx, kw, ohl, owl, sy, sx, oy0, ox0;
+  int ih, iw, cin, ldx, kw, sy, sx, oy0, ox0;
+  FastDiv ohw_d, ow_d;  // GEMM pixel grid: pixel m -> (b, oy, ox) = (m / (oh*ow), (m % (oh*ow)) / ow, m % ow)
   int ktiles_per_split, nsplit;
   const bf16_t* A2; int lda2; int k_split;
 };
+
+__device__ __forceinline__ void pixel_coords(const Args& g, int m, int& b, int& oy, int& ox) {
+  b = (int)g.ohw_d.div((unsigned)m);
+  const int r = m - b * g.ohw_d.d();
+  oy = (int)g.ow_d.div((unsigned)r);
+  ox = r - oy * g.ow_d.d();
+}
 
 // epilogue parameters (a separate kernel argument keeps both structs small enough to stay in SGPRs)
 struct EpiArgs {
   int M, N;
   void* C; int ldc; int c_f32; long long split_stride;
-  const float* bias; const float* bias2; const bf16_t* rowbias; int rb_ld, rb_shift;
+  const float* bias; const float* bias2; const bf16_t* rowbias; int rb_ld;
   const bf16_t* resid; int ldr;
   float alpha; int act;
-  int remap, r_ghl, r_gwl, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
+  int remap, r_oh, r_ow, r_sy, r_sx, r_oy, r_ox;
+  // output-row grid of the GEMM: rows per sample (the rowbias row divisor, and gh * gw of a remap) and the remap's
+  // grid width gw (fill_args rejects a remap whose rowbias divisor differs)
+  FastDiv pix_d, gw_d;
   int perm, p_cin, p_taps, p_cvalid;
   unsigned p_magic;   // ceil(2^32 / p_cin): tap = umulhi(col, p_magic), exact for col < 2^32 / p_cin
   unsigned n8_magic;  // ceil(2^32 / (N / 8)) for the reducer's row split (0: N / 8 == 1)
@@ -58,12 +69,12 @@ struct EpiArgs {
   unsigned* counters;  // per-tile arrival counters: the last split of a tile reduces it (0: separate reducer)
   int vec;          // LDS-staged 16-B row stores (no column permute, 8-aligned columns/strides)
   int n8;           // N % 8 == 0: split-K slabs are written / read as 16-B rows even when !vec
-  int rb_mod;       // rowbias row = (row >> rb_shift) % rb_mod when > 0 (per-token tables, e.g. position embedding)
+  int rb_mod;       // rowbias row = (row / rb_div) % rb_mod when > 0 (per-token tables, e.g. position embedding)
   const bf16_t* aux; int ld_aux;  // act 3: ReLU-gradient mask source (aux[orow*ld_aux + col] > 0)
 };
 
 __device__ __forceinline__ long long rb_row(const EpiArgs& g, int row) {
-  long long r = row >> g.rb_shift;
+  long long r = g.pix_d.div((unsigned)row);
   return g.rb_mod > 0 ? r % g.rb_mod : r;
 }
 
@@ -88,9 +99,10 @@ struct Epi {
     if (g.rowbias) v += bf2f(g.rowbias[rb_row(g, row) * g.rb_ld + col]);
     long long orow = row;
     if (g.remap) {
-      int b = row >> (g.r_ghl + g.r_gwl);
-      int oy = (row >> g.r_gwl) & ((1 << g.r_ghl) - 1);
-      int ox = row & ((1 << g.r_gwl) - 1);
+      const int b = (int)g.pix_d.div((unsigned)row);
+      const int rr = row - b * g.pix_d.d();
+      const int oy = (int)g.gw_d.div((unsigned)rr);
+      const int ox = rr - oy * g.gw_d.d();
       orow = ((long long)b * g.r_oh + oy * g.r_sy + g.r_oy) * g.r_ow + ox * g.r_sx + g.r_ox;
     }
     if (g.resid) v += bf2f(g.resid[orow * g.ldr + col]);
@@ -126,9 +138,10 @@ struct Epi {
     }
     long long orow = row;
     if (g.remap) {
-      int b = row >> (g.r_ghl + g.r_gwl);
-      int oy = (row >> g.r_gwl) & ((1 << g.r_ghl) - 1);
-      int ox = row & ((1 << g.r_gwl) - 1);
+      const int b = (int)g.pix_d.div((unsigned)row);
+      const int rr = row - b * g.pix_d.d();
+      const int oy = (int)g.gw_d.div((unsigned)rr);
+      const int ox = rr - oy * g.gw_d.d();
       orow = ((long long)b * g.r_oh + oy * g.r_sy + g.r_oy) * g.r_ow + ox * g.r_sx + g.r_ox;
     }
     if (g.resid) {
@@ -175,9 +188,10 @@ struct Epi {
     if (g.rowbias) v += bf2f(g.rowbias[rb_row(g, row) * g.rb_ld + col]);
     long long orow = row;
     if (g.remap) {
-      int b = row >> (g.r_ghl + g.r_gwl);
-      int oy = (row >> g.r_gwl) & ((1 << g.r_ghl) - 1);
-      int ox = row & ((1 << g.r_gwl) - 1);
+      const int b = (int)g.pix_d.div((unsigned)row);
+      const int rr = row - b * g.pix_d.d();
+      const int oy = (int)g.gw_d.div((unsigned)rr);
+      const int ox = rr - oy * g.gw_d.d();
       orow = ((long long)b * g.r_oh + oy * g.r_sy + g.r_oy) * g.r_ow + ox * g.r_sx + g.r_ox;
     }
     if (g.resid) v += bf2f(g.resid[orow * g.ldr + col]);
@@ -200,87 +214,59 @@ template <int TBN = BN>
 __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][TBN / 32], char* smem, int m0, int n0,
                                               int wm, int wn, int lane, int z) {
   constexpr int NJ = TBN / 32;  // 16-column MFMA tiles per wave
-  // ---------------- epilogue ----------------
-  if (e.vec || (e.raw && e.n8)) {
-    // Stage the fp32 tile through LDS in two 64-row halves and write whole rows with 16-B stores
-    // (8 bf16 or 4 fp32 per lane) instead of 64 scattered 2-byte stores per lane.
-    float* st = (float*)smem;  // [64][SROW] fp32, 33 KB (TBN 128) / 49 KB (TBN 192)
-    constexpr int SROW = TBN + 4;  // +4 floats: lanes of one ds_write hit distinct banks
+  // Stage the fp32 tile through LDS in two 64-row halves; each thread then owns runs of 8 consecutive columns of one
+  // row: 16-B stores (8 bf16 or 2 x 4 fp32) on the aligned paths, and a ROLLED per-element loop on the rare general
+  // path (column permutes of weight gradients, unaligned outputs) instead of 4 x NJ x 4 unrolled scattered stores,
+  // whose code and register footprint pushed the 192-column tile's accumulators to scratch.
+  float* st = (float*)smem;      // [64][SROW] fp32, 33 KB (TBN 128) / 49 KB (TBN 192)
+  constexpr int SROW = TBN + 4;  // +4 floats: lanes of one ds_write hit distinct banks
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (wm == half * 64) {
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half * 64) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int cl = wn + 16 * j + (lane & 15);
+      for (int j = 0; j < NJ; ++j) {
+        const int cl = wn + 16 * j + (lane & 15);
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) st[(16 * i + 4 * (lane >> 4) + r) * SROW + cl] = acc[i][j][r];
-        }
+          for (int r = 0; r < 4; ++r) st[(16 * i + 4 * (lane >> 4) + r) * SROW + cl] = acc[i][j][r];
       }
-      __syncthreads();
-#pragma unroll
-      for (int it = 0; it < TBN / 32; ++it) {  // 64 rows x TBN/8 chunks of 8 columns
-        const int ch = threadIdx.x + it * NT;
-        const int rl = ch / (TBN / 8), c8 = (ch - rl * (TBN / 8)) * 8;
-        const int row = m0 + half * 64 + rl, col = n0 + c8;
-        float v[8];
-        const float4 lo = *(const float4*)(st + rl * SROW + c8), hi = *(const float4*)(st + rl * SROW + c8 + 4);
-        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-        if (e.raw) {
-          if (row < e.M && col < e.N) {
-            // device-coherent (sc1) stores: the tile's last split may run on another XCD
-            const int off = (int)(((long long)z * e.split_stride + (long long)row * e.N + col) * 4);
-            const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), rw, off, 0, CPOL_SC1);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), rw, off + 16, 0, CPOL_SC1);
-          }
-        } else if (row < e.m_store && col < e.n_store) {
-          Epi::finish8(e, row, col, v);
-        }
-      }
-      __syncthreads();
     }
-    return;
-  }
-  if (e.raw) {  // split-K slab: raw fp32 partials, the reducer applies the epilogue
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
-    const long long zoff = (long long)z * e.split_stride;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int col = n0 + wn + 16 * j + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const f32x4 v = acc[i][j];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
-          if (row < e.M && col < e.N)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), rw,
-                                                  (int)((zoff + (long long)row * e.N + col) * 4), 0, CPOL_SC1);
+    __syncthreads();
+#pragma unroll 1
+    for (int it = 0; it < TBN / 32; ++it) {  // 64 rows x TBN/8 chunks of 8 columns
+      const int ch = threadIdx.x + it * NT;
+      const int rl = ch / (TBN / 8), c8 = (ch - rl * (TBN / 8)) * 8;
+      const int row = m0 + half * 64 + rl, col = n0 + c8;
+      float v[8];
+      const float4 lo = *(const float4*)(st + rl * SROW + c8), hi = *(const float4*)(st + rl * SROW + c8 + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      if (e.raw) {
+        if (row >= e.M || col >= e.N) continue;
+        // split-K slab, device-coherent (sc1) stores: the tile's last split may run on another XCD
+        const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
+        const int off = (int)(((long long)z * e.split_stride + (long long)row * e.N + col) * 4);
+        if (e.n8) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), rw, off, 0, CPOL_SC1);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), rw, off + 16, 0, CPOL_SC1);
+        } else {
+#pragma unroll 1
+          for (int q = 0; q < 8 && col + q < e.N; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), rw, off + 4 * q, 0, CPOL_SC1);
+        }
+      } else if (e.vec) {
+        if (row < e.m_store && col < e.n_store) Epi::finish8(e, row, col, v);
+      } else if (row < e.m_store) {
+#pragma unroll 1
+        for (int q = 0; q < 8 && col + q < e.n_store; ++q) {
+          float b = 0.f;
+          if (e.bias) b += e.bias[col + q];
+          if (e.bias2) b += e.bias2[col + q];
+          Epi::finish(e, row, col + q, e.alpha * v[q] + b);
         }
       }
     }
-  } else {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int col = n0 + wn + 16 * j + (lane & 15);
-      const bool cok = col < e.n_store;
-      float bsum = 0.f;
-      if (cok) {
-        if (e.bias) bsum += e.bias[col];
-        if (e.bias2) bsum += e.bias2[col];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const f32x4 v = acc[i][j];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
-          if (cok && row < e.m_store) Epi::finish(e, row, col, e.alpha * v[r] + bsum);
-        }
-      }
-    }
+    __syncthreads();
   }
 }
 
@@ -394,9 +380,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
     for (int i = 0; i < 4; ++i) {
       int m = m0 + (tid >> 3) + 32 * i;
       a_ok[i] = m < g.M;
-      int b = m >> (g.ohl + g.owl);
-      int oy = (m >> g.owl) & ((1 << g.ohl) - 1);
-      int ox = m & ((1 << g.owl) - 1);
+      int b, oy, ox;
+      pixel_coords(g, m, b, oy, ox);
       a_pb[i] = b * g.ih;
       a_iy[i] = oy * g.sy + g.oy0;
       a_ix[i] = ox * g.sx + g.ox0;
@@ -488,9 +473,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int p = k0 + (tid >> 4) + 16 * i;
-        int b = p >> (g.ohl + g.owl);
-        int oy = (p >> g.owl) & ((1 << g.ohl) - 1);
-        int ox = p & ((1 << g.owl) - 1);
+        int b, oy, ox;
+        pixel_coords(g, p, b, oy, ox);
         int iy = oy * g.sy + g.oy0 + b_ty, ix = ox * g.sx + g.ox0 + b_tx;
         bool ok = b_nok && p < g.K && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
         int off = ok ? (((b * g.ih + iy) * g.iw + ix) * g.ldx + b_ci) * 2 : OOB;
@@ -663,9 +647,8 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
       if (AM == SDMI_A_ROWMAJOR) {
         a_base[j] = m * g.lda;
       } else {
-        int b = m >> (g.ohl + g.owl);
-        int oy = (m >> g.owl) & ((1 << g.ohl) - 1);
-        int ox = m & ((1 << g.owl) - 1);
+        int b, oy, ox;
+        pixel_coords(g, m, b, oy, ox);
         a_pb[j] = b * g.ih;
         a_iy[j] = oy * g.sy + g.oy0;
         a_ix[j] = ox * g.sx + g.ox0;
@@ -771,9 +754,8 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
         off = (b_ok[j] && k < g.K) ? (k * g.ldb + b_base[j]) * 2 : OOB;
       } else {
         int p = k0 + b_kk[j];
-        int b = p >> (g.ohl + g.owl);
-        int oy = (p >> g.owl) & ((1 << g.ohl) - 1);
-        int ox = p & ((1 << g.owl) - 1);
+        int b, oy, ox;
+        pixel_coords(g, p, b, oy, ox);
         int iy = oy * g.sy + g.oy0 + b_ty[j], ix = ox * g.sx + g.ox0 + b_tx[j];
         bool ok = b_ok[j] && p < g.K && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
         off = ok ? (((b * g.ih + iy) * g.iw + ix) * g.ldx + b_base[j]) * 2 : OOB;
@@ -901,7 +883,7 @@ __global__ void splitk_reduce_kernel(const EpiArgs g) {
 hipError_t launch_reduce(const EpiArgs& red, hipStream_t s) {
   if (!red.n8) {
     const long long total = (long long)red.M * red.N;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096)), dim3(256),
+    sdmi_rt::launch(splitk_reduce_kernel, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096)), dim3(256),
                        0, s, red);
     return hipGetLastError();
   }
@@ -910,12 +892,12 @@ hipError_t launch_reduce(const EpiArgs& red, hipStream_t s) {
   while (sl < 32 && sl * 2 <= red.nsplit && items * sl / 256 < 1024) sl *= 2;
   const unsigned blocks = (unsigned)std::min<long long>((items * sl + 255) / 256, 8192);
   switch (sl) {
-    case 1: hipLaunchKernelGGL(splitk_reduce_n8_kernel<1>, dim3(blocks), dim3(256), 0, s, red); break;
-    case 2: hipLaunchKernelGGL(splitk_reduce_n8_kernel<2>, dim3(blocks), dim3(256), 0, s, red); break;
-    case 4: hipLaunchKernelGGL(splitk_reduce_n8_kernel<4>, dim3(blocks), dim3(256), 0, s, red); break;
-    case 8: hipLaunchKernelGGL(splitk_reduce_n8_kernel<8>, dim3(blocks), dim3(256), 0, s, red); break;
-    case 16: hipLaunchKernelGGL(splitk_reduce_n8_kernel<16>, dim3(blocks), dim3(256), 0, s, red); break;
-    default: hipLaunchKernelGGL(splitk_reduce_n8_kernel<32>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 1: sdmi_rt::launch(splitk_reduce_n8_kernel<1>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 2: sdmi_rt::launch(splitk_reduce_n8_kernel<2>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 4: sdmi_rt::launch(splitk_reduce_n8_kernel<4>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 8: sdmi_rt::launch(splitk_reduce_n8_kernel<8>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 16: sdmi_rt::launch(splitk_reduce_n8_kernel<16>, dim3(blocks), dim3(256), 0, s, red); break;
+    default: sdmi_rt::launch(splitk_reduce_n8_kernel<32>, dim3(blocks), dim3(256), 0, s, red); break;
   }
   return hipGetLastError();
 }
@@ -979,16 +961,16 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
 template <int AM, int BMODE>
 hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
   if (v == 0) {
-    hipLaunchKernelGGL((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
+    sdmi_rt::launch((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
   } else if (v == 3) {
-    hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 3>), grid, dim3(NT), 3 * 2 * TILE_BYTES, s, a, e);
+    sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, 3>), grid, dim3(NT), 3 * 2 * TILE_BYTES, s, a, e);
   } else if (tbn == BN) {
-    hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2>), grid, dim3(NT), 2 * 2 * TILE_BYTES, s, a, e);
+    sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, 2>), grid, dim3(NT), 2 * 2 * TILE_BYTES, s, a, e);
   } else if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR) {
     if (tbn == 64)
-      hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2, 64>), grid, dim3(NT), 2 * (TILE_BYTES + 64 * BK * 2), s, a, e);
+      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, 2, 64>), grid, dim3(NT), 2 * (TILE_BYTES + 64 * BK * 2), s, a, e);
     else
-      hipLaunchKernelGGL((gemm_dma_kernel<AM, BMODE, 2, 192>), grid, dim3(NT), 2 * (TILE_BYTES + 192 * BK * 2), s, a,
+      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, 2, 192>), grid, dim3(NT), 2 * (TILE_BYTES + 192 * BK * 2), s, a,
                          e);
   } else {
     return hipErrorInvalidValue;
@@ -1042,17 +1024,23 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   a.A = (const bf16_t*)d->a; a.lda = d->lda;
   a.B = (const bf16_t*)d->b; a.ldb = d->ldb;
   a.ih = d->geom.ih; a.iw = d->geom.iw; a.cin = d->geom.cin; a.ldx = d->geom.ldx; a.kw = d->geom.kw;
-  a.ohl = d->geom.oh_log2; a.owl = d->geom.ow_log2;
+  if ((d->a_mode == SDMI_A_CONV || d->b_mode == SDMI_B_KN_CONV) && (d->geom.oh <= 0 || d->geom.ow <= 0)) return -5;
+  a.ohw_d = FastDiv::make(std::max(1, d->geom.oh * d->geom.ow));
+  a.ow_d = FastDiv::make(std::max(1, d->geom.ow));
   a.sy = d->geom.sy; a.sx = d->geom.sx; a.oy0 = d->geom.oy0; a.ox0 = d->geom.ox0;
   a.A2 = (const bf16_t*)d->a2; a.lda2 = d->lda2;
   a.k_split = (d->a_mode == SDMI_A_CONV && d->a2) ? d->k_split : d->k;
   e.M = d->m; e.N = d->n;
   e.C = d->c; e.ldc = d->ldc; e.c_f32 = d->c_f32;
   e.bias = d->bias; e.bias2 = d->bias2;
-  e.rowbias = (const bf16_t*)d->rowbias; e.rb_ld = d->rb_ld; e.rb_shift = d->rb_shift;
+  e.rowbias = (const bf16_t*)d->rowbias; e.rb_ld = d->rb_ld;
   e.resid = (const bf16_t*)d->resid; e.ldr = d->ldr;
   e.alpha = d->alpha; e.act = d->act;
-  e.remap = d->remap; e.r_ghl = d->r_gh_log2; e.r_gwl = d->r_gw_log2; e.r_oh = d->r_oh; e.r_ow = d->r_ow;
+  e.remap = d->remap; e.r_oh = d->r_oh; e.r_ow = d->r_ow;
+  if (d->remap && (d->r_gh <= 0 || d->r_gw <= 0)) return -11;
+  if (d->remap && d->rowbias && std::max(1, d->rb_div) != d->r_gh * d->r_gw) return -12;
+  e.pix_d = FastDiv::make(d->remap ? d->r_gh * d->r_gw : std::max(1, d->rb_div));
+  e.gw_d = FastDiv::make(d->remap ? d->r_gw : 1);
   e.r_sy = d->r_sy; e.r_sx = d->r_sx; e.r_oy = d->r_oy; e.r_ox = d->r_ox;
   e.perm = d->perm; e.p_cin = d->p_cin; e.p_taps = d->p_taps;
   if (d->perm && (d->p_cin < 8 || d->p_cin % 8)) return -10;

@@ -121,10 +121,10 @@ int launch_cond_wgrad(const void* dxin, int ld, int cx, int B, int H, int W, con
                       int cmo, float* dw, const float* keep, hipStream_t s) {
   if (cmo < 1 || cmo > 16 || cmi < 1 || cmi > 255) return -1;
   const int slot = cw_slot();
-  hipLaunchKernelGGL(cond_wgrad_kernel<CMAP>, dim3(cmo * cmi, CW_SPLITS), dim3(NT), 0, s, (const bf16_t*)dxin, ld, cx,
+  sdmi_rt::launch(cond_wgrad_kernel<CMAP>, dim3(cmo * cmi, CW_SPLITS), dim3(NT), 0, s, (const bf16_t*)dxin, ld, cx,
                      B, H, W, mask, cmi, MH, MW, slot, keep);
   SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(cond_wgrad_finish_kernel, dim3((cmo * cmi + NT - 1) / NT), dim3(NT), 0, s, cmo * cmi, slot, dw);
+  sdmi_rt::launch(cond_wgrad_finish_kernel, dim3((cmo * cmi + NT - 1) / NT), dim3(NT), 0, s, cmo * cmi, slot, dw);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(NT) void pack_transpose_kernel(const sdmi_tpack_des
 extern "C" int sdmi_pack_transpose(const sdmi_tpack_desc* descs_dev, const void* bmap_dev, int nblocks,
                                    sdmi_stream_t stream) {
   if (nblocks <= 0) return 0;
-  hipLaunchKernelGGL(pack_transpose_kernel, dim3(nblocks), dim3(NT), 0, (hipStream_t)stream, descs_dev,
+  sdmi_rt::launch(pack_transpose_kernel, dim3(nblocks), dim3(NT), 0, (hipStream_t)stream, descs_dev,
                      (const int4*)bmap_dev);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -366,7 +366,7 @@ extern "C" int sdmi_prep_input(const float* x, int B, int cx, int H, int W, cons
                                const float* wcond, int cmo, void* out, int cpad, const float* keep,
                                sdmi_stream_t stream) {
   if (cpad % 8 || cx + (mask ? cmo : 0) > cpad || cpad > 16) return -1;
-  hipLaunchKernelGGL(prep_input_kernel<false>, dim3(prep_grid((long long)B * H * W)), dim3(PREP_NT), 0, (hipStream_t)stream, x,
+  sdmi_rt::launch(prep_input_kernel<false>, dim3(prep_grid((long long)B * H * W)), dim3(PREP_NT), 0, (hipStream_t)stream, x,
                      B, cx, H, W, mask, cmi, MH, MW, wcond, cmo, (bf16_t*)out, cpad, keep);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -376,7 +376,7 @@ extern "C" int sdmi_prep_input_cmap(const float* x, int B, int cx, int H, int W,
                                     int MH, int MW, const float* wcond, int cmo, void* out, int cpad, const float* keep,
                                     sdmi_stream_t stream) {
   if (cpad % 8 || cx + (cmap ? cmo : 0) > cpad || cpad > 16 || cmi < 1 || cmi > 255) return -1;
-  hipLaunchKernelGGL(prep_input_kernel<true>, dim3(prep_grid((long long)B * H * W)), dim3(PREP_NT), 0, (hipStream_t)stream, x,
+  sdmi_rt::launch(prep_input_kernel<true>, dim3(prep_grid((long long)B * H * W)), dim3(PREP_NT), 0, (hipStream_t)stream, x,
                      B, cx, H, W, cmap, cmi, MH, MW, wcond, cmo, (bf16_t*)out, cpad, keep);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -395,14 +395,14 @@ extern "C" int sdmi_cond_wgrad_cmap(const void* dxin, int ld, int cx, int B, int
 
 extern "C" int sdmi_nhwc_to_nchw(const void* src, int src_f32, int ld, int B, int C, int HW, float* dst,
                                  sdmi_stream_t stream) {
-  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(grid_for((long long)B * C * HW)), dim3(NT), 0, (hipStream_t)stream, src,
+  sdmi_rt::launch(nhwc_to_nchw_kernel, dim3(grid_for((long long)B * C * HW)), dim3(NT), 0, (hipStream_t)stream, src,
                      src_f32, ld, B, C, HW, dst);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int sdmi_nchw_to_nhwc_bf16(const float* src, int B, int C, int HW, void* dst, int ld, sdmi_stream_t stream) {
-  hipLaunchKernelGGL(nchw_to_nhwc_bf16_kernel, dim3(grid_for((long long)B * HW * ld)), dim3(NT), 0, (hipStream_t)stream,
+  sdmi_rt::launch(nchw_to_nhwc_bf16_kernel, dim3(grid_for((long long)B * HW * ld)), dim3(NT), 0, (hipStream_t)stream,
                      src, B, C, HW, (bf16_t*)dst, ld);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -411,7 +411,7 @@ extern "C" int sdmi_nchw_to_nhwc_bf16(const float* src, int B, int C, int HW, vo
 extern "C" int sdmi_add_noise(const float* x0, const float* eps, const long long* t, const float* sqrt_abar,
                               const float* sqrt_one_minus_abar, int B, long long per_sample, float* out,
                               sdmi_stream_t stream) {
-  hipLaunchKernelGGL(add_noise_kernel, dim3(grid_for((long long)B * per_sample)), dim3(NT), 0, (hipStream_t)stream, x0,
+  sdmi_rt::launch(add_noise_kernel, dim3(grid_for((long long)B * per_sample)), dim3(NT), 0, (hipStream_t)stream, x0,
                      eps, t, sqrt_abar, sqrt_one_minus_abar, B, per_sample, out);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -424,10 +424,10 @@ extern "C" int sdmi_mse(const float* pred, int ld, const float* target, int B, i
   hipStream_t s = (hipStream_t)stream;
   int blocks = grid_for((long long)B * HW * ld);
   if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(mse_kernel, dim3(blocks), dim3(NT), 0, s, pred, ld, target, B, C, HW, gscale, gscale_dev,
+  sdmi_rt::launch(mse_kernel, dim3(blocks), dim3(NT), 0, s, pred, ld, target, B, C, HW, gscale, gscale_dev,
                      (bf16_t*)grad, ws);
   SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(NT), 0, s, ws, blocks, 1.0f / (float)((long long)B * C * HW),
+  sdmi_rt::launch(sum_partials_kernel, dim3(1), dim3(NT), 0, s, ws, blocks, 1.0f / (float)((long long)B * C * HW),
                      loss);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -436,14 +436,14 @@ extern "C" int sdmi_mse(const float* pred, int ld, const float* target, int B, i
 extern "C" int sdmi_time_embedding(const long long* t, int tstride, int B, int dim, void* out, int ld, float* out_f32,
                                    sdmi_stream_t stream) {
   if (dim % 2) return -1;
-  hipLaunchKernelGGL(time_embedding_kernel, dim3(grid_for((long long)B * dim / 2)), dim3(NT), 0, (hipStream_t)stream, t,
+  sdmi_rt::launch(time_embedding_kernel, dim3(grid_for((long long)B * dim / 2)), dim3(NT), 0, (hipStream_t)stream, t,
                      tstride, B, dim, (bf16_t*)out, ld, out_f32);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int sdmi_silu(const void* x, const void* dy, void* y, long long n, sdmi_stream_t stream) {
-  hipLaunchKernelGGL(silu_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)x,
+  sdmi_rt::launch(silu_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)x,
                      (const bf16_t*)dy, (bf16_t*)y, n);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -452,7 +452,7 @@ extern "C" int sdmi_silu(const void* x, const void* dy, void* y, long long n, sd
 extern "C" int sdmi_copy_slice(const void* src, int lds, void* dst, int ldd, long long P, int C, int accumulate,
                                sdmi_stream_t stream) {
   if (C % 8 || lds % 8 || ldd % 8) return -1;
-  hipLaunchKernelGGL(copy_slice_kernel, dim3(grid_for(P * C / 8)), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)src,
+  sdmi_rt::launch(copy_slice_kernel, dim3(grid_for(P * C / 8)), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)src,
                      lds, (bf16_t*)dst, ldd, P, C, accumulate);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -463,7 +463,7 @@ extern "C" int sdmi_pack_chunk(void) { return PACK_CHUNK; }
 // descs_dev: device array of descriptors; bmap_dev: device array of int2 (descriptor, chunk), one per workgroup
 extern "C" int sdmi_pack_weights(const sdmi_pack_desc* descs_dev, const void* bmap_dev, int nblocks, sdmi_stream_t stream) {
   if (nblocks <= 0) return 0;
-  hipLaunchKernelGGL(pack_kernel, dim3(nblocks), dim3(NT), PACK_LDS_ELEMS * sizeof(bf16_t), (hipStream_t)stream, descs_dev,
+  sdmi_rt::launch(pack_kernel, dim3(nblocks), dim3(NT), PACK_LDS_ELEMS * sizeof(bf16_t), (hipStream_t)stream, descs_dev,
                      (const int2*)bmap_dev);
   SDMI_CHECK_LAUNCH();
   return 0;

@@ -729,7 +729,7 @@ extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G,
     a.part = part_base(ws, B, C);
     if (!(a.ctr = counter_slot())) return -4;
   }
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(nch, B, ps), dim3(NT), 0, (hipStream_t)stream, a);
+  sdmi_rt::launch(gn_stats_kernel, dim3(nch, B, ps), dim3(NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -746,9 +746,9 @@ extern "C" int sdmi_gn_fwd(const void* x, int ldx, void* y, int ldy, int B, int 
     a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table; a.CW = cw;
     const dim3 grid((C + cw - 1) / cw, B);
     if (nth == 256)
-      hipLaunchKernelGGL(gn_fwd_pass_kernel<256>, grid, dim3(256), 0, (hipStream_t)stream, a, (bf16_t*)y, ldy);
+      sdmi_rt::launch(gn_fwd_pass_kernel<256>, grid, dim3(256), 0, (hipStream_t)stream, a, (bf16_t*)y, ldy);
     else
-      hipLaunchKernelGGL(gn_fwd_pass_kernel<1024>, grid, dim3(1024), 0, (hipStream_t)stream, a, (bf16_t*)y, ldy);
+      sdmi_rt::launch(gn_fwd_pass_kernel<1024>, grid, dim3(1024), 0, (hipStream_t)stream, a, (bf16_t*)y, ldy);
     SDMI_CHECK_LAUNCH();
     return 0;
   }
@@ -763,7 +763,7 @@ extern "C" int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const flo
   ApplyArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.y = (bf16_t*)y; a.ldy = ldy;
   a.tab = (const float4*)table; a.B = B; a.P = P; a.C = C; a.silu = silu;
-  hipLaunchKernelGGL(gn_apply_kernel, apply_grid(B, P, C), dim3(NT), 0, (hipStream_t)stream, a);
+  sdmi_rt::launch(gn_apply_kernel, apply_grid(B, P, C), dim3(NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -785,10 +785,10 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   if (const int nth = gn_pass_threads_for(P, r.CW, nch, B)) {  // single pass
     if (dgamma && !(r.ctr = counter_slot())) return -4;
     if (nth == 256)
-      hipLaunchKernelGGL(gn_bwd_pass_kernel<256>, dim3(nch, B), dim3(256), 0, s, r, (bf16_t*)dx, lddx,
+      sdmi_rt::launch(gn_bwd_pass_kernel<256>, dim3(nch, B), dim3(256), 0, s, r, (bf16_t*)dx, lddx,
                          (const bf16_t*)addend, ldadd);
     else
-      hipLaunchKernelGGL(gn_bwd_pass_kernel<1024>, dim3(nch, B), dim3(1024), 0, s, r, (bf16_t*)dx, lddx,
+      sdmi_rt::launch(gn_bwd_pass_kernel<1024>, dim3(nch, B), dim3(1024), 0, s, r, (bf16_t*)dx, lddx,
                          (const bf16_t*)addend, ldadd);
     SDMI_CHECK_LAUNCH();
     return 0;
@@ -796,13 +796,13 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   const int ps = pick_psplit(nch, B, P);
   r.part = part_base(ws, B, C);
   if ((dgamma || ps > 1) && !(r.ctr = counter_slot())) return -4;
-  hipLaunchKernelGGL(gn_bwd_reduce_kernel, dim3(nch, B, ps), dim3(NT), 0, s, r);
+  sdmi_rt::launch(gn_bwd_reduce_kernel, dim3(nch, B, ps), dim3(NT), 0, s, r);
   SDMI_CHECK_LAUNCH();
   ApplyArgs a = {};
   a.x = (const bf16_t*)x; a.ldx = ldx; a.dy = (const bf16_t*)dy; a.lddy = lddy; a.dx = (bf16_t*)dx; a.lddx = lddx;
   a.tab = (const float4*)table2_ws; a.add = (const bf16_t*)addend; a.ldadd = ldadd;
   a.B = B; a.P = P; a.C = C; a.silu = silu;
-  hipLaunchKernelGGL(gn_bwd_apply_kernel, apply_grid(B, P, C), dim3(NT), 0, s, a);
+  sdmi_rt::launch(gn_bwd_apply_kernel, apply_grid(B, P, C), dim3(NT), 0, s, a);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -832,7 +832,7 @@ extern "C" int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, floa
   const int ps = pick_psplit(nch, r.nb, r.seg);
   r.part = part_base(ws, r.nb, C);
   if ((per_c || per_c2 || ps > 1) && !(r.ctr = counter_slot())) return -4;
-  hipLaunchKernelGGL(chan_sum_kernel, dim3(nch, r.nb, ps), dim3(NT), 0, (hipStream_t)stream, r);
+  sdmi_rt::launch(chan_sum_kernel, dim3(nch, r.nb, ps), dim3(NT), 0, (hipStream_t)stream, r);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

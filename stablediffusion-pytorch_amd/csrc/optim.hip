@@ -98,9 +98,9 @@ extern "C" size_t sdmi_optim_workspace(void) { return NORM_BLOCKS * sizeof(float
 extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws,
                                  int growth_interval, int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(NORM_BLOCKS), dim3(NT), 0, s, grads, n, ws);
+  sdmi_rt::launch(sumsq_kernel, dim3(NORM_BLOCKS), dim3(NT), 0, s, grads, n, ws);
   SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(NT), 0, s, ws, NORM_BLOCKS, max_norm, state, growth_interval,
+  sdmi_rt::launch(norm_finalize_kernel, dim3(1), dim3(NT), 0, s, ws, NORM_BLOCKS, max_norm, state, growth_interval,
                      skip_if_loss_nonfinite, grad_div);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -117,7 +117,7 @@ extern "C" int sdmi_adam_ema(float* params, const float* grads, float* m, float*
   }
   long long blocks = (n + NT - 1) / NT;
   if (blocks > max_blocks) blocks = max_blocks;
-  hipLaunchKernelGGL(adam_ema_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v, ema,
+  sdmi_rt::launch(adam_ema_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v, ema,
                      n, state, lr, b1, b2, eps, ema_decay);
   SDMI_CHECK_LAUNCH();
   return 0;

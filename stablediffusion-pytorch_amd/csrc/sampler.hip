@@ -86,11 +86,11 @@ extern "C" int sdmi_ddpm_prev(const float* xt, const float* eps, const float* z,
                               const float* betas, const float* alphas, const float* abar, const float* s1m,
                               float* prev, float* x0, int decrement_t, sdmi_stream_t stream) {
   if (!xt || !eps || !t_dev || !betas || !alphas || !abar || !s1m || !prev || n <= 0) return -1;
-  hipLaunchKernelGGL(ddpm_prev_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, xt, eps, z, n, t_dev,
+  sdmi_rt::launch(ddpm_prev_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, xt, eps, z, n, t_dev,
                      betas, alphas, abar, s1m, prev, x0);
   SDMI_CHECK_LAUNCH();
   if (decrement_t) {
-    hipLaunchKernelGGL(dec_t_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t_dev);
+    sdmi_rt::launch(dec_t_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t_dev);
     SDMI_CHECK_LAUNCH();
   }
   return 0;
@@ -99,7 +99,7 @@ extern "C" int sdmi_ddpm_prev(const float* xt, const float* eps, const float* z,
 extern "C" int sdmi_ddim_prev(const float* xt, const float* eps, const float* noise, long long n, float alpha_t,
                               float alpha_prev, float eta, float* out, sdmi_stream_t stream) {
   if (!xt || !eps || !out || n <= 0) return -1;
-  hipLaunchKernelGGL(ddim_prev_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, xt, eps, noise, n, alpha_t,
+  sdmi_rt::launch(ddim_prev_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, xt, eps, noise, n, alpha_t,
                      alpha_prev, eta, out);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -108,7 +108,7 @@ extern "C" int sdmi_ddim_prev(const float* xt, const float* eps, const float* no
 extern "C" int sdmi_affine_step(const float* x, const float* eps, const float* z, long long n, float c1, float c2,
                                 float var, float* out, sdmi_stream_t stream) {
   if (!x || !eps || !out || n <= 0) return -1;
-  hipLaunchKernelGGL(affine_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, x, eps, z, n, c1, c2, var,
+  sdmi_rt::launch(affine_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, x, eps, z, n, c1, c2, var,
                      out);
   SDMI_CHECK_LAUNCH();
   return 0;

@@ -162,9 +162,9 @@ extern "C" int sdmi_vq_quantize(const float* z, int ldz, const float* w, const f
   a.zq = zq; a.idx = idx; a.xq = xq; a.partial = ws;
   const long long P = (long long)B * HW;
   const int blocks = (int)((P + 63) / 64);
-  hipLaunchKernelGGL(vq_quantize_kernel, dim3(blocks), dim3(VQ_NT), 0, (hipStream_t)stream, a);
+  sdmi_rt::launch(vq_quantize_kernel, dim3(blocks), dim3(VQ_NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
-  hipLaunchKernelGGL(vq_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ws, blocks, 1.0f / (float)(P * C),
+  sdmi_rt::launch(vq_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ws, blocks, 1.0f / (float)(P * C),
                      loss);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -175,7 +175,7 @@ extern "C" int sdmi_pointwise_in(const float* z, int B, int C, int HW, const flo
   if (!z || !out || B <= 0 || C <= 0 || HW <= 0 || cout <= 0 || ld < cout) return -1;
   const long long total = (long long)B * HW * ld;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(pointwise_in_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, B, C, HW, w, b, cout,
+  sdmi_rt::launch(pointwise_in_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, B, C, HW, w, b, cout,
                      (bf16_t*)out, ld);
   SDMI_CHECK_LAUNCH();
   return 0;

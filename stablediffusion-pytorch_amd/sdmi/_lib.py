@@ -5,8 +5,6 @@ The product path has no fallback: if the library is missing or fails to load, ev
 import ctypes
 import os
 
-from . import plan
-
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SDMI_LIB_PATH") or os.path.join(_HERE, "libsdmi.so")  # override: A/B timing only
 
@@ -17,7 +15,7 @@ B_NK, B_KN, B_KN_CONV = 0, 1, 2
 
 class ConvGeom(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in
-                ("ih", "iw", "cin", "ldx", "kh", "kw", "oh_log2", "ow_log2", "sy", "sx", "oy0", "ox0")]
+                ("ih", "iw", "cin", "ldx", "kh", "kw", "oh", "ow", "sy", "sx", "oy0", "ox0")]
 
 
 class GemmDesc(ctypes.Structure):
@@ -29,11 +27,11 @@ class GemmDesc(ctypes.Structure):
         ("geom", ConvGeom),
         ("c", ctypes.c_void_p), ("ldc", ctypes.c_int), ("c_f32", ctypes.c_int),
         ("bias", ctypes.c_void_p),
-        ("rowbias", ctypes.c_void_p), ("rb_ld", ctypes.c_int), ("rb_shift", ctypes.c_int),
+        ("rowbias", ctypes.c_void_p), ("rb_ld", ctypes.c_int), ("rb_div", ctypes.c_int),
         ("resid", ctypes.c_void_p), ("ldr", ctypes.c_int),
         ("alpha", ctypes.c_float),
         ("act", ctypes.c_int),
-        ("remap", ctypes.c_int), ("r_gh_log2", ctypes.c_int), ("r_gw_log2", ctypes.c_int),
+        ("remap", ctypes.c_int), ("r_gh", ctypes.c_int), ("r_gw", ctypes.c_int),
         ("r_oh", ctypes.c_int), ("r_ow", ctypes.c_int), ("r_sy", ctypes.c_int), ("r_sx", ctypes.c_int),
         ("r_oy", ctypes.c_int), ("r_ox", ctypes.c_int),
         ("perm", ctypes.c_int), ("p_cin", ctypes.c_int), ("p_taps", ctypes.c_int), ("p_cvalid", ctypes.c_int),
@@ -115,26 +113,21 @@ SIGNATURES = {
     "sdmi_ddim_prev": ([_P, _P, _P, _L, _F, _F, _F, _P, _P], _I),
     "sdmi_affine_step": ([_P, _P, _P, _L, _F, _F, _F, _P, _P], _I),
     "sdmi_mse_patch": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
+    "sdmi_plan_begin": ([], _I),
+    "sdmi_plan_end": ([ctypes.POINTER(ctypes.c_void_p)], _I),
+    "sdmi_plan_recording": ([], _I),
+    "sdmi_plan_note_event": ([_P, _P], _I),
+    "sdmi_plan_note_wait": ([_P, _P], _I),
+    "sdmi_plan_note_callout": ([_I], _I),
+    "sdmi_plan_info": ([_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
+    "sdmi_plan_replay": ([_P, _I, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
+    "sdmi_plan_destroy": ([_P], _I),
 }
 
 
-class _Recorded:
-    """Launch entry point (takes a stream): called now, and appended to the plan while one is recorded."""
-    __slots__ = ("fn", "__name__")
-
-    def __init__(self, fn, name):
-        self.fn = fn
-        self.__name__ = name
-
-    def __call__(self, *args):
-        r = self.fn(*args)
-        if plan.RECORDING is not None:
-            plan.RECORDING.append((self.fn, args))
-        return r
-
-
 class _Lib:
-    """libsdmi.so with its stream-taking entry points wrapped for plan recording (sdmi.plan)."""
+    """libsdmi.so with argument / result types set on every entry point of include/sdmi.h. Launches made while a
+    native plan records (sdmi.plan.StepPlan) are captured inside the library itself (csrc/plan.hip)."""
 
     def __init__(self, cdll):
         self._cdll = cdll
@@ -142,13 +135,7 @@ class _Lib:
             fn = getattr(cdll, name)
             fn.argtypes = argt
             fn.restype = rest
-            launches = len(argt) > 0 and name not in _HOST_ONLY
-            setattr(self, name, _Recorded(fn, name) if launches else fn)
-
-
-# entry points that only answer host-side queries (never launch; not recorded)
-_HOST_ONLY = {"sdmi_gemm_plan", "sdmi_gemm_kernel_info", "sdmi_chan_reduce_workspace", "sdmi_mse_workspace", "sdmi_pack_chunk",
-              "sdmi_optim_workspace", "sdmi_ln_chunk_rows", "sdmi_vq_workspace"}
+            setattr(self, name, fn)
 
 
 def lib():

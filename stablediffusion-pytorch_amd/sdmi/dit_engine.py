@@ -235,7 +235,7 @@ class DiTEngine:
         g = K.conv_geom(H, W, self.cpad, self.cpad, p, p, gh, gw, p, p, 0, 0)
         K.gemm(M, D, p * p * self.cpad, xin, _lib.A_CONV, 0, self.W("pe"), _lib.B_NK, p * p * self.cpad, tok, D,
                geom=g, bias=P["patch_embed_layer.patch_embed.0.bias"], rowbias=self.pos_table(gh, gw), rb_ld=D,
-               rb_shift=0, rb_mod=N)
+               rb_div=1, rb_mod=N)
         # ---- time embedding -> t_proj (ReLU) -> ReLU(t_emb) -> all adaLN tables in one GEMM ----
         t = plan.timesteps(t, self.device)
         if t.numel() not in (1, B):
@@ -495,7 +495,7 @@ class DiTEngine:
             for ph in range(p):
                 for pw in range(p):
                     tap = ph * p + pw
-                    remap = (K._log2(gh), K._log2(gw), H, W, p, p, ph, pw)
+                    remap = (gh, gw, H, W, p, p, ph, pw)
                     K.gemm(M, self.cpad, D, dtok, _lib.A_ROWMAJOR, D, wpe[:, tap * self.cpad:], _lib.B_KN,
                            p * p * self.cpad, dxin, self.cpad, remap=remap)
             K.cond_wgrad(dxin, self.cpad, self.im_channels, B, H, W, st["mask"], L["im_in"], L["im_out"],

@@ -22,13 +22,6 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def _log2(v):
-    l = v.bit_length() - 1
-    if (1 << l) != v:
-        raise ValueError(f"spatial size {v} must be a power of two")
-    return l
-
-
 # optional per-launch timing hook (bench.py): list of (tag, flops, start_event, end_event, info)
 PROFILE = None
 PHASE = ""  # label prefixed to profiled launches ("fwd" / "bwd" / "wg" ...; set by the engines)
@@ -76,7 +69,7 @@ class _Prof:
 
 
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
-         rb_ld=0, rb_shift=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0,
+         rb_ld=0, rb_div=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0,
          a2=None, lda2=0, k_split=0, bias2=None, rb_mod=0, aux=None, ld_aux=0):
     """C[m][n] = epi(sum_k A[m][k] B[k][n]).  a/b/c/resid/rowbias are tensors (pointer = data_ptr,
     offsets already applied by slicing); see include/sdmi.h for the operand modes."""
@@ -93,13 +86,13 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     d.c_f32 = 1 if c.dtype == torch.float32 else 0
     d.bias = bias.data_ptr() if bias is not None else None
     if rowbias is not None:
-        d.rowbias, d.rb_ld, d.rb_shift = rowbias.data_ptr(), rb_ld, rb_shift
+        d.rowbias, d.rb_ld, d.rb_div = rowbias.data_ptr(), rb_ld, rb_div
     if resid is not None:
         d.resid, d.ldr = resid.data_ptr(), ldr
     d.alpha = alpha
     d.act = act
     if remap is not None:
-        (d.r_gh_log2, d.r_gw_log2, d.r_oh, d.r_ow, d.r_sy, d.r_sx, d.r_oy, d.r_ox) = remap
+        (d.r_gh, d.r_gw, d.r_oh, d.r_ow, d.r_sy, d.r_sx, d.r_oy, d.r_ox) = remap
         d.remap = 1
     if perm is not None:
         d.perm = perm[3] if len(perm) > 3 else 1
@@ -138,7 +131,9 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
 # ------------------------------------------------------------------------------------------------
 
 def conv_geom(ih, iw, cin, ldx, kh, kw, oh, ow, sy, sx, oy0, ox0):
-    return dict(ih=ih, iw=iw, cin=cin, ldx=ldx, kh=kh, kw=kw, oh_log2=_log2(oh), ow_log2=_log2(ow),
+    if oh <= 0 or ow <= 0:
+        raise ValueError(f"empty convolution output grid {oh} x {ow}")
+    return dict(ih=ih, iw=iw, cin=cin, ldx=ldx, kh=kh, kw=kw, oh=oh, ow=ow,
                 sy=sy, sx=sx, oy0=oy0, ox0=ox0)
 
 
@@ -149,13 +144,12 @@ def conv_fwd(x, B, H, W, cin, ldx, wpk, cout, kh, kw, stride, pad, out, ldo, *, 
     OH = (H + 2 * pad - kh) // stride + 1
     OW = (W + 2 * pad - kw) // stride + 1
     g = conv_geom(H, W, cin, ldx, kh, kw, OH, OW, stride, stride, -pad, -pad)
-    rb_shift = _log2(OH * OW)
     K1 = kh * kw * cin
     if x2 is not None:  # fused 1x1 conv of x2 (same pixel grid) by K-concatenation: wpk = [W | W2]
         assert stride == 1 and OH == H and OW == W
     return gemm(B * OH * OW, cout, K1 + cin2, x, _lib.A_CONV, 0, wpk, _lib.B_NK, ldw or (K1 + cin2), out, ldo,
                 geom=g, bias=bias, rowbias=rowbias, rb_ld=(rb_ld or cout) if rowbias is not None else 0,
-                rb_shift=rb_shift, resid=resid, ldr=ldr, act=act, n_store=n_store,
+                rb_div=OH * OW, resid=resid, ldr=ldr, act=act, n_store=n_store,
                 a2=x2, lda2=ld_of(x2) if x2 is not None else 0, k_split=K1, bias2=bias2)
 
 
@@ -186,7 +180,7 @@ def convT_fwd_phases(x, B, H, W, cin, ldx, wph, cout, out, ldo, *, bias=None, re
     for ph in range(2):
         for pw in range(2):
             g = conv_geom(H, W, cin, ldx, 2, 2, H, W, 1, 1, ph - 1, pw - 1)
-            remap = (_log2(H), _log2(W), 2 * H, 2 * W, 2, 2, ph, pw)
+            remap = (H, W, 2 * H, 2 * W, 2, 2, ph, pw)
             gemm(B * H * W, cout, 4 * cin, x, _lib.A_CONV, 0, wph[ph * 2 + pw], _lib.B_NK, 4 * cin, out, ldo,
                  geom=g, bias=bias, resid=resid, ldr=ldr, remap=remap)
     return out
@@ -312,7 +306,7 @@ def conv_dgrad_phases(dy, B, H, W, cout, ldy, wph, cin, out, ldo, *, resid=None,
     for ph in range(2):
         for pw in range(2):
             g = conv_geom(h, w, cout, ldy, 2, 2, h, w, 1, 1, ph - 1, pw - 1)
-            remap = (_log2(h), _log2(w), H, W, 2, 2, ph, pw)
+            remap = (h, w, H, W, 2, 2, ph, pw)
             gemm(B * h * w, cin, 4 * cout, dy, _lib.A_CONV, 0, wph[ph * 2 + pw], _lib.B_NK, 4 * cout, out, ldo,
                  geom=g, resid=resid, ldr=ldr, remap=remap)
     return out

@@ -24,6 +24,7 @@ class EngineHolder:
         self.base = base
         self.store = None
         self.engine = None
+        self._packed_sig = None
 
     def ensure(self, device):
         params = dict(self.module.named_parameters())
@@ -43,14 +44,23 @@ class EngineHolder:
                 self.engine = DiTEngine(self.cfg, store.p, None, im_channels=self.module.im_channels)
             else:
                 self.engine = UNetEngine(self.cfg, store.p, None, base=self.base, im_channels=self.module.im_channels)
+            self._packed_sig = None
         return self.engine
+
+    def refresh(self, params):
+        """Repack the bf16 GEMM-layout weights only when a parameter changed since the last pack: every in-place
+        update (optimizer.step, load_state_dict, .copy_) bumps the tensor's version counter. A sampling loop
+        (tools/sample_ddpm_*.py: 1000 forwards, no updates) packs once instead of once per call."""
+        sig = tuple(p._version for p in params)
+        if sig != self._packed_sig:
+            self.engine.refresh_weights()
+            self._packed_sig = sig
 
 
 class DenoiserFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, holder, x, t, text, mask, klass, *params):
         eng = holder.engine
-        eng.refresh_weights()
         B, C, H, W = x.shape
         pred, tape = eng.forward(x, t, text, mask, need_backward=True, klass=klass)
         out = eng.pred_to_nchw(pred, B, H, W)
@@ -77,9 +87,15 @@ UNetFunction = DenoiserFunction
 
 def run_unet(module, holder, x, t, text=None, mask=None, klass=None):
     _require_gpu(x)
-    holder.ensure(x.device)
+    eng = holder.ensure(x.device)
     params = [p for _, p in module.named_parameters()]
-    return DenoiserFunction.apply(holder, x, t, text, mask, klass, *params)
+    holder.refresh(params)
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
+        return DenoiserFunction.apply(holder, x, t, text, mask, klass, *params)
+    # inference (torch.no_grad sampling loops): no backward tape, no saved activations
+    B, C, H, W = x.shape
+    pred, _ = eng.forward(x, t, text, mask, need_backward=False, klass=klass)
+    return eng.pred_to_nchw(pred, B, H, W)
 
 
 run_denoiser = run_unet

@@ -1,27 +1,42 @@
-"""Launch-plan record / replay: the host side of a training step as a flat list of native calls.
+"""Launch-plan record / replay: the host side of a training step recorded once, re-issued from C++.
 
-One eager step issues ~1,100 kernel launches through the C ABI (plus stream / event edges and, for N > 1, the
-RCCL bucket all-reduces); Python + ctypes bookkeeping costs ~15 us per launch, so an eager step is bound by the
-host at ~17 ms. A hipGraph removes that cost only for single-stream captures on this ROCm (a two-stream capture
-replays at the same ~16 ms of host time), and RCCL collectives sit between segments. StepPlan instead records
-the step ONCE -- every libsdmi entry point call with its already-marshalled arguments, every stream / event edge,
-every collective -- while running it for real, with all its temporaries allocated from a private memory pool
-that stays reserved; replay() re-issues exactly those calls: same pointers, same streams, same ordering, no
-Python-side shape logic, ~1 us per call. Per-step inputs live in static buffers filled before each replay.
+One eager step issues ~1,000 kernel launches through the C ABI (plus stream / event edges and, for N > 1, the RCCL
+bucket all-reduces). Issued from Python, each launch costs the ctypes marshalling, the library's host-side planning
+(descriptor validation, split-K / tile choice) and the HIP launch: ~12 ms of host time per cond-UNet step, as much
+as the device time. StepPlan records the step ONCE while running it for real -- libsdmi appends every kernel launch
+with a copy of its marshalled arguments to a native plan (csrc/plan.hip), this module notes the stream / event edges
+and, as numbered callouts, the work the library does not own (RCCL collectives, torch copies) -- with all
+temporaries allocated from a private memory pool that stays reserved. replay() then runs the recorded launches in
+C++ (one hipLaunchKernel each: same pointers, grids, streams and order), returning to Python only at callouts.
+Per-step inputs live in static buffers refilled before each replay.
 
-Hazard model = the eager step's: replay issues the same operations on the same streams in the same order, and
-no memory of the pool is handed to anything outside the plan between replays."""
+Hazard model = the eager step's: replay issues the same operations on the same streams in the same order, and no
+memory of the pool is handed to anything outside the plan between replays."""
+import ctypes
+
 import torch
 
-RECORDING = None  # list of (callable, args) while a plan is being recorded
+RECORDING = None  # callout list [(callable, args)] while a plan is being recorded
+KEEP = None       # objects the recorded plan refers to by handle (events) -- kept alive with the plan
+
+
+def _lib():
+    from . import _lib as L
+    return L.lib()
 
 
 def record(fn, *args):
-    """Call fn(*args) now and, while recording, append it to the plan."""
+    """Call fn(*args) now and, while recording, make it a callout of the plan (replayed from Python)."""
     r = fn(*args)
     if RECORDING is not None:
         RECORDING.append((fn, args))
+        _check(_lib().sdmi_plan_note_callout(len(RECORDING) - 1), "sdmi_plan_note_callout")
     return r
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with status {rc}")
 
 
 def as_operand(t, dtype=torch.float32):
@@ -43,40 +58,85 @@ def timesteps(t, device):
     return torch.as_tensor(t, device=device).long().reshape(-1)  # host value: baked into the plan by design
 
 
-def wait_stream(dst, src):
-    record(dst.wait_stream, src)
-
-
 def record_event(ev, stream):
-    record(ev.record, stream)
+    ev.record(stream)
+    if RECORDING is not None:
+        KEEP.append(ev)
+        _check(_lib().sdmi_plan_note_event(ev.cuda_event, stream.cuda_stream), "sdmi_plan_note_event")
 
 
 def wait_event(stream, ev):
-    record(stream.wait_event, ev)
+    stream.wait_event(ev)
+    if RECORDING is not None:
+        KEEP.append(ev)
+        _check(_lib().sdmi_plan_note_wait(stream.cuda_stream, ev.cuda_event), "sdmi_plan_note_wait")
+
+
+def wait_stream(dst, src):
+    """dst waits for everything issued so far on src (an event edge the plan can replay)."""
+    if RECORDING is None:
+        dst.wait_stream(src)
+        return
+    ev = torch.cuda.Event()
+    record_event(ev, src)
+    wait_event(dst, ev)
 
 
 class StepPlan:
     def __init__(self, step_fn, device=None):
-        global RECORDING
+        global RECORDING, KEEP
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         torch.cuda.synchronize(self.device)
         self.pool = torch.cuda.MemPool()
-        ops = []
+        lib = _lib()
+        self.handle = None
+        ops, keep = [], []
         with torch.cuda.use_mem_pool(self.pool, device=self.device):
-            RECORDING = ops
+            _check(lib.sdmi_plan_begin(), "sdmi_plan_begin")
+            RECORDING, KEEP = ops, keep
+            h = ctypes.c_void_p()
             try:
                 step_fn()
             finally:
-                RECORDING = None
+                RECORDING, KEEP = None, None
+                _check(lib.sdmi_plan_end(ctypes.byref(h)), "sdmi_plan_end")
+                self.handle = h
         torch.cuda.synchronize(self.device)
         self.ops = ops
+        self.keep = keep
+        self._cid, self._next = ctypes.c_int(0), ctypes.c_int(0)
+
+    def info(self):
+        """(recorded ops, kernel launches, callouts)."""
+        n, k = ctypes.c_int(0), ctypes.c_int(0)
+        _check(_lib().sdmi_plan_info(self.handle, ctypes.byref(n), ctypes.byref(k)), "sdmi_plan_info")
+        return n.value, k.value, len(self.ops)
 
     def __len__(self):
-        return len(self.ops)
+        return self.info()[0]
+
+    def collectives(self):
+        """Number of recorded all-reduce callouts (sdmi.reducer bucket issues)."""
+        return sum(1 for fn, _ in self.ops if getattr(fn, "__name__", "") == "_issue")
 
     def replay(self):
-        for fn, args in self.ops:
-            r = fn(*args)
-            # libsdmi entry points return an int status (0 = ok); torch / dist calls return None, tensors or works
-            if type(r) is int and r != 0:
-                raise RuntimeError(f"plan replay: {getattr(fn, '__name__', fn)} failed with status {r}")
+        lib = _lib()
+        cid, nxt = self._cid, self._next
+        pos = 0
+        while True:
+            rc = lib.sdmi_plan_replay(self.handle, pos, ctypes.byref(cid), ctypes.byref(nxt))
+            if rc != 0:
+                raise RuntimeError(f"plan replay failed at op {nxt.value} with status {rc}")
+            if cid.value < 0:
+                return
+            fn, args = self.ops[cid.value]
+            fn(*args)
+            pos = nxt.value
+
+    def __del__(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            try:
+                _lib().sdmi_plan_destroy(self.handle)
+            except Exception:
+                pass
+            self.handle = None

@@ -40,7 +40,7 @@ class DDPMTrainer:
 
     def __init__(self, cfg, state_dict, device, *, base="cond", lr=1e-5, betas=(0.9, 0.999), eps=1e-8,
                  max_grad_norm=1.0, ema_decay=0.9999, init_scale=65536.0, growth_interval=2000,
-                 sched=(1000, 0.00085, 0.012), group=None, bucket_bytes=64 << 20):
+                 sched=(1000, 0.00085, 0.012), group=None, bucket_bytes=64 << 20, force_reducer=False):
         self.cfg = cfg
         self.base = base
         self.device = torch.device(device)
@@ -48,6 +48,13 @@ class DDPMTrainer:
         order = dit_flat_order(cfg, list(shapes)) if base == "dit" else None
         self.store = FlatStore(shapes, cfg, self.device, order=order)
         self.store.load(state_dict)
+        self.group = group
+        self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
+        if self.world > 1:
+            # DistributedDataParallel broadcasts rank 0's parameters when it wraps the model
+            # (train_ddpm_cond_celebhq_multi_gpu.py:257-263): every replica (and its EMA copy) starts from them
+            src = 0 if group is None or group is dist.group.WORLD else dist.get_global_rank(group, 0)
+            dist.broadcast(self.store.params, src=src, group=group)
         # EMA copy (train_ddpm_cond_celebhq_multi_gpu.py:376-378); none for the DiT trainer (commented out at
         # Model_DiT_12L_train.py:377-379): the fused optimizer then skips the EMA stream entirely
         self.ema = self.store.params.clone() if ema_decay is not None else None
@@ -59,13 +66,15 @@ class DDPMTrainer:
         if base == "dit":
             self.engine = DiTEngine(cfg, self.store.p, self.store.g)
         else:
-            self.engine = UNetEngine(cfg, self.store.p, self.store.g, base=base)
+            # latent channels from the state dict (4 for CelebHQ, the VQVAE's z_channels in general: 3 for MNIST)
+            self.engine = UNetEngine(cfg, self.store.p, self.store.g, base=base,
+                                     im_channels=shapes["conv_out.weight"][0])
         self.num_timesteps = sched[0]
         sa, s1a = scheduler_tables(*sched)
         self.sqrt_abar, self.sqrt_1m_abar = sa.to(self.device), s1a.to(self.device)
-        self.group = group
-        self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
-        self.reducer = BucketReducer(self.store.grads, group, bucket_bytes) if self.world > 1 else None
+        # force_reducer: run the bucketed all-reduce even at world size 1 (exercises RCCL + plan replay on one GPU)
+        self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes) if self.world > 1 or force_reducer
+                        else None)
         if self.reducer is not None and getattr(self.engine, "side", None) is not None:
             self.reducer.producers.append(self.engine.side)
         self._progress = None
@@ -85,6 +94,18 @@ class DDPMTrainer:
             self.opt_events = [torch.cuda.Event() for _ in self.opt_ranges]
             self.late_event = torch.cuda.Event()
         self.engine.refresh_weights()
+        if self.opt_ranges is not None:
+            # Seed the pipeline: every chunk event is recorded once (after the initial pack) and pending, so the
+            # FIRST step -- possibly the one a StepPlan records -- already issues the forward / backward waits on
+            # the optimizer chunks that later replays need (they are trivially satisfied here).
+            side = self.engine.side
+            plan.wait_stream(side, torch.cuda.current_stream(self.device))
+            for ev in self.opt_events:
+                plan.record_event(ev, side)
+            self.engine._pending = {c: ev for c, ev in enumerate(self.opt_events)}
+            if self.engine.pack.late_chunk is not None:
+                plan.record_event(self.late_event, side)
+                self.engine._pending[self.engine.pack.late_chunk] = self.late_event
 
     # ------------------------------------------------------------------------------------------
     def _watermarks(self, tape):
@@ -151,8 +172,13 @@ class DDPMTrainer:
         L = _lib.lib()
         ws = torch.empty(L.sdmi_optim_workspace() // 4, dtype=torch.float32, device=self.device)
         hp = self.hp
+        # Non-finite loss: one process skips before scaler.update() (:348-352). With N > 1 only the rank-local loss
+        # is known here, so the skip / back-off decision is left to the all-reduced gradient norm (a non-finite loss
+        # makes that rank's gradients, hence the global sum, non-finite): every replica then skips and halves its
+        # loss scale identically instead of drifting apart.
         _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(), ws.data_ptr(),
-                                       hp["growth"], 1, float(self.world), K._stream()), "sdmi_clip_unscale")
+                                       hp["growth"], 1 if self.world == 1 else 0, float(self.world), K._stream()),
+                   "sdmi_clip_unscale")
         ema_decay = hp["ema"] if hp["ema"] is not None else 0.0
         if self.opt_ranges is None:
             _lib.check(L.sdmi_adam_ema(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
@@ -202,6 +228,13 @@ class DDPMTrainer:
             raise RuntimeError("this trainer keeps no EMA copy (ema_decay=None)")
         self.sync_optimizer()
         return {k: self.store.view(self.ema, k) for k in self.store.order}
+
+    def state_dict(self):
+        """Model state dict (views of the flat fp32 master weights), safe to read or save on the current stream:
+        it first waits for the chunked optimizer step still in flight on the side stream. Never read
+        store.params / store.p directly after step() without sync_optimizer()."""
+        self.sync_optimizer()
+        return {k: self.store.p[k] for k in self.store.order}
 
     def sync_optimizer(self):
         """The current stream waits for the chunked optimizer step still in flight (parameters, EMA and packed

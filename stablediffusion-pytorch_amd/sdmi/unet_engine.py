@@ -27,10 +27,6 @@ from . import kernels as K
 from . import plan
 
 
-def _log2(v):
-    return v.bit_length() - 1
-
-
 def layout(cfg):
     down = list(cfg["down_channels"])
     mid = list(cfg["mid_channels"])

@@ -77,3 +77,17 @@ def _class_cond(n=10):
 
 SMALL_CLASS_UNET = dict(SMALL_UNCOND, condition_config=_class_cond())
 SMALL_CLASS_DIT = dict(SMALL_DIT_UNCOND, condition_config=_class_cond())
+
+
+# ---- BASELINE config 1: MNIST unconditional LDM (tools/train_ddpm_vqvae.py, default --config config/mnist.yaml).
+# config/mnist.yaml is NOT in the reference tree, so these are BUILD-AUTHORED values in the
+# reference's yaml schema: 28x28 single-channel images -> VQVAE (two stride-2 levels) -> 3 x 7 x 7 latents -> an
+# unconditional UNet that does not down-sample (7 is odd: a stride-2 level would break the skip concatenation).
+MNIST_VQVAE = {"z_channels": 3, "codebook_size": 20, "down_channels": [32, 64, 128], "mid_channels": [128, 128],
+               "down_sample": [True, True], "attn_down": [False, False], "norm_channels": 32, "num_heads": 16,
+               "num_down_layers": 1, "num_mid_layers": 1, "num_up_layers": 1}
+MNIST_LDM = {"down_channels": [64, 128, 128], "mid_channels": [128, 128], "down_sample": [False, False],
+             "attn_down": [True, True], "time_emb_dim": 128, "norm_channels": 32, "num_heads": 8,
+             "conv_out_channels": 64, "num_down_layers": 1, "num_mid_layers": 1, "num_up_layers": 1}
+MNIST_SCHED = (1000, 0.0015, 0.0195)
+MNIST_LR = 1e-5

@@ -186,6 +186,71 @@ def main():
     print("golden fixtures written to", HERE)
 
 
+def gen_mnist():
+    """BASELINE config 1 (tools/train_ddpm_vqvae.py:85-113 without cached latents): per step, images (B=4, 1 x 28 x 28 in
+    [-1, 1] as MnistDataset yields them) -> vae.encode under no_grad -> add_noise -> uncond Unet -> MSE -> backward ->
+    Adam(ldm_lr), no clip, no EMA. Two steps; the first also stores the loss gradients of selected parameters."""
+    import models.vqvae as ref_vq
+    from oracle import vqvae_oracle as VO
+    from tests.golden.configs import MNIST_VQVAE, MNIST_LDM, MNIST_SCHED, MNIST_LR
+    vae = ref_vq.VQVAE(im_channels=1, model_config=MNIST_VQVAE)
+    shapes = VO.vqvae_param_shapes(MNIST_VQVAE, im_channels=1)
+    assert list(vae.state_dict().keys()) == list(shapes.keys())
+    vae.load_state_dict(O.deterministic_state(shapes, seed=51))
+    vae.eval()
+    model = ref_uncond.Unet(im_channels=MNIST_VQVAE["z_channels"], model_config=MNIST_LDM)
+    ushapes = O.unet_param_shapes(MNIST_LDM, im_channels=3, base="uncond")
+    assert list(model.state_dict().keys()) == list(ushapes.keys())
+    for k, v in model.state_dict().items():
+        assert tuple(v.shape) == tuple(ushapes[k]), k
+    model.load_state_dict(O.deterministic_state(ushapes, seed=52))
+    model.train()
+    sched = ref_sched.LinearNoiseScheduler(*MNIST_SCHED)
+    opt = torch.optim.Adam(model.parameters(), lr=MNIST_LR)
+    f = {}
+    g = torch.Generator().manual_seed(53)
+    for step in range(2):
+        im = torch.rand(4, 1, 28, 28, generator=g) * 2 - 1
+        opt.zero_grad()
+        with torch.no_grad():
+            z, _ = vae.encode(im)
+            _, _, idx = vae.quantize(vae.pre_quant_conv(vae.encoder_conv_out(torch.nn.SiLU()(vae.encoder_norm_out(
+                _enc_trunk(vae, im))))))
+        noise = torch.randn(z.shape, generator=g)
+        t = torch.randint(0, MNIST_SCHED[0], (4,), generator=g)
+        noisy = sched.add_noise(z, noise, t)
+        pred = model(noisy, t)
+        loss = torch.nn.functional.mse_loss(pred, noise)
+        loss.backward()
+        f.update({f"s{step}.im": im, f"s{step}.z": z, f"s{step}.indices": idx, f"s{step}.noise": noise,
+                  f"s{step}.t": t, f"s{step}.pred": pred.detach(), f"s{step}.loss": loss.detach().reshape(1),
+                  f"s{step}.grad_norm": torch.norm(torch.stack([p.grad.norm() for p in model.parameters()])).reshape(1)})
+        if step == 0:
+            for k, p in model.named_parameters():
+                if k in MNIST_GRAD_KEYS:
+                    f["grad." + k] = p.grad.detach().reshape(-1)[:8192].clone()
+        opt.step()
+    for k, p in model.named_parameters():
+        if k in MNIST_GRAD_KEYS:
+            f["param." + k] = p.detach().reshape(-1)[:8192].clone()
+    save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, "mnist_ldm.safetensors"))
+
+
+def _enc_trunk(vae, x):
+    out = vae.encoder_conv_in(x)
+    for down in vae.encoder_layers:
+        out = down(out)
+    for mid in vae.encoder_mids:
+        out = mid(out)
+    return out
+
+
+MNIST_GRAD_KEYS = ("conv_in.weight", "t_proj.0.weight", "downs.0.resnet_conv_first.0.2.weight",
+                   "downs.1.attentions.0.in_proj_weight", "mids.0.resnet_conv_second.1.2.weight",
+                   "ups.0.residual_input_conv.0.weight", "ups.1.attentions.0.out_proj.weight", "norm_out.weight",
+                   "conv_out.weight", "conv_out.bias")
+
+
 GRAD_KEYS = {
     "small_cond": ("cond_conv_in.weight", "conv_in_concat.weight", "t_proj.0.weight",
                    "downs.0.attentions.0.in_proj_weight", "downs.1.cross_attentions.0.out_proj.weight",
@@ -200,4 +265,7 @@ STEP_KEYS = ("conv_in_concat.weight", "downs.0.resnet_conv_first.0.2.weight", "d
              "norm_out.bias", "cond_conv_in.weight")
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["mnist"]:
+        gen_mnist()
+    else:
+        main()

@@ -2,7 +2,7 @@
 implementation (read-only at /root/reference) in THIS container. Only input/output tensors are
 committed (safetensors); weights regenerate from oracle.sd_oracle.deterministic_state.
 
-Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae] [sampler] [class]
+Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae] [vqvae256] [sampler] [class]
 
 The reference DIT zero-initialises adaptive_norm_layer and proj_out (models/transformer.py:147-151,
 transformer_layer.py:70-71), so a freshly built reference model outputs exactly 0; the fixtures load
@@ -168,6 +168,23 @@ def gen_vqvae():
         save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, f"{name}.safetensors"))
 
 
+def gen_vqvae256():
+    """The celebhq autoencoder at its bench size (256x256, config 2), batch 1: encoder latent, indices, decoder."""
+    from tests.golden.configs import vqvae_celebhq_config
+    model, sd = make_vqvae(vqvae_celebhq_config(), 8)
+    g = torch.Generator().manual_seed(23)
+    x = torch.rand(1, 3, 256, 256, generator=g) * 2 - 1
+    pre = {}
+    h = model.pre_quant_conv.register_forward_hook(lambda m, i, o: pre.__setitem__("z", o.detach().clone()))
+    with torch.no_grad():
+        out, zq, losses = model(x)
+    h.remove()
+    _, _, idx = model.quantize(pre["z"])
+    f = {"x": x, "pre_quant": pre["z"], "zq": zq, "indices": idx, "out": out,
+         "codebook_loss": losses["codebook_loss"].reshape(1)}
+    save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, "vqvae_celebhq256.safetensors"))
+
+
 def gen_sampler():
     """DDIMSampler / DDPMSampler steps (scheduler/linear_noise_scheduler.py:93-232) with a fixed-output model
     and fixed noise (torch.randn_like patched), so the step arithmetic alone is pinned."""
@@ -235,6 +252,8 @@ def main():
         gen_dit()
     if "vqvae" in what:
         gen_vqvae()
+    if "vqvae256" in what:
+        gen_vqvae256()
     if "sampler" in what:
         gen_sampler()
     if "class" in what:

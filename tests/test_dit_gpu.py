@@ -238,6 +238,38 @@ def test_dit12l_forward_matches_golden():
     assert mse <= 1e-4, mse
 
 
+def test_dit12l_forward_backward_b2():
+    """BASELINE config 5 (Model_DiT_12L_config, 12 layers, hidden 288, image condition at 512x512) at batch 2:
+    forward MSE <= 1e-4 and every parameter gradient (cosine >= 0.99, global norm within 5 %) against the fp32
+    oracle on the same weights and inputs."""
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cfg = dit12l_config()
+    model, sd = make(cfg, seed=6)
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(2, 4, 32, 32, generator=g)
+    t = torch.randint(0, 1000, (2,), generator=g)
+    c = {"image": one_hot(torch.randint(0, 19, (2, 512, 512), generator=g))}
+    noise = torch.randn(x.shape, generator=g)
+    leaves = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ref = DO.dit_forward(leaves, cfg, x, t, c)
+    torch.nn.functional.mse_loss(ref, noise).backward()
+    out = model(x.cuda(), t.cuda(), {"image": c["image"].cuda()})
+    torch.nn.functional.mse_loss(out, noise.cuda()).backward()
+    torch.cuda.synchronize()
+    mse = ((out.detach().cpu() - ref.detach()) ** 2).mean().item()
+    assert mse <= 1e-4, mse
+    worst = (1.0, None)
+    for k, p in model.named_parameters():
+        r = leaves[k].grad
+        if r is not None and r.norm() > 1e-6:
+            worst = min(worst, (cos(p.grad.cpu(), r), k))
+    gn = torch.norm(torch.stack([p.grad.norm() for p in model.parameters()])).item()
+    rn = torch.norm(torch.stack([v.grad.norm() for v in leaves.values() if v.grad is not None])).item()
+    print(f"DiT-12L B=2: fwd MSE {mse:.3e}, worst grad cos {worst}, norm {gn:.5f} vs {rn:.5f}")
+    assert worst[0] >= 0.99, worst
+    assert abs(gn - rn) <= 0.05 * rn, (gn, rn)
+
+
 def test_fresh_dit_outputs_zero():
     """The reference zero-initialises adaLN and proj_out (transformer.py:147-151): a fresh DIT predicts 0."""
     from models.transformer import DIT

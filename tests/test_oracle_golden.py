@@ -149,3 +149,30 @@ def test_class_conditional_unet_and_dit_forward_and_grads():
         assert abs(loss.item() - f["loss"].item()) <= 1e-5 * abs(f["loss"].item())
         for k in ("class_emb.weight", "t_proj.0.weight", "t_proj.2.bias"):
             assert rel(leaves[k].grad, f["grad." + k]) < 1e-4, (name, k)
+
+
+def test_mnist_ldm_matches_reference():
+    """BASELINE config 1 chain (tools/train_ddpm_vqvae.py:85-113: VQVAE encode of 1 x 28 x 28 images -> 3 x 7 x 7
+    latents -> uncond UNet step) on the reference's own outputs (tests/golden/mnist_ldm.safetensors)."""
+    from oracle import vqvae_oracle as VO
+    from tests.golden.configs import MNIST_VQVAE, MNIST_LDM, MNIST_SCHED, MNIST_LR
+    f = fx("mnist_ldm")
+    vsd = O.deterministic_state(VO.vqvae_param_shapes(MNIST_VQVAE, im_channels=1), seed=51)
+    usd = O.deterministic_state(O.unet_param_shapes(MNIST_LDM, im_channels=3, base="uncond"), seed=52)
+    with torch.no_grad():
+        z, _, idx = VO.encode(vsd, MNIST_VQVAE, f["s0.im"])
+    assert torch.equal(idx.reshape(f["s0.indices"].shape), f["s0.indices"])
+    assert rel(z, f["s0.z"]) < 1e-5
+    ema = {k: v.clone() for k, v in usd.items()}
+    opt = O.AdamState(usd)
+    sched = O.SchedulerTables(*MNIST_SCHED)
+    for s in range(2):
+        loss, norm, ok = O.train_step(usd, ema, opt, MNIST_LDM, sched, f[f"s{s}.z"], f[f"s{s}.noise"], f[f"s{s}.t"], None,
+                                      lr=MNIST_LR, clip=float("inf"), ema_decay=0.0)
+        assert ok
+        assert abs(loss.item() - f[f"s{s}.loss"].item()) <= 1e-5 * f[f"s{s}.loss"].item()
+        assert abs(norm.item() - f[f"s{s}.grad_norm"].item()) <= 1e-4 * f[f"s{s}.grad_norm"].item()
+    for k in f:
+        if k.startswith("param."):
+            n = f[k].numel()
+            assert rel(usd[k[6:]].reshape(-1)[:n], f[k]) < 1e-5, k

@@ -7,7 +7,8 @@ Tolerances:
   encoder (bf16 activations through 20+ convs, fp32 head): relative RMS error of the pre-quantisation latent
     <= 2e-2; codebook indices agree on >= 90 % of positions (bf16 moves latents that sit near a Voronoi
     boundary to the neighbouring code; identical inputs give identical indices, see above);
-  decoder on the reference's own z_q: relative RMS error <= 2e-2."""
+  decoder on the reference's own z_q: relative RMS error <= 2e-2.
+The celebhq autoencoder is checked at 128x128 and at its bench size 256x256 (BASELINE config 2), batch 1."""
 import os
 
 import pytest
@@ -64,7 +65,8 @@ def test_quantize_kernel_bit_exact():
     assert abs(loss.item() - f["codebook_loss"].item()) <= 1e-6 * f["codebook_loss"].item()
 
 
-@pytest.mark.parametrize("name,cfg,seed", [("vqvae_small", SMALL_VQVAE, 9), ("vqvae_celebhq", vqvae_celebhq_config(), 8)])
+@pytest.mark.parametrize("name,cfg,seed", [("vqvae_small", SMALL_VQVAE, 9), ("vqvae_celebhq", vqvae_celebhq_config(), 8),
+                                           ("vqvae_celebhq256", vqvae_celebhq_config(), 8)])
 def test_encode_decode_vs_reference(name, cfg, seed):
     f = fx(name)
     model, sd = make(cfg, seed)
