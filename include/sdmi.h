@@ -95,6 +95,16 @@ typedef struct sdmi_gemm_desc {
   /* column-tile width request (0 = by occupancy: 192 when N % 192 == 0 fills the 512 workgroup slots in fewer
    * rounds; 128 / 192 = that width where the 192-wide tile applies: B_NK, row-major or implicit-conv A) */
   int tile_n_hint;
+  /* reduction outputs of a col-major-A GEMM (SDMI_A_COLMAJOR: A = dY^T of a weight gradient), computed in the same
+   * launch by extra synthesised B columns: sum_out[m] (and sum_out2[m]) = sum_k A[m][k] -- the bias gradient,
+   * replacing a separate column-sum pass over dY -- and gsum_out[g*gsum_ld + m] (bf16) = sum over k in
+   * [g*sum_group, (g+1)*sum_group) of A[m][k] -- per-sample sums, the time-embedding bias gradient
+   * (models/blocks.py:117-118). NULL = not computed. Rows >= m_store are not stored. */
+  float* sum_out;
+  float* sum_out2;
+  void* gsum_out;
+  int gsum_ld;
+  int sum_group;
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */
@@ -284,8 +294,10 @@ int sdmi_pack_transpose(const sdmi_tpack_desc* descs_dev, const void* bmap_dev, 
 size_t sdmi_optim_workspace(void);
 int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws, int growth_interval,
                       int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
+/* ema_alpha: the fp32 value of (1 - ema_decay) as the caller computes it (the reference passes alpha = 1 - 0.9999
+ * from Python doubles, :376-378) */
 int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n, const float* state,
-                  float lr, float b1, float b2, float eps, float ema_decay, sdmi_stream_t stream);
+                  float lr, float b1, float b2, float eps, float ema_decay, float ema_alpha, sdmi_stream_t stream);
 
 /* Streams restricted to a share of the CUs (hipExtStreamCreateWithCUMask): keep_num of every keep_den CUs.
  * Used for the engine's weight-gradient side stream (SDMI_SIDE_CU=num/den), no reference counterpart. */
@@ -311,6 +323,10 @@ int sdmi_plan_note_callout(int id);
 int sdmi_plan_info(const void* plan, int* ops, int* launches);
 int sdmi_plan_replay(void* plan, int start, int* callout, int* next);
 int sdmi_plan_destroy(void* plan);
+/* profiling: op kind (0 launch, 1 event record, 2 stream wait, 3 callout), kernel name, grid[3], block, LDS bytes;
+ * and the average device time of launch op i re-issued alone (iters times after warm untimed issues). */
+int sdmi_plan_op_info(const void* plan, int i, int* kind, const char** name, int* grid, int* block, int* shmem);
+int sdmi_plan_time_op(void* plan, int i, int warm, int iters, float* us);
 
 #ifdef __cplusplus
 }

@@ -39,6 +39,11 @@ struct Args {
   FastDiv ohw_d, ow_d;  // GEMM pixel grid: pixel m -> (b, oy, ox) = (m / (oh*ow), (m % (oh*ow)) / ow, m % ow)
   int ktiles_per_split, nsplit;
   const bf16_t* A2; int lda2; int k_split;
+  // reduction columns (col-major A only): B columns n >= n_x0 are synthesised instead of loaded -- column n_x0 is
+  // all ones (C gets the row sums of A over k: a bias gradient), columns n_x0 + 8 + j are the indicator of
+  // k / grp == j (C gets per-group row sums: the per-sample time-embedding gradient). 0 = none.
+  int n_x0;
+  FastDiv grp_d;
 };
 
 __device__ __forceinline__ void pixel_coords(const Args& g, int m, int& b, int& oy, int& ox) {
@@ -46,6 +51,22 @@ __device__ __forceinline__ void pixel_coords(const Args& g, int m, int& b, int& 
   const int r = m - b * g.ohw_d.d();
   oy = (int)g.ow_d.div((unsigned)r);
   ox = r - oy * g.ow_d.d();
+}
+
+// 8 synthesised B values (one 16-B chunk, columns [n, n + 8)) of the reduction columns at k (see Args::n_x0):
+// bf16 1.0 where the column's indicator holds, 0 elsewhere and for k >= K
+__device__ __forceinline__ uint4 reduction_cols(const Args& g, int n, int k) {
+  uint4 r = make_uint4(0u, 0u, 0u, 0u);
+  if (k >= g.K) return r;
+  const int j = n - g.n_x0;
+  const int d = j == 0 ? 0 : (int)g.grp_d.div((unsigned)k) - (j - 8);
+  if (d < 0 || d >= 8) return r;
+  const unsigned one = 0x3F80u << ((d & 1) * 16);  // bf16 1.0 in the low / high half of the 32-bit lane
+  if ((d >> 1) == 0) r.x = one;
+  else if ((d >> 1) == 1) r.y = one;
+  else if ((d >> 1) == 2) r.z = one;
+  else r.w = one;
+  return r;
 }
 
 // epilogue parameters (a separate kernel argument keeps both structs small enough to stay in SGPRs)
@@ -71,6 +92,12 @@ struct EpiArgs {
   int n8;           // N % 8 == 0: split-K slabs are written / read as 16-B rows even when !vec
   int rb_mod;       // rowbias row = (row / rb_div) % rb_mod when > 0 (per-token tables, e.g. position embedding)
   const bf16_t* aux; int ld_aux;  // act 3: ReLU-gradient mask source (aux[orow*ld_aux + col] > 0)
+  // reduction columns (Args::n_x0): column n_x0 -> sum_out[row] (and sum_out2), column n_x0 + 8 + j (j < ngrp)
+  // -> gsum[j * gsum_ld + row] (bf16); rows < m_store only
+  int n_x0, ngrp, gsum_ld;
+  float* sum_out;
+  float* sum_out2;
+  bf16_t* gsum;
 };
 
 __device__ __forceinline__ long long rb_row(const EpiArgs& g, int row) {
@@ -94,6 +121,20 @@ __device__ __forceinline__ float act1(const EpiArgs& g, float v, long long orow,
 }
 
 struct Epi {
+  // reduction columns [col, col + nv) of one row (raw sums: no alpha / bias / activation)
+  __device__ __forceinline__ static void extra(const EpiArgs& g, int row, int col, const float* v, int nv) {
+    if (row >= g.m_store) return;
+    for (int q = 0; q < nv; ++q) {
+      const int j = col + q - g.n_x0;
+      if (j == 0) {
+        if (g.sum_out) g.sum_out[row] = v[q];
+        if (g.sum_out2) g.sum_out2[row] = v[q];
+      } else if (j >= 8 && j - 8 < g.ngrp && g.gsum) {
+        g.gsum[(long long)(j - 8) * g.gsum_ld + row] = f2bf(v[q]);
+      }
+    }
+  }
+
   // v already holds alpha*acc + bias + bias2
   __device__ __forceinline__ static void finish(const EpiArgs& g, int row, int col, float v) {
     if (g.rowbias) v += bf2f(g.rowbias[rb_row(g, row) * g.rb_ld + col]);
@@ -181,6 +222,10 @@ struct Epi {
   }
 
   __device__ __forceinline__ static void store_final(const EpiArgs& g, int row, int col, float acc) {
+    if (g.n_x0 && col >= g.n_x0) {
+      extra(g, row, col, &acc, 1);
+      return;
+    }
     if (row >= g.m_store || col >= g.n_store) return;
     float v = g.alpha * acc;
     if (g.bias) v += g.bias[col];
@@ -254,6 +299,8 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
           for (int q = 0; q < 8 && col + q < e.N; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), rw, off + 4 * q, 0, CPOL_SC1);
         }
+      } else if (e.n_x0 && col >= e.n_x0) {
+        if (row < e.M) Epi::extra(e, row, col, v, 8);
       } else if (e.vec) {
         if (row < e.m_store && col < e.n_store) Epi::finish8(e, row, col, v);
       } else if (row < e.m_store) {
@@ -322,7 +369,9 @@ __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0
     for (int ch = threadIdx.x; ch < BM * (TBN / 8); ch += NT) {
       const int rl = ch / (TBN / 8);
       const int row = m0 + rl, col = n0 + (ch - rl * (TBN / 8)) * 8;
-      if (e.vec ? (row >= e.m_store || col >= e.n_store) : (row >= e.M || col >= e.N)) continue;
+      const bool xcol = e.n_x0 && col >= e.n_x0;
+      if (!xcol && (e.vec ? (row >= e.m_store || col >= e.n_store) : (row >= e.M || col >= e.N))) continue;
+      if (xcol && row >= e.M) continue;
       float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       const int off = (row * e.N + col) * 4;
 #pragma unroll 4
@@ -332,7 +381,9 @@ __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0
         const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, o + 16, 0, CPOL_SC1));
         v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3]; v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
       }
-      if (e.vec) {
+      if (xcol) {
+        Epi::extra(e, row, col, v, 8);
+      } else if (e.vec) {
         Epi::finish8(e, row, col, v);
       } else {
 #pragma unroll
@@ -461,6 +512,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
         int off = (n < g.N && k < g.K) ? (n * g.ldb + k) * 2 : OOB;
         rb[i] = BUF_LD(rsB, off);
       }
+    } else if (g.n_x0 && n0 + (tid & 15) * 8 >= g.n_x0) {  // reduction columns (both MN-contiguous B modes)
+      const int n = n0 + (tid & 15) * 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rb[i] = reduction_cols(g, n, k0 + (tid >> 4) + 16 * i);
     } else if (BMODE == SDMI_B_KN) {
       int n = n0 + (tid & 15) * 8;
 #pragma unroll
@@ -857,7 +912,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_n8_kernel(const EpiArgs g) 
     }
     if (sl == 0 && idx < total) {
       float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-      if (g.vec) {
+      if (g.n_x0 && col >= g.n_x0) {
+        Epi::extra(g, row, col, v, 8);
+      } else if (g.vec) {
         if (row < g.m_store && col < g.n_store) Epi::finish8(g, row, col, v);
       } else {
 #pragma unroll
@@ -902,6 +959,18 @@ hipError_t launch_reduce(const EpiArgs& red, hipStream_t s) {
   return hipGetLastError();
 }
 
+bool has_reductions(const sdmi_gemm_desc* d) { return d->sum_out || d->sum_out2 || d->gsum_out; }
+
+int reduction_groups(const sdmi_gemm_desc* d) {
+  return d->gsum_out && d->sum_group > 0 ? (d->k + d->sum_group - 1) / d->sum_group : 0;
+}
+
+// columns the launch computes: n, plus the reduction columns (8 for the sums, then the groups rounded to 8)
+int n_total(const sdmi_gemm_desc* d) {
+  if (!has_reductions(d)) return d->n;
+  return (d->n + 7) / 8 * 8 + 8 + (reduction_groups(d) + 7) / 8 * 8;
+}
+
 // Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged, 2 / 3 LDS-DMA ring
 // with that many stages, -1 (default) per mode: the DMA ring where it measured faster on the step's
 // shapes (row-major and implicit-conv A), register staging for the col-major (weight-gradient) A.
@@ -918,6 +987,7 @@ int gemm_variant() {
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
   if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
+  if (has_reductions(d)) v = 0;  // reduction columns are synthesised in the register-staged loader
   // the DMA path needs a tile-uniform second source (k_split % BK == 0)
   if (d->a_mode == SDMI_A_CONV && d->a2 && d->k_split % BK) v = 0;
   return v;
@@ -1056,6 +1126,21 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   e.n8 = d->n % 8 == 0;
   e.rb_mod = d->rb_mod;
   e.aux = (const bf16_t*)d->aux; e.ld_aux = d->ld_aux;
+  if (has_reductions(d)) {
+    if (d->a_mode != SDMI_A_COLMAJOR || d->b_mode == SDMI_B_NK) return -13;
+    if (d->gsum_out && (d->sum_group <= 0 || d->gsum_ld <= 0)) return -14;
+    a.n_x0 = e.n_x0 = (d->n + 7) / 8 * 8;
+    a.grp_d = FastDiv::make(std::max(1, d->sum_group));
+    e.ngrp = reduction_groups(d);
+    e.gsum_ld = d->gsum_ld;
+    e.sum_out = d->sum_out;
+    e.sum_out2 = d->sum_out2;
+    e.gsum = (bf16_t*)d->gsum_out;
+    e.N = n_total(d);  // split-K slabs and tile bounds cover the reduction columns too
+    const unsigned long long n8 = (unsigned long long)(e.N >> 3);
+    e.n8_magic = (n8 > 1 && (unsigned long long)d->m * n8 * n8 < (1ULL << 32)) ? (unsigned)(((1ULL << 32) + n8 - 1) / n8)
+                                                                              : 0u;
+  }
   if (d->act == 3 && !d->aux) return -8;
   if (d->act < 0 || d->act > 3) return -9;
   e.vec = !d->perm && d->n % 8 == 0 && e.n_store % 8 == 0 && d->ldc % 8 == 0 &&
@@ -1069,11 +1154,11 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
 
 int plan_splits(const sdmi_gemm_desc* d) {
   const int tbn = pick_tbn(d, pick_variant(d));
-  long long tiles = (long long)((d->m + BM - 1) / BM) * ((d->n + tbn - 1) / tbn);
+  long long tiles = (long long)((d->m + BM - 1) / BM) * ((n_total(d) + tbn - 1) / tbn);
   int nkt = (d->k + BK - 1) / BK;
   if (d->splits_hint > 0) {
     int s = std::min(d->splits_hint, nkt);
-    while (s > 1 && (long long)s * d->m * d->n * 4 >= (1LL << 31)) s >>= 1;
+    while (s > 1 && (long long)s * d->m * n_total(d) * 4 >= (1LL << 31)) s >>= 1;
     return std::max(s, 1);
   }
   int s = 1;
@@ -1094,7 +1179,7 @@ int plan_splits(const sdmi_gemm_desc* d) {
   // fill the 256 CUs: deep split-K for the small-output / long-K weight gradients (a 128 x 128 dW over
   // 32768 pixels is ONE tile), keeping >= 4 k-tiles per slice and the slabs within 32-bit offsets
   while (tiles * s < 256 && nkt / (s * 2) >= 4 && s < 128 &&
-         (long long)(s * 2) * d->m * d->n * 4 < (1LL << 31))
+         (long long)(s * 2) * d->m * n_total(d) * 4 < (1LL << 31))
     s *= 2;
   return s;
 }
@@ -1118,7 +1203,7 @@ extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) 
   if (rc) return rc;
   int s = plan_splits(d);
   if (splits) *splits = s;
-  if (ws) *ws = s > 1 ? (size_t)s * d->m * d->n * sizeof(float) : 0;
+  if (ws) *ws = s > 1 ? (size_t)s * d->m * n_total(d) * sizeof(float) : 0;
   return 0;
 }
 
@@ -1129,20 +1214,21 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   int splits = plan_splits(d);
-  if (splits > 1 && (!workspace || ws_bytes < (size_t)splits * d->m * d->n * sizeof(float))) splits = 1;
-  if ((long long)splits * d->m * d->n * 4 >= (1LL << 31)) splits = 1;  // slab offsets are 32-bit
+  const int nt = n_total(d);
+  if (splits > 1 && (!workspace || ws_bytes < (size_t)splits * d->m * nt * sizeof(float))) splits = 1;
+  if ((long long)splits * d->m * nt * 4 >= (1LL << 31)) splits = 1;  // slab offsets are 32-bit
   int nkt = (d->k + BK - 1) / BK;
   a.ktiles_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + a.ktiles_per_split - 1) / a.ktiles_per_split;
   a.nsplit = splits;
   EpiArgs run = e;
   const int variant = pick_variant(d), tbn = pick_tbn(d, variant);
-  dim3 grid((d->n + tbn - 1) / tbn, (d->m + BM - 1) / BM, splits);
+  dim3 grid((nt + tbn - 1) / tbn, (d->m + BM - 1) / BM, splits);
   if (splits > 1) {
     run.raw = 1;
     run.ws = (const float*)workspace;
     run.nsplit = splits;
-    run.split_stride = (long long)d->m * d->n;
+    run.split_stride = (long long)d->m * nt;
     run.counters = splitk_counters((long long)grid.x * grid.y, splits);
   }
   hipError_t err;
@@ -1160,7 +1246,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     EpiArgs red = e;
     red.raw = 0;
     red.nsplit = splits;
-    red.split_stride = (long long)d->m * d->n;
+    red.split_stride = (long long)d->m * nt;
     red.ws = (const float*)workspace;
     err = launch_reduce(red, s);
     if (err != hipSuccess) return (int)err;

@@ -70,14 +70,13 @@ __global__ void norm_finalize_kernel(const float* partial, int n, float max_norm
 }
 
 __global__ void adam_ema_kernel(float* p, const float* g, float* m, float* v, float* ema, long long n, const float* state,
-                                float lr, float b1, float b2, float eps, float ema_decay) {
+                                float lr, float b1, float b2, float eps, float ema_decay, float ema_alpha) {
   if (state[5] != 0.f) return;  // skipped step
   const float gs = state[1];
   const int step = (int)state[4];
   const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
   const float step_size = (float)(lr / bc1);
   const float bc2s = (float)sqrt(bc2);
-  const float omd = 1.0f - ema_decay;
   for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
     float gi = g[i] * gs;
     float mi = m[i] + (1.f - b1) * (gi - m[i]);  // lerp(m, g, 1 - b1)
@@ -87,7 +86,9 @@ __global__ void adam_ema_kernel(float* p, const float* g, float* m, float* v, fl
     float denom = sqrtf(vi) / bc2s + eps;
     float pi = p[i] - step_size * (mi / denom);
     p[i] = pi;
-    if (ema) ema[i] = ema[i] * ema_decay + omd * pi;
+    // ema.mul_(decay).add_(p, alpha=1 - decay) (:376-378): a rounded product, then add_'s fused alpha * p + self;
+    // alpha is the reference's own fp32 value of (1 - decay) computed in double (1e-4f, not 1 - 0.9999f)
+    if (ema) ema[i] = __builtin_fmaf(ema_alpha, pi, mul_ieee(ema[i], ema_decay));
   }
 }
 }  // namespace
@@ -108,7 +109,7 @@ extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm
 
 extern "C" int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n,
                              const float* state, float lr, float b1, float b2, float eps, float ema_decay,
-                             sdmi_stream_t stream) {
+                             float ema_alpha, sdmi_stream_t stream) {
   static long long max_blocks = -1;  // grid cap (SDMI_ADAM_BLOCKS): a narrower grid leaves CUs to concurrent work
   if (max_blocks < 0) {
     const char* e = getenv("SDMI_ADAM_BLOCKS");
@@ -118,7 +119,7 @@ extern "C" int sdmi_adam_ema(float* params, const float* grads, float* m, float*
   long long blocks = (n + NT - 1) / NT;
   if (blocks > max_blocks) blocks = max_blocks;
   sdmi_rt::launch(adam_ema_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v, ema,
-                     n, state, lr, b1, b2, eps, ema_decay);
+                     n, state, lr, b1, b2, eps, ema_decay, ema_alpha);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

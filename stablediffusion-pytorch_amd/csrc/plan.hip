@@ -159,6 +159,54 @@ extern "C" int sdmi_plan_replay(void* plan, int start, int* callout, int* next) 
   return 0;
 }
 
+// Per-op inspection for profiling tools (scripts/plan_profile.py): op kind (0 launch, 1 event record, 2 stream wait,
+// 3 callout), kernel name, grid / block, LDS bytes.
+extern "C" int sdmi_plan_op_info(const void* plan, int i, int* kind, const char** name, int* grid, int* block,
+                                 int* shmem) {
+  const Plan* p = (const Plan*)plan;
+  if (!p || i < 0 || i >= (int)p->ops.size()) return -1;
+  const sdmi_rt::Op& op = p->ops[i];
+  if (kind) *kind = op.kind;
+  if (name) *name = op.kind == sdmi_rt::OP_LAUNCH ? hipKernelNameRefByPtr(op.fn, op.stream) : nullptr;
+  if (grid) {
+    grid[0] = (int)op.grid.x;
+    grid[1] = (int)op.grid.y;
+    grid[2] = (int)op.grid.z;
+  }
+  if (block) *block = (int)(op.block.x * op.block.y * op.block.z);
+  if (shmem) *shmem = (int)op.shmem;
+  return 0;
+}
+
+// Re-issue launch op i alone `iters` times on its stream between two events (after `warm` untimed issues) and
+// return the average device time in microseconds. The plan's buffers are live (private pool), so the op reads and
+// writes exactly the memory it does inside the step (in-place accumulating ops change values; timing only).
+extern "C" int sdmi_plan_time_op(void* plan, int i, int warm, int iters, float* us) {
+  Plan* p = (Plan*)plan;
+  if (!p || i < 0 || i >= (int)p->ops.size() || iters < 1 || !us) return -1;
+  const sdmi_rt::Op& op = p->ops[i];
+  if (op.kind != sdmi_rt::OP_LAUNCH) return -2;
+  void** ptrs = p->scratch.data();
+  const unsigned char* base = (const unsigned char*)op.args.data();
+  for (size_t a = 0; a < op.offs.size(); ++a) ptrs[a] = (void*)(base + op.offs[a]);
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return -3;
+  if (hipEventCreate(&e1) != hipSuccess) return -3;
+  hipError_t e = hipSuccess;
+  for (int w = 0; w < warm && e == hipSuccess; ++w) e = hipLaunchKernel(op.fn, op.grid, op.block, ptrs, op.shmem, op.stream);
+  if (e == hipSuccess) e = hipEventRecord(e0, op.stream);
+  for (int r = 0; r < iters && e == hipSuccess; ++r) e = hipLaunchKernel(op.fn, op.grid, op.block, ptrs, op.shmem, op.stream);
+  if (e == hipSuccess) e = hipEventRecord(e1, op.stream);
+  if (e == hipSuccess) e = hipEventSynchronize(e1);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (e != hipSuccess) return (int)e;
+  *us = ms * 1000.f / (float)iters;
+  return 0;
+}
+
 extern "C" int sdmi_plan_destroy(void* plan) {
   delete (Plan*)plan;
   return 0;

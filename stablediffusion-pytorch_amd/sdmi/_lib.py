@@ -42,6 +42,8 @@ class GemmDesc(ctypes.Structure):
         ("aux", ctypes.c_void_p), ("ld_aux", ctypes.c_int),
         ("splits_hint", ctypes.c_int),
         ("tile_n_hint", ctypes.c_int),
+        ("sum_out", ctypes.c_void_p), ("sum_out2", ctypes.c_void_p), ("gsum_out", ctypes.c_void_p),
+        ("gsum_ld", ctypes.c_int), ("sum_group", ctypes.c_int),
     ]
 
 
@@ -98,7 +100,7 @@ SIGNATURES = {
     "sdmi_pack_transpose": ([_P, _P, _I, _P], _I),
     "sdmi_optim_workspace": ([], _SZ),
     "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
-    "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _P], _I),
+    "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _F, _P], _I),
     "sdmi_ln_chunk_rows": ([_I], _I),
     "sdmi_ln_mod_fwd": ([_P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _I, _F, _I, _P], _I),
     "sdmi_ln_mod_bwd": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P,
@@ -122,6 +124,9 @@ SIGNATURES = {
     "sdmi_plan_info": ([_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
     "sdmi_plan_replay": ([_P, _I, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
     "sdmi_plan_destroy": ([_P], _I),
+    "sdmi_plan_op_info": ([_P, _I, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
+                           ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
+    "sdmi_plan_time_op": ([_P, _I, _I, _I, ctypes.POINTER(ctypes.c_float)], _I),
 }
 
 

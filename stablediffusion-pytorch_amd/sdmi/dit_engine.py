@@ -387,8 +387,7 @@ class DiTEngine:
             return t[:, o:o + D]
 
         # ---- proj_out + final norm ----
-        K.linear_wgrad(dpred, st["yf"], self.g("proj_out.weight"))
-        K.chan_sum(dpred, 1, M, dpred.shape[1], per_c=self.g("proj_out.bias"))
+        K.linear_wgrad(dpred, st["yf"], self.g("proj_out.weight"), bias_grad=self.g("proj_out.bias"))
         dy = self._new(M, D)
         K.linear_dgrad(dpred, self.W("proj_out.weight"), dy)
         of = 6 * D * L["n_layers"]
@@ -402,12 +401,10 @@ class DiTEngine:
             c = st["layers"][i]
             q = f"transformer_layers.{i}."
             # MLP (transformer_layer.py:104-106)
-            K.linear_wgrad(dv2, c["h"], self.g(q + "mlp_block.2.weight"))
-            K.chan_sum(dv2, 1, M, D, per_c=self.g(q + "mlp_block.2.bias"))
+            K.linear_wgrad(dv2, c["h"], self.g(q + "mlp_block.2.weight"), bias_grad=self.g(q + "mlp_block.2.bias"))
             dh = self._new(M, 4 * D)
             self._dgrad(dv2, q + "mlp_block.2.weight", dh, relu_of=c["h"])
-            K.linear_wgrad(dh, c["y2"], self.g(q + "mlp_block.0.weight"))
-            K.chan_sum(dh, 1, M, 4 * D, per_c=self.g(q + "mlp_block.0.bias"))
+            K.linear_wgrad(dh, c["y2"], self.g(q + "mlp_block.0.weight"), bias_grad=self.g(q + "mlp_block.0.bias"))
             dy2 = self._new(M, D)
             self._dgrad(dh, q + "mlp_block.0.weight", dy2)
             dv1 = self._new(M, D)
@@ -417,23 +414,23 @@ class DiTEngine:
                 self._ln_bwd(c["x2"], c["m2"], c["r2"], dy2, dxs, scale=mcol(mod, i, 4), dres=dxs,
                              psh=mcol(ws, i, 3), psc=mcol(ws, i, 4), dx16=dvc, N=N)
                 S = st["S"]
-                K.linear_wgrad(dvc, c["co"], self.g(q + "cross_attn_block.out_proj.weight"))
-                K.chan_sum(dvc, 1, M, D, per_c=self.g(q + "cross_attn_block.out_proj.bias"))
+                K.linear_wgrad(dvc, c["co"], self.g(q + "cross_attn_block.out_proj.weight"),
+                               bias_grad=self.g(q + "cross_attn_block.out_proj.bias"))
                 dco = self._new(M, D)
                 self._dgrad(dvc, q + "cross_attn_block.out_proj.weight", dco)
                 dcq, dckv = self._new(M, D), self._new(B * S, 2 * D)
                 K.attn_bwd(c["cq"], c["ckv"][:, :D], c["ckv"][:, D:], c["co"], dco, c["clse"], dcq, dckv[:, :D],
                            dckv[:, D:], B, Hh, N, S, D // Hh)
-                K.linear_wgrad(dcq, c["yc"], self.g(q + "cross_attn_block.q_proj.weight"))
-                K.chan_sum(dcq, 1, M, D, per_c=self.g(q + "cross_attn_block.q_proj.bias"))
-                K.linear_wgrad(dckv[:, :D], c["cp"], self.g(q + "cross_attn_block.k_proj.weight"))
-                K.chan_sum(dckv[:, :D], 1, B * S, D, per_c=self.g(q + "cross_attn_block.k_proj.bias"))
-                K.linear_wgrad(dckv[:, D:], c["cp"], self.g(q + "cross_attn_block.v_proj.weight"))
-                K.chan_sum(dckv[:, D:], 1, B * S, D, per_c=self.g(q + "cross_attn_block.v_proj.bias"))
+                K.linear_wgrad(dcq, c["yc"], self.g(q + "cross_attn_block.q_proj.weight"),
+                               bias_grad=self.g(q + "cross_attn_block.q_proj.bias"))
+                K.linear_wgrad(dckv[:, :D], c["cp"], self.g(q + "cross_attn_block.k_proj.weight"),
+                               bias_grad=self.g(q + "cross_attn_block.k_proj.bias"))
+                K.linear_wgrad(dckv[:, D:], c["cp"], self.g(q + "cross_attn_block.v_proj.weight"),
+                               bias_grad=self.g(q + "cross_attn_block.v_proj.bias"))
                 dcp = self._new(B * S, D)
                 self._dgrad(dckv, q + "kv", dcp)
-                K.linear_wgrad(dcp, st["ctx"], self.g(q + "context_proj.weight"))
-                K.chan_sum(dcp, 1, B * S, D, per_c=self.g(q + "context_proj.bias"))
+                K.linear_wgrad(dcp, st["ctx"], self.g(q + "context_proj.weight"),
+                               bias_grad=self.g(q + "context_proj.bias"))
                 dyc = self._new(M, D)
                 self._dgrad(dcq, q + "cross_attn_block.q_proj.weight", dyc)
                 self._ln_bwd(c["xc"], c["mc"], c["rc"], dyc, dxs, dres=dxs, gate=mcol(mod, i, 2), v=c["v1"], dv=dv1,
@@ -442,16 +439,16 @@ class DiTEngine:
                 self._ln_bwd(c["x2"], c["m2"], c["r2"], dy2, dxs, scale=mcol(mod, i, 4), dres=dxs, psh=mcol(ws, i, 3),
                              psc=mcol(ws, i, 4), gate=mcol(mod, i, 2), v=c["v1"], dv=dv1, pg=mcol(ws, i, 2), N=N)
             # self attention (attention.py:33-78)
-            K.linear_wgrad(dv1, c["o"], self.g(q + "attn_block.output_proj.0.weight"))
-            K.chan_sum(dv1, 1, M, D, per_c=self.g(q + "attn_block.output_proj.0.bias"))
+            K.linear_wgrad(dv1, c["o"], self.g(q + "attn_block.output_proj.0.weight"),
+                           bias_grad=self.g(q + "attn_block.output_proj.0.bias"))
             do = self._new(M, A)
             self._dgrad(dv1, q + "attn_block.output_proj.0.weight", do)
             qkv = c["qkv"]
             dqkv = self._new(M, 3 * A)
             K.attn_bwd(qkv[:, :A], qkv[:, A:2 * A], qkv[:, 2 * A:], c["o"], do, c["lse"], dqkv[:, :A],
                        dqkv[:, A:2 * A], dqkv[:, 2 * A:], B, Hh, N, N, hd)
-            K.linear_wgrad(dqkv, c["y1"], self.g(q + "attn_block.qkv_proj.weight"))
-            K.chan_sum(dqkv, 1, M, 3 * A, per_c=self.g(q + "attn_block.qkv_proj.bias"))
+            K.linear_wgrad(dqkv, c["y1"], self.g(q + "attn_block.qkv_proj.weight"),
+                           bias_grad=self.g(q + "attn_block.qkv_proj.bias"))
             dy1 = self._new(M, D)
             self._dgrad(dqkv, q + "attn_block.qkv_proj.weight", dy1)
             prev = st["layers"][i - 1] if i > 0 else None
@@ -467,16 +464,14 @@ class DiTEngine:
         dmod = self._new(B, L["mod_w"])
         _lib.check(_lib.lib().sdmi_mod_finalize(ws.data_ptr(), B, chunks, L["mod_w"], L["mod_w"], dmod.data_ptr(),
                                                 L["mod_w"], K._stream()), "sdmi_mod_finalize")
-        K.linear_wgrad(dmod, st["r"], contiguous_run(self.Gd, ada_keys(L, "weight"), (L["mod_w"], D)))
-        K.chan_sum(dmod, 1, B, L["mod_w"], per_c=contiguous_run(self.Gd, ada_keys(L, "bias"), (L["mod_w"],)))
+        K.linear_wgrad(dmod, st["r"], contiguous_run(self.Gd, ada_keys(L, "weight"), (L["mod_w"], D)),
+                       bias_grad=contiguous_run(self.Gd, ada_keys(L, "bias"), (L["mod_w"],)))
         dt = self._new(B, D)
         K.linear_dgrad(dmod, self.W("ada"), dt, relu_of=st["r"])
-        K.linear_wgrad(dt, st["h1"], self.g("t_proj.2.weight"))
-        K.chan_sum(dt, 1, B, D, per_c=self.g("t_proj.2.bias"))
+        K.linear_wgrad(dt, st["h1"], self.g("t_proj.2.weight"), bias_grad=self.g("t_proj.2.bias"))
         dh1 = self._new(B, D)
         K.linear_dgrad(dt, self.W("t_proj.2.weight"), dh1, relu_of=st["h1"])
-        K.linear_wgrad(dh1, st["e"], self.g("t_proj.0.weight"))
-        K.chan_sum(dh1, 1, B, D, per_c=self.g("t_proj.0.bias"))
+        K.linear_wgrad(dh1, st["e"], self.g("t_proj.0.weight"), bias_grad=self.g("t_proj.0.bias"))
         if st.get("cls") is not None:  # d class_emb.weight = class^T @ d(t_emb), d(t_emb) = dh1 @ W(t_proj.0)
             de = self._new(B, L["T"])
             K.linear_dgrad(dh1, self.W("t_proj.0.weight"), de)
@@ -486,8 +481,8 @@ class DiTEngine:
         gh, gw = H // p, W // p
         xin = st["xin"]
         K.conv_wgrad(dtok, D, xin, B, H, W, self.cpad, self.cpad, D, p, p, p, 0,
-                     self.g("patch_embed_layer.patch_embed.0.weight"), gh, gw, perm=(self.cpad, p * p, L["patch_in"], 2))
-        K.chan_sum(dtok, 1, M, D, per_c=self.g("patch_embed_layer.patch_embed.0.bias"))
+                     self.g("patch_embed_layer.patch_embed.0.weight"), gh, gw, perm=(self.cpad, p * p, L["patch_in"], 2),
+                     bias_grad=self.g("patch_embed_layer.patch_embed.0.bias"))
         if L["image"]:
             # d(patch source): each input pixel feeds exactly one token -> p*p sub-pixel GEMMs [M, D] x [D, cpad]
             dxin = self._new(B * H * W, self.cpad)

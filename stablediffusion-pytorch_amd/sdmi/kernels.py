@@ -24,6 +24,8 @@ def _stream():
 
 # optional per-launch timing hook (bench.py): list of (tag, flops, start_event, end_event, info)
 PROFILE = None
+# optional GEMM call log (scripts/plan_profile.py): list of (m, n, k, a_mode, b_mode, splits, tile_n, phase, kernel info)
+GEMM_LOG = None
 PHASE = ""  # label prefixed to profiled launches ("fwd" / "bwd" / "wg" ...; set by the engines)
 # phases whose GEMMs may take the 192-column tile (measured per phase: faster in fwd / bwd; in the weight-gradient
 # phase its 80 KiB of LDS per workgroup crowds out the concurrent streams and the step ran 0.4 ms slower)
@@ -70,7 +72,8 @@ class _Prof:
 
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
          rb_ld=0, rb_div=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0,
-         a2=None, lda2=0, k_split=0, bias2=None, rb_mod=0, aux=None, ld_aux=0):
+         a2=None, lda2=0, k_split=0, bias2=None, rb_mod=0, aux=None, ld_aux=0, sum_out=None, sum_out2=None,
+         gsum=None, sum_group=0):
     """C[m][n] = epi(sum_k A[m][k] B[k][n]).  a/b/c/resid/rowbias are tensors (pointer = data_ptr,
     offsets already applied by slicing); see include/sdmi.h for the operand modes."""
     L = _lib.lib()
@@ -105,6 +108,11 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     d.rb_mod = rb_mod
     if aux is not None:
         d.aux, d.ld_aux = aux.data_ptr(), ld_aux or ld_of(aux)
+    if sum_out is not None or sum_out2 is not None or gsum is not None:  # reductions of A (col-major A only)
+        d.sum_out = _p(sum_out)
+        d.sum_out2 = _p(sum_out2)
+        if gsum is not None:
+            d.gsum_out, d.gsum_ld, d.sum_group = gsum.data_ptr(), ld_of(gsum), sum_group
     d.tile_n_hint = 0 if (not PHASE or PHASE in TILE192_PHASES) else 128
     tuned = _tuned()
     if tuned:
@@ -116,6 +124,12 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     if ws_bytes.value:
         ws = torch.empty(ws_bytes.value // 4, dtype=torch.float32, device=c.device)
     info = ""
+    if GEMM_LOG is not None:
+        var, tn = ctypes.c_int(0), ctypes.c_int(0)
+        check(L.sdmi_gemm_kernel_info(ctypes.byref(d), ctypes.byref(var), ctypes.byref(tn)), "sdmi_gemm_kernel_info")
+        GEMM_LOG.append(dict(m=m, n=n, k=k, a=a_mode, b=b_mode, splits=splits.value, tile_n=tn.value, variant=var.value,
+                             phase=PHASE, conv=geom is not None and a_mode == _lib.A_CONV and (geom or {}).get("kh", 1),
+                             flops=2.0 * m * n * k))
     if PROFILE is not None:  # attribute the launch to its kernel instantiation (roofline / profiles)
         var, tn = ctypes.c_int(0), ctypes.c_int(0)
         check(L.sdmi_gemm_kernel_info(ctypes.byref(d), ctypes.byref(var), ctypes.byref(tn)), "sdmi_gemm_kernel_info")
@@ -154,10 +168,12 @@ def conv_fwd(x, B, H, W, cin, ldx, wpk, cout, kh, kw, stride, pad, out, ldo, *, 
 
 
 def conv_wgrad(dy, ldy, x, B, H, W, cin, ldx, cout, kh, kw, stride, pad, out, OH, OW, *, perm=True, cvalid=0,
-               m_store=0):
+               m_store=0, bias_grad=None, bias_grad2=None, group_sums=None):
     """dW[co][(ty,tx,ci)] = sum_pixels dy[p, co] * x[gather(p, ty, tx), ci]; written fp32 in torch
     layout (co, ci, kh, kw) when perm is True (only ci < cvalid, co < m_store when given); perm may also be
-    an explicit (p_cin, p_taps, p_cvalid, mode) tuple (mode 2: tap-major (co, kh, kw, ci) Linear layout)."""
+    an explicit (p_cin, p_taps, p_cvalid, mode) tuple (mode 2: tap-major (co, kh, kw, ci) Linear layout).
+    In the same launch: bias_grad[co] (and bias_grad2) = sum_pixels dy[p, co], group_sums[b][co] (bf16 2-D view) =
+    per-sample sums -- the column-sum passes of the conv bias and time-embedding gradients."""
     g = conv_geom(H, W, cin, ldx, kh, kw, OH, OW, stride, stride, -pad, -pad)
     cv = cvalid or cin
     if perm is True:
@@ -165,7 +181,8 @@ def conv_wgrad(dy, ldy, x, B, H, W, cin, ldx, cout, kh, kw, stride, pad, out, OH
     elif isinstance(perm, tuple):
         cv = perm[2]
     return gemm(cout, kh * kw * cin, B * OH * OW, dy, _lib.A_COLMAJOR, ldy, x, _lib.B_KN_CONV, 0, out,
-                kh * kw * cv, geom=g, perm=perm or None, m_store=m_store)
+                kh * kw * cv, geom=g, perm=perm or None, m_store=m_store, sum_out=bias_grad, sum_out2=bias_grad2,
+                gsum=group_sums, sum_group=OH * OW)
 
 
 # stride-2, 4x4, pad-1 transposed convolution as four 2x2 sub-pixel convolutions.
@@ -227,11 +244,13 @@ def linear_dgrad_t(dy, wt, out, *, resid=None, relu_of=None):
                 ldr=ld_of(resid) if resid is not None else 0, act=3 if relu_of is not None else 0, aux=relu_of)
 
 
-def linear_wgrad(dy, x, out):
-    """out[n][k] = sum_m dy[m][n] x[m][k]  (fp32 weight gradient, out [N,K] contiguous rows)."""
+def linear_wgrad(dy, x, out, *, bias_grad=None, bias_grad2=None, group_sums=None, group=0, m_store=0):
+    """out[n][k] = sum_m dy[m][n] x[m][k]  (fp32 weight gradient, out [N,K] contiguous rows); in the same launch
+    bias_grad[n] (and bias_grad2) = sum_m dy[m][n] and group_sums[g][n] (bf16) = sums over rows [g*group, ...)."""
     M, N = dy.shape
     K = x.shape[1]
-    return gemm(N, K, M, dy, _lib.A_COLMAJOR, ld_of(dy), x, _lib.B_KN, ld_of(x), out, out.stride(0))
+    return gemm(N, K, M, dy, _lib.A_COLMAJOR, ld_of(dy), x, _lib.B_KN, ld_of(x), out, out.stride(0),
+                sum_out=bias_grad, sum_out2=bias_grad2, gsum=group_sums, sum_group=group, m_store=m_store)
 
 
 def gn_stats(x, B, P, C, G, gamma, beta, eps=1e-5):

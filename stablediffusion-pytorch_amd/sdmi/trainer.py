@@ -183,7 +183,7 @@ class DDPMTrainer:
         if self.opt_ranges is None:
             _lib.check(L.sdmi_adam_ema(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                                        K._p(self.ema), st.numel, self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"],
-                                       hp["eps"], ema_decay, K._stream()), "sdmi_adam_ema")
+                                       hp["eps"], ema_decay, 1.0 - ema_decay, K._stream()), "sdmi_adam_ema")
             eng.refresh_weights()
             return self.state
         side = eng.side
@@ -194,7 +194,7 @@ class DDPMTrainer:
                 _lib.check(L.sdmi_adam_ema(st.params[lo:hi].data_ptr(), st.grads[lo:hi].data_ptr(),
                                            self.m[lo:hi].data_ptr(), self.v[lo:hi].data_ptr(), K._p(e), hi - lo,
                                            self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"], hp["eps"], ema_decay,
-                                           K._stream()), "sdmi_adam_ema")
+                                           1.0 - ema_decay, K._stream()), "sdmi_adam_ema")
                 eng.pack.run_chunk(c)
                 plan.record_event(self.opt_events[c], side)
             late = eng.pack.late_chunk

@@ -690,8 +690,9 @@ class UNetEngine:
         dy, _ = grads.get(c["yn"])
         ldy = K.ld_of(dy)
         with self._wg(dy):
-            K.conv_wgrad(dy, ldy, c["h2"], B, h, w, cout, cout, cout, 3, 3, 1, 1, self.g(b + ".2.weight"), h, w)
-            K.chan_sum(dy, B, Pn, cout, per_c=self.g(b + ".2.bias"), per_c2=self.g(rc + ".bias"))
+            # conv2 and residual-conv bias gradients (both = column sums of dy) come out of the same launch
+            K.conv_wgrad(dy, ldy, c["h2"], B, h, w, cout, cout, cout, 3, 3, 1, 1, self.g(b + ".2.weight"), h, w,
+                         bias_grad=self.g(b + ".2.bias"), bias_grad2=self.g(rc + ".bias"))
             K.linear_wgrad(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
         dh2 = self._new(B * Pn, cout)
         K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout)
@@ -704,9 +705,11 @@ class UNetEngine:
                  self.g(b + ".0.weight"), self.g(b + ".0.bias"))
         off = self.temb_off[(p, l)]
         with self._wg(dh2):
-            K.chan_sum(dh2, B, Pn, cout, per_bc=self.dtemb_all[:, off:off + cout], per_c=self.g(a + ".2.bias"),
-                       per_c2=self.g(f"{p}.t_emb_layers.{l}.1.bias"))
-            K.conv_wgrad(dh2, cout, c["h0"], B, h, w, cin, cin, cout, 3, 3, 1, 1, self.g(a + ".2.weight"), h, w)
+            # conv1 bias, t_emb_layers bias and the per-sample time-embedding gradient (blocks.py:117-118) are
+            # reductions of dh2 computed by the weight-gradient launch itself
+            K.conv_wgrad(dh2, cout, c["h0"], B, h, w, cin, cin, cout, 3, 3, 1, 1, self.g(a + ".2.weight"), h, w,
+                         bias_grad=self.g(a + ".2.bias"), bias_grad2=self.g(f"{p}.t_emb_layers.{l}.1.bias"),
+                         group_sums=self.dtemb_all[:, off:off + cout])
         dh0 = self._new(B * Pn, cin)
         K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin)
         K.gn_bwd(c["x"], dh0, dx, c["t1"], P[a + ".0.weight"], B, Pn, cin, G, True,
@@ -753,8 +756,7 @@ class UNetEngine:
         d = C // Hh
         dy, _ = grads.get(c["yn"])
         with self._wg(dy):
-            K.linear_wgrad(dy, c["o"], self.g(mk + ".out_proj.weight"))
-            K.chan_sum(dy, 1, B * N, C, per_c=self.g(mk + ".out_proj.bias"))
+            K.linear_wgrad(dy, c["o"], self.g(mk + ".out_proj.weight"), bias_grad=self.g(mk + ".out_proj.bias"))
         dy_read = self.wg_event if self.side is not None else None
         do = self._new(B * N, C)
         self._dgrad(dy, mk + ".out_proj", do)
@@ -769,8 +771,7 @@ class UNetEngine:
             K.attn_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], c["o"], do, c["lse"], dqkv[:, :C],
                        dqkv[:, C:2 * C], dqkv[:, 2 * C:], B, Hh, N, N, d)
             with self._wg(dqkv):
-                K.linear_wgrad(dqkv, c["a"], gW)
-                K.chan_sum(dqkv, 1, B * N, 3 * C, per_c=gb)
+                K.linear_wgrad(dqkv, c["a"], gW, bias_grad=gb)
             if WinT is not None:
                 K.linear_dgrad_t(dqkv, WinT, da)
             else:
@@ -781,18 +782,15 @@ class UNetEngine:
             dkv = self._new(B * S, 2 * C)
             K.attn_bwd(c["q"], kv[:, :C], kv[:, C:], c["o"], do, c["lse"], dq, dkv[:, :C], dkv[:, C:], B, Hh, N, S, d)
             with self._wg(dq, dkv):
-                K.linear_wgrad(dq, c["a"], gW[:C])
-                K.chan_sum(dq, 1, B * N, C, per_c=gb[:C])
-                K.linear_wgrad(dkv, c["cp"], gW[C:])
-                K.chan_sum(dkv, 1, B * S, 2 * C, per_c=gb[C:])
+                K.linear_wgrad(dq, c["a"], gW[:C], bias_grad=gb[:C])
+                K.linear_wgrad(dkv, c["cp"], gW[C:], bias_grad=gb[C:])
             dcp = self._new(B * S, C)
             if WinT is not None:
                 K.linear_dgrad_t(dkv, WinT[:, C:], dcp)
             else:
                 K.linear_dgrad(dkv, Win[C:], dcp)
             with self._wg(dcp):
-                K.linear_wgrad(dcp, c["ctx"], self.g(c["ck"] + ".weight"))
-                K.chan_sum(dcp, 1, B * S, C, per_c=self.g(c["ck"] + ".bias"))
+                K.linear_wgrad(dcp, c["ctx"], self.g(c["ck"] + ".weight"), bias_grad=self.g(c["ck"] + ".bias"))
             if WinT is not None:
                 K.linear_dgrad_t(dq, WinT[:, :C], da)
             else:
@@ -830,8 +828,7 @@ class UNetEngine:
         ldy = K.ld_of(dy)
         with self._wg(dy):
             K.conv_wgrad(dy, ldy, c["x"], B, h, w, C, K.ld_of(c["x"]), C, 4, 4, 2, 1, self.g(key + ".weight"),
-                         h // 2, w // 2)
-            K.chan_sum(dy, B, (h // 2) * (w // 2), C, per_c=self.g(key + ".bias"))
+                         h // 2, w // 2, bias_grad=self.g(key + ".bias"))
         dx, fresh = grads.get(c["xn"])
         wph = [self.W(f"{key}#d{ph}{pw}") for ph in range(2) for pw in range(2)]
         K.conv_dgrad_phases(dy, B, h, w, C, ldy, wph, C, dx, K.ld_of(dx), resid=None if fresh else dx,
@@ -873,8 +870,7 @@ class UNetEngine:
         dpred = self.dpred
         with self._wg(dpred):
             K.conv_wgrad(dpred, 8, c["hs"], B, H, W, C, C, 8, 3, 3, 1, 1, self.g("conv_out.weight"), H, W,
-                         m_store=self.im_channels)
-            K.chan_sum(dpred, B, Pn, 8, per_c=self.g("conv_out.bias"), c_store=self.im_channels)
+                         m_store=self.im_channels, bias_grad=self.g("conv_out.bias"))
         dhs = self._new(B * Pn, C)
         K.conv_fwd(dpred, B, H, W, 8, 8, self.W("conv_out#d"), C, 3, 3, 1, 1, dhs, C)
         dx, fresh = grads.get(c["xn"])
@@ -890,8 +886,7 @@ class UNetEngine:
         cin_real = self.im_channels + (L["im_out"] if L["image"] else 0)
         with self._wg(dy):
             K.conv_wgrad(dy, ldy, c["xin"], B, H, W, self.cin_pad, self.cin_pad, C0, 3, 3, 1, 1,
-                         self.g(self.first + ".weight"), H, W, cvalid=cin_real)
-            K.chan_sum(dy, B, H * W, C0, per_c=self.g(self.first + ".bias"))
+                         self.g(self.first + ".weight"), H, W, cvalid=cin_real, bias_grad=self.g(self.first + ".bias"))
         if L["image"]:
             dxin = self._new(B * H * W, self.cin_pad)
             K.conv_fwd(dy, B, H, W, C0, ldy, self.W(self.first + "#d"), self.cin_pad, 3, 3, 1, 1, dxin, self.cin_pad)
@@ -913,14 +908,12 @@ class UNetEngine:
         if c.get("cls") is not None:  # d class_emb.weight = class^T @ dtemb (A = the bf16 class rows, col-major)
             K.gemm(self.kpad, T, B, c["cls"], _lib.A_COLMAJOR, self.kpad, dtemb, _lib.B_KN, T,
                    self.g("class_emb.weight"), T, m_store=L["num_classes"])
-        K.linear_wgrad(dtemb, c["s1"], self.g("t_proj.2.weight"))
-        K.chan_sum(dtemb, 1, B, T, per_c=self.g("t_proj.2.bias"))
+        K.linear_wgrad(dtemb, c["s1"], self.g("t_proj.2.weight"), bias_grad=self.g("t_proj.2.bias"))
         ds1 = self._new(B, T)
         K.linear_dgrad(dtemb, self.W("t_proj.2#f"), ds1)
         dh1 = self._new(B, T)
         _lib.check(lib.sdmi_silu(c["h1"].data_ptr(), ds1.data_ptr(), dh1.data_ptr(), B * T, K._stream()), "silu")
-        K.linear_wgrad(dh1, c["e"], self.g("t_proj.0.weight"))
-        K.chan_sum(dh1, 1, B, T, per_c=self.g("t_proj.0.bias"))
+        K.linear_wgrad(dh1, c["e"], self.g("t_proj.0.weight"), bias_grad=self.g("t_proj.0.bias"))
 
     # ------------------------------------------------------------------------------------------
     def loss(self, pred, noise, dpred, loss_out, gscale_dev=None, gscale=1.0):

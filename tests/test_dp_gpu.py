@@ -118,7 +118,8 @@ def _reference_steps(tr, world, ema_decay):
                                        ws.data_ptr(), 2000, 0, float(world), K._stream()), "clip")
         _lib.check(L.sdmi_adam_ema(tr.store.params.data_ptr(), tr.store.grads.data_ptr(), tr.m.data_ptr(),
                                    tr.v.data_ptr(), K._p(tr.ema), tr.store.numel, tr.state.data_ptr(), 1e-3, 0.9,
-                                   0.999, 1e-8, ema_decay or 0.0, K._stream()), "adam")
+                                   0.999, 1e-8, ema_decay or 0.0, 1.0 - (ema_decay or 0.0),
+                                   K._stream()), "adam")
         tr.engine.refresh_weights()
     torch.cuda.synchronize()
 

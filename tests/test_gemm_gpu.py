@@ -144,3 +144,60 @@ def test_conv_fwd_tile192():
     out = torch.empty(B, H, H, cout, device="cuda", dtype=torch.bfloat16)
     k.conv_fwd(xn, B, H, H, cin, cin, wpk, cout, 3, 3, 1, 1, out, cout)
     close(out.permute(0, 3, 1, 2), ref)
+
+
+@pytest.mark.parametrize("M,N,K,group,splits", [(136, 264, 200, 50, 0), (384, 384, 32768, 1024, 0),
+                                                 (512, 512, 2048, 64, 1), (128, 128, 4096, 256, 8)])
+def test_wgrad_with_fused_bias_and_group_sums(M, N, K, group, splits):
+    """Weight-gradient GEMM (col-major A = dY^T) with the bias gradient (row sums of A over k) and per-group sums
+    (per-sample time-embedding gradient) produced by the same launch through synthesised B columns; with and
+    without split-K (the reducer applies the same routing)."""
+    k, L = _k()
+    torch.manual_seed(7)
+    dy = bf(torch.randn(K, M, device="cuda"))
+    x = bf(torch.randn(K, N, device="cuda"))
+    out = torch.empty(M, N, device="cuda")
+    bg = torch.full((M,), float("nan"), device="cuda")
+    bg2 = torch.full((M,), float("nan"), device="cuda")
+    G = (K + group - 1) // group
+    gs = torch.zeros(G, M + 16, device="cuda", dtype=torch.bfloat16)[:, 8:8 + M]
+    if splits:
+        k.TUNED = {k.gemm_key(_desc(k, L, M, N, K)): splits}
+    try:
+        k.gemm(M, N, K, dy, L.A_COLMAJOR, M, x, L.B_KN, N, out, N, sum_out=bg, sum_out2=bg2, gsum=gs, sum_group=group)
+    finally:
+        k.TUNED = None
+    torch.cuda.synchronize()
+    close(out, dy.float().t() @ x.float(), 2e-3)
+    ref = dy.float().sum(0)
+    close(bg, ref, 1e-5)
+    assert torch.equal(bg, bg2)
+    gref = torch.stack([dy.float()[g * group:(g + 1) * group].sum(0) for g in range(G)])
+    close(gs, gref, 1e-2)
+
+
+def _desc(k, L, M, N, K):
+    d = L.GemmDesc()
+    d.m, d.n, d.k, d.a_mode, d.b_mode = M, N, K, L.A_COLMAJOR, L.B_KN
+    return d
+
+
+def test_conv_wgrad_with_fused_bias_and_group_sums():
+    """conv_wgrad (implicit im2col B) with the conv-bias and per-sample sums of dY fused, at a non-power-of-two
+    grid (B=3, 12x20)."""
+    k, L = _k()
+    torch.manual_seed(8)
+    B, H, W, C, O = 3, 12, 20, 32, 48
+    x = bf(torch.randn(B * H * W, C, device="cuda"))
+    dy = bf(torch.randn(B * H * W, O, device="cuda"))
+    dw = torch.empty(O, C, 3, 3, device="cuda")
+    bg = torch.empty(O, device="cuda")
+    gs = torch.empty(B, O, device="cuda", dtype=torch.bfloat16)
+    k.conv_wgrad(dy, O, x, B, H, W, C, C, O, 3, 3, 1, 1, dw, H, W, bias_grad=bg, group_sums=gs)
+    torch.cuda.synchronize()
+    xn = x.float().view(B, H, W, C).permute(0, 3, 1, 2)
+    dyn = dy.float().view(B, H, W, O).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xn, (O, C, 3, 3), dyn, padding=1)
+    close(dw, ref, 2e-3)
+    close(bg, dyn.sum((0, 2, 3)), 1e-5)
+    close(gs, dyn.sum((2, 3)), 1e-2)

@@ -300,9 +300,9 @@ def test_cond_trainer_two_steps_match_reference():
     """The headline step (train_ddpm_cond_celebhq_multi_gpu.py:341-378) -- add_noise, bf16 forward, MSE x loss scale
     (GradScaler init 65536), backward, unscale, clip_grad_norm_(1.0), Adam(1e-5), EMA(0.9999) -- through
     sdmi.trainer.DDPMTrainer, two steps against the reference's own two fp32 steps (train_step_small_cond fixture):
-    loss within 1 %, pre-clip gradient norm within 5 %, and for every fixture key the parameter update and the EMA
-    update (ema - init) point the same way (cosine >= 0.9) with magnitudes within 10 %. Against the fp32 oracle step
-    (same inputs) the update of the whole flat parameter vector has cosine >= 0.95."""
+    loss within 1 %, pre-clip gradient norm within 5 %, for every fixture key the parameter update points the same
+    way (cosine >= 0.9, magnitude within 10 %) and the EMA copy equals the reference's within fp32 rounding. Against
+    the fp32 oracle step (same inputs) the update of the whole flat parameter vector has cosine >= 0.95."""
     from safetensors.torch import load_file
     from sdmi.trainer import DDPMTrainer, S_LOSS, S_NORM, S_SCALE
     f = load_file(os.path.join(os.path.dirname(__file__), "golden", "train_step_small_cond.safetensors"))
@@ -332,11 +332,45 @@ def test_cond_trainer_two_steps_match_reference():
         key = k[6:]
         n = f[k].numel()
         init = sd0[key].reshape(-1)[:n]
-        for mine, want, what in ((sd[key].reshape(-1)[:n].cpu(), f[k], "param"),
-                                 (ema_hip[key].reshape(-1)[:n].cpu(), f["ema." + key], "ema")):
-            d_hip, d_ref = (mine - init).double(), (want - init).double()
-            assert cos(d_hip, d_ref) >= 0.9, (what, key, cos(d_hip, d_ref))
-            assert abs(d_hip.norm() - d_ref.norm()) <= 0.1 * d_ref.norm(), (what, key)
+        mine = sd[key].reshape(-1)[:n].cpu()
+        d_hip, d_ref = (mine - init).double(), (f[k] - init).double()
+        assert cos(d_hip, d_ref) >= 0.9, (key, cos(d_hip, d_ref))
+        assert abs(d_hip.norm() - d_ref.norm()) <= 0.1 * d_ref.norm(), key
+        # EMA(0.9999): its two-step move (1e-4 of a ~1e-5 update) sits at the fp32 resolution of the weights, so it
+        # is checked element-wise: within 4 ulp of the reference's EMA plus 1e-4 x the parameter difference
+        # (test_ema_follows_oracle_at_large_lr checks the EMA arithmetic where its move is resolvable)
+        e_hip, e_ref = ema_hip[key].reshape(-1)[:n].cpu().double(), f["ema." + key].double()
+        # EMA difference = 1e-4 x (step-1 param difference + step-2 param difference); Adam moves a parameter by at
+        # most ~lr per step, so the (unstored) step-1 difference is bounded by 2 lr = 2e-5
+        tol = 4 * 1.2e-7 * e_ref.abs() + 1e-4 * ((mine.double() - f[k].double()).abs() + 2e-5) + 1e-12
+        bad = (e_hip - e_ref).abs() > tol
+        j = int(((e_hip - e_ref).abs() - tol).argmax())
+        assert not bad.any(), (key, int(bad.sum()), n, e_hip[j].item(), e_ref[j].item(), init[j].item(), mine[j].item(),
+                               f[k][j].item())
     p = torch.cat([sd[k].flatten().cpu() - sd0[k].flatten() for k in tr.store.order])
     r = torch.cat([ref[k].flatten() - sd0[k].flatten() for k in tr.store.order])
     assert cos(p, r) >= 0.95, cos(p, r)
+
+
+def test_ema_follows_oracle_at_large_lr():
+    """The fused optimizer's EMA stream (adam_ema_kernel) against the oracle's ema.mul_(d).add_(p, alpha=1-d) where the
+    EMA's move is far above fp32 resolution: lr 1e-3, decay 0.9, two steps; the EMA update (ema - init) has cosine
+    >= 0.95 with the oracle's and its norm is within 5 %."""
+    from sdmi.trainer import DDPMTrainer
+    cfg = SMALL_COND
+    sd0 = O.deterministic_state(O.unet_param_shapes(cfg), seed=8)
+    tr = DDPMTrainer(cfg, sd0, "cuda", lr=1e-3, ema_decay=0.9)
+    ref = {k: v.clone() for k, v in sd0.items()}
+    ema = {k: v.clone() for k, v in sd0.items()}
+    opt = O.AdamState(ref)
+    sched = O.SchedulerTables(1000, 0.00085, 0.012)
+    for s in range(2):
+        x, t, c = inputs(2, cfg, True, seed=60 + s)
+        noise = torch.randn(x.shape, generator=torch.Generator().manual_seed(70 + s))
+        tr.step(x.cuda(), noise.cuda(), t.cuda(), c["text"].cuda(), c["image"].cuda())
+        O.train_step(ref, ema, opt, cfg, sched, x, noise, t, c, lr=1e-3, ema_decay=0.9)
+    e = tr.ema_state_dict()
+    d_hip = torch.cat([(e[k].cpu() - sd0[k]).flatten() for k in tr.store.order])
+    d_ref = torch.cat([(ema[k] - sd0[k]).flatten() for k in tr.store.order])
+    assert cos(d_hip, d_ref) >= 0.95, cos(d_hip, d_ref)
+    assert abs(d_hip.norm() - d_ref.norm()) <= 0.05 * d_ref.norm(), (d_hip.norm(), d_ref.norm())
