@@ -36,6 +36,10 @@ WORKLOADS = {
     # VQVAE encode + decode (no grad) of a batch of 8 CelebHQ-256 images: 2.9497e11 FLOP per image
     "vqvae": dict(metric="VQVAE encode+decode steps/sec (celebhq.yaml autoencoder, 256x256, B=8) on MI355X",
                   flop=8 * 2.9497e11),
+    # DDPM sampling (tools/sample_ddpm_text_image_cond.py loop, train_num_samples = 1 in the reference config):
+    # one step = cond-UNet forward at batch --sample-batch + the reverse step; fwd 1.2988e12 FLOP at B=32
+    "sample": dict(metric="DDPM sampling steps/sec (cond-UNet, CelebHQ-256 latents, captured loop) on MI355X",
+                   flop=1.2988e12 / 32),
 }
 PEAK_BF16 = 2.5e15             # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
@@ -236,16 +240,64 @@ def main_vqvae(args, wl, world, rank, device):
         dist.destroy_process_group()
 
 
+def main_sample(args, wl, world, rank, device):
+    """Reverse-diffusion sampling throughput: the cond-UNet sampler loop recorded once and replayed (sdmi.sampling),
+    against the same loop issued step by step (eager). Replicas for N > 1 (sampling does not shard)."""
+    import models.unet_cond_base as mc
+    from scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    from sdmi.sampling import DDPMSampleLoop
+    cfg = cond_config()
+    torch.manual_seed(1111)
+    model = mc.Unet(4, cfg).to(device).eval()
+    B = args.sample_batch
+    x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
+    sched = LinearNoiseScheduler(1000, 0.00085, 0.012)
+    loop = DDPMSampleLoop(model, sched, (B, 4, 32, 32), cond_input={"text": text, "image": mask}, seed=rank)
+    xT = torch.randn(B, 4, 32, 32, generator=torch.Generator().manual_seed(5 + rank)).to(device)
+    res = {}
+    for mode in ("captured", "eager"):
+        cap = mode == "captured"
+        loop.run(xT, steps=args.warmup + 1, captured=cap)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        loop.run(xT, steps=args.steps, captured=cap)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            e = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = e.item()
+        res[mode] = args.steps / el
+    sps = res["captured"]
+    result = {"metric": wl["metric"], "value": sps * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+              "warmup": args.warmup, "ms_per_step": 1000.0 / sps, "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": "bf16", "data": "synthetic latents / text / masks, random-init weights",
+              "config": {"workload": "cond-UNet DDPM reverse step (model forward + sample_prev_timestep), captured",
+                         "model": "cond-UNet 118.5M", "samples_per_gpu": B, "latent": [4, 32, 32],
+                         "parallelism": f"replicas{world}"},
+              "eager_steps_per_s": res["eager"], "captured_speedup": sps / res["eager"],
+              "model_flops_utilization": wl["flop"] * B * sps / PEAK_BF16}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--sample-batch", type=int, default=1, help="samples per GPU of --workload sample (reference: 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="cond-unet", choices=sorted(WORKLOADS),
                     help="cond-unet (the headline metric, default), uncond-unet (celebhq.yaml), dit (DiT-12L training "
-                         "step) or vqvae (encode + decode)")
+                         "step), vqvae (encode + decode) or sample (captured DDPM sampling loop)")
     ap.add_argument("--profile-gemm", action="store_true", default=True)
     ap.add_argument("--issue", default="plan", choices=("plan", "eager", "graph"),
                     help="plan (default): the step recorded once and its native calls replayed (sdmi.plan); eager: "
@@ -279,6 +331,8 @@ def main():
     is_uncond = args.workload == "uncond-unet"
     if args.workload == "vqvae":
         return main_vqvae(args, wl, world, rank, device)
+    if args.workload == "sample":
+        return main_sample(args, wl, world, rank, device)
     cfg = dit_config() if is_dit else (uncond_config() if is_uncond else cond_config())
     torch.manual_seed(1111)  # identical initial weights on every rank (DDP broadcasts rank 0's)
     group = dist.group.WORLD if world > 1 else None

@@ -256,6 +256,12 @@ int sdmi_ddim_prev(const float* xt, const float* eps, const float* noise, long l
 int sdmi_affine_step(const float* x, const float* eps, const float* z, long long n, float c1, float c2, float var,
                      float* out, sdmi_stream_t stream);
 
+/* Device standard-normal noise (captured sampling loops): out[i] ~ N(0,1), Philox4x32-10(seed, i / 4, *offset_dev)
+ * + Box-Muller; advance != 0 increments *offset_dev after the draw (the next replay draws fresh noise). Replaces
+ * the host torch.randn of LinearNoiseScheduler.sample_prev_timestep (scheduler/linear_noise_scheduler.py:72). */
+int sdmi_randn(float* out, long long n, unsigned long long seed, unsigned long long* offset_dev, int advance,
+               sdmi_stream_t stream);
+
 /* bf16 GEMM-layout weight packing (the per-step fp32 -> bf16 cast that autocast performs,
  * train_ddpm_cond_celebhq_multi_gpu.py:281-283, fused with the layout change):
  * dst[o][a][b][i] = bf16(src[o*so + i*si + (kh_off + kh_mul*a)*skh + (kw_off + kw_mul*b)*skw]), 0 for i >= I. */

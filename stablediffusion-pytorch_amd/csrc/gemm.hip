@@ -44,6 +44,9 @@ struct Args {
   // k / grp == j (C gets per-group row sums: the per-sample time-embedding gradient). 0 = none.
   int n_x0;
   FastDiv grp_d;
+  // 1: row sums of A over k accumulated from the staged A chunks in VALU (bias gradient without the extra tile
+  // column the synthesised-column path costs; used when no per-group sums are wanted)
+  int rowsum;
 };
 
 __device__ __forceinline__ void pixel_coords(const Args& g, int m, int& b, int& oy, int& ox) {
@@ -98,6 +101,8 @@ struct EpiArgs {
   float* sum_out;
   float* sum_out2;
   bf16_t* gsum;
+  int n_gemm;  // columns the MFMA tiles produce (N, or N plus the synthesised reduction columns); with split-K the
+               // slab row width N is n_gemm + 8 when the VALU row sums ride along in slab column n_x0 = n_gemm
 };
 
 __device__ __forceinline__ long long rb_row(const EpiArgs& g, int row) {
@@ -255,7 +260,7 @@ struct Epi {
 
 // Shared epilogue of the GEMM kernels: acc = this wave's 64x64 sub-tile (4x4 MFMA tiles), smem >= 34 KB
 // of LDS that no wave reads any more (the caller synchronises before).
-template <int TBN = BN>
+template <int TBN = BN, bool XCOL = false>
 __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][TBN / 32], char* smem, int m0, int n0,
                                               int wm, int wn, int lane, int z) {
   constexpr int NJ = TBN / 32;  // 16-column MFMA tiles per wave
@@ -286,8 +291,10 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
       float v[8];
       const float4 lo = *(const float4*)(st + rl * SROW + c8), hi = *(const float4*)(st + rl * SROW + c8 + 4);
       v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      if (XCOL && col >= e.n_gemm) continue;  // beyond the produced columns (tile padding)
       if (e.raw) {
-        if (row >= e.M || col >= e.N) continue;
+        // only produced columns: with VALU row sums the slab column n_x0 = n_gemm belongs to those sums
+        if (row >= e.M || col >= e.n_gemm) continue;
         // split-K slab, device-coherent (sc1) stores: the tile's last split may run on another XCD
         const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
         const int off = (int)(((long long)z * e.split_stride + (long long)row * e.N + col) * 4);
@@ -299,7 +306,7 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
           for (int q = 0; q < 8 && col + q < e.N; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[q]), rw, off + 4 * q, 0, CPOL_SC1);
         }
-      } else if (e.n_x0 && col >= e.n_x0) {
+      } else if (XCOL && e.n_x0 && col >= e.n_x0) {
         if (row < e.M) Epi::extra(e, row, col, v, 8);
       } else if (e.vec) {
         if (row < e.m_store && col < e.n_store) Epi::finish8(e, row, col, v);
@@ -315,6 +322,21 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
     }
     __syncthreads();
   }
+}
+
+// The kernels take (const Args g, const EpiArgs e): e sits in the kernel-argument segment right after g. Reading it
+// through a laundered segment pointer AFTER the main loop keeps the compiler from hoisting ~50 scalar loads of
+// epilogue fields to the kernel entry, where they stayed live (and spilled) in SGPRs across the whole main loop.
+__device__ __forceinline__ EpiArgs epi_args_late() {
+  EpiArgs r;
+#if defined(__HIP_DEVICE_COMPILE__)  // the host compilation pass never runs device code
+  typedef __attribute__((address_space(4))) const char* kptr_t;
+  kptr_t ka = (kptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(ka));
+  constexpr size_t off = (sizeof(Args) + alignof(EpiArgs) - 1) / alignof(EpiArgs) * alignof(EpiArgs);
+  __builtin_memcpy(&r, ka + off, sizeof(EpiArgs));
+#endif
+  return r;
 }
 
 // XCD-aware tile order. Workgroups are dispatched round-robin over the 8 XCDs (dispatch id d runs on XCD d % 8,
@@ -404,7 +426,9 @@ __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0
   }
 }
 
-template <int AM, int BMODE>
+// RED (col-major A only): 0 plain GEMM, 1 + VALU row sums of A (bias gradient), 2 + synthesised reduction columns
+// (bias and per-group sums) -- compile-time so the plain instantiations carry none of it
+template <int AM, int BMODE, int RED = 0>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs e) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   // buffer b: A tile at smem + 2*b*TILE_BYTES, B tile right after it
@@ -512,7 +536,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
         int off = (n < g.N && k < g.K) ? (n * g.ldb + k) * 2 : OOB;
         rb[i] = BUF_LD(rsB, off);
       }
-    } else if (g.n_x0 && n0 + (tid & 15) * 8 >= g.n_x0) {  // reduction columns (both MN-contiguous B modes)
+    } else if (RED == 2 && n0 + (tid & 15) * 8 >= g.n_x0) {  // reduction columns (both MN-contiguous B modes)
       const int n = n0 + (tid & 15) * 8;
 #pragma unroll
       for (int i = 0; i < 4; ++i) rb[i] = reduction_cols(g, n, k0 + (tid >> 4) + 16 * i);
@@ -581,8 +605,24 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  // VALU row sums of col-major A (Args::rowsum) by the workgroups of n-tile 0: m = m0 + (tid & 15) * 8 + e
+  const bool rowsum = RED == 1 && n0 == 0;
+  float rs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto sum_rows = [&]() __attribute__((always_inline)) {
+    if (rowsum) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float t[8];
+        unpack8(ra[i], t);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) rs[q] += t[q];
+      }
+    }
+  };
+
   if (kt0 < kt1) {
     load_tiles(kt0);
+    sum_rows();
     store_tiles(0);
     __syncthreads();
     int cur = 0;
@@ -606,14 +646,43 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
           for (int j = 0; j < 4; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
       }
-      if (more) store_tiles(cur ^ 1);
+      if (more) {
+        sum_rows();
+        store_tiles(cur ^ 1);
+      }
       __syncthreads();
       cur ^= 1;
     }
   }
+  // The epilogue arguments are read through a laundered pointer into the kernel-argument segment: the compiler
+  // cannot hoist those scalar loads above this point, so ~50 EpiArgs fields are not held (and spilled) in SGPRs
+  // across the main loop.
+  const EpiArgs ev = epi_args_late();
+  const EpiArgs* ep = &ev;
+  if (rowsum) {  // combine the 16 k-row lanes of each 8-column chunk in LDS (workgroup-uniform branch)
+    float* red = (float*)smem;  // [16][128]
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[(tid >> 4) * 128 + (tid & 15) * 8 + q] = rs[q];
+    __syncthreads();
+    if (tid < BM) {
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t += red[r * 128 + tid];
+      const int m = m0 + tid;
+      if (m < ep->M) {
+        if (ep->raw) {  // slab column n_x0 of this split (the reducer routes it to sum_out / sum_out2)
+          ((float*)ep->ws)[(long long)z * ep->split_stride + (long long)m * ep->N + ep->n_x0] = t;
+        } else if (m < ep->m_store) {
+          if (ep->sum_out) ep->sum_out[m] = t;
+          if (ep->sum_out2) ep->sum_out2[m] = t;
+        }
+      }
+    }
+    __syncthreads();
+  }
 
-  gemm_epilogue(e, acc, smem, m0, n0, wm, wn, lane, z);
-  if (e.raw && e.counters) splitk_tail(e, smem, m0, n0, tl.tile);
+  gemm_epilogue<BN, RED == 2>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
+  if (ep->raw && ep->counters) splitk_tail(*ep, smem, m0, n0, tl.tile);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -864,8 +933,10 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
     }
   }
   __syncthreads();
-  gemm_epilogue<TBN>(e, acc, smem, m0, n0, wm, wn, lane, z);
-  if (e.raw && e.counters) splitk_tail<TBN>(e, smem, m0, n0, tl.tile);
+  const EpiArgs ev = epi_args_late();  // epilogue arguments loaded only from here on (see gemm_kernel)
+  const EpiArgs* ep = &ev;
+  gemm_epilogue<TBN>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
+  if (ep->raw && ep->counters) splitk_tail<TBN>(*ep, smem, m0, n0, tl.tile);
 }
 
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
@@ -967,9 +1038,12 @@ int reduction_groups(const sdmi_gemm_desc* d) {
 
 // columns the launch computes: n, plus the reduction columns (8 for the sums, then the groups rounded to 8)
 int n_total(const sdmi_gemm_desc* d) {
-  if (!has_reductions(d)) return d->n;
+  if (!d->gsum_out) return d->n;  // plain sums: VALU row sums (Args::rowsum), no extra columns
   return (d->n + 7) / 8 * 8 + 8 + (reduction_groups(d) + 7) / 8 * 8;
 }
+
+// slab row width with split-K: the produced columns, plus one 8-column chunk carrying the VALU row sums
+int slab_n(const sdmi_gemm_desc* d) { return n_total(d) + ((has_reductions(d) && !d->gsum_out) ? 8 : 0); }
 
 // Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged, 2 / 3 LDS-DMA ring
 // with that many stages, -1 (default) per mode: the DMA ring where it measured faster on the step's
@@ -1030,6 +1104,16 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
 
 template <int AM, int BMODE>
 hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
+  if constexpr (AM == SDMI_A_COLMAJOR) {
+    if (a.rowsum) {
+      sdmi_rt::launch((gemm_kernel<AM, BMODE, 1>), grid, dim3(NT), 0, s, a, e);
+      return hipGetLastError();
+    }
+    if (a.n_x0) {
+      sdmi_rt::launch((gemm_kernel<AM, BMODE, 2>), grid, dim3(NT), 0, s, a, e);
+      return hipGetLastError();
+    }
+  }
   if (v == 0) {
     sdmi_rt::launch((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
   } else if (v == 3) {
@@ -1101,6 +1185,7 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   a.A2 = (const bf16_t*)d->a2; a.lda2 = d->lda2;
   a.k_split = (d->a_mode == SDMI_A_CONV && d->a2) ? d->k_split : d->k;
   e.M = d->m; e.N = d->n;
+  e.n_gemm = n_total(d);
   e.C = d->c; e.ldc = d->ldc; e.c_f32 = d->c_f32;
   e.bias = d->bias; e.bias2 = d->bias2;
   e.rowbias = (const bf16_t*)d->rowbias; e.rb_ld = d->rb_ld;
@@ -1129,14 +1214,19 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   if (has_reductions(d)) {
     if (d->a_mode != SDMI_A_COLMAJOR || d->b_mode == SDMI_B_NK) return -13;
     if (d->gsum_out && (d->sum_group <= 0 || d->gsum_ld <= 0)) return -14;
-    a.n_x0 = e.n_x0 = (d->n + 7) / 8 * 8;
-    a.grp_d = FastDiv::make(std::max(1, d->sum_group));
+    if (d->gsum_out) {
+      a.n_x0 = e.n_x0 = (d->n + 7) / 8 * 8;
+      a.grp_d = FastDiv::make(std::max(1, d->sum_group));
+    } else {
+      a.rowsum = 1;
+      e.n_x0 = d->n;  // slab chunk of the row sums (split-K); never produced by the MFMA tiles
+    }
     e.ngrp = reduction_groups(d);
     e.gsum_ld = d->gsum_ld;
     e.sum_out = d->sum_out;
     e.sum_out2 = d->sum_out2;
     e.gsum = (bf16_t*)d->gsum_out;
-    e.N = n_total(d);  // split-K slabs and tile bounds cover the reduction columns too
+    e.N = slab_n(d);  // split-K slabs cover the reduction columns too
     const unsigned long long n8 = (unsigned long long)(e.N >> 3);
     e.n8_magic = (n8 > 1 && (unsigned long long)d->m * n8 * n8 < (1ULL << 32)) ? (unsigned)(((1ULL << 32) + n8 - 1) / n8)
                                                                               : 0u;
@@ -1158,7 +1248,7 @@ int plan_splits(const sdmi_gemm_desc* d) {
   int nkt = (d->k + BK - 1) / BK;
   if (d->splits_hint > 0) {
     int s = std::min(d->splits_hint, nkt);
-    while (s > 1 && (long long)s * d->m * n_total(d) * 4 >= (1LL << 31)) s >>= 1;
+    while (s > 1 && (long long)s * d->m * slab_n(d) * 4 >= (1LL << 31)) s >>= 1;
     return std::max(s, 1);
   }
   int s = 1;
@@ -1179,7 +1269,7 @@ int plan_splits(const sdmi_gemm_desc* d) {
   // fill the 256 CUs: deep split-K for the small-output / long-K weight gradients (a 128 x 128 dW over
   // 32768 pixels is ONE tile), keeping >= 4 k-tiles per slice and the slabs within 32-bit offsets
   while (tiles * s < 256 && nkt / (s * 2) >= 4 && s < 128 &&
-         (long long)(s * 2) * d->m * n_total(d) * 4 < (1LL << 31))
+         (long long)(s * 2) * d->m * slab_n(d) * 4 < (1LL << 31))
     s *= 2;
   return s;
 }
@@ -1203,7 +1293,7 @@ extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) 
   if (rc) return rc;
   int s = plan_splits(d);
   if (splits) *splits = s;
-  if (ws) *ws = s > 1 ? (size_t)s * d->m * n_total(d) * sizeof(float) : 0;
+  if (ws) *ws = s > 1 ? (size_t)s * d->m * slab_n(d) * sizeof(float) : 0;
   return 0;
 }
 
@@ -1214,9 +1304,9 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   int splits = plan_splits(d);
-  const int nt = n_total(d);
-  if (splits > 1 && (!workspace || ws_bytes < (size_t)splits * d->m * nt * sizeof(float))) splits = 1;
-  if ((long long)splits * d->m * nt * 4 >= (1LL << 31)) splits = 1;  // slab offsets are 32-bit
+  const int nt = n_total(d), ns = slab_n(d);
+  if (splits > 1 && (!workspace || ws_bytes < (size_t)splits * d->m * ns * sizeof(float))) splits = 1;
+  if ((long long)splits * d->m * ns * 4 >= (1LL << 31)) splits = 1;  // slab offsets are 32-bit
   int nkt = (d->k + BK - 1) / BK;
   a.ktiles_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + a.ktiles_per_split - 1) / a.ktiles_per_split;
@@ -1228,8 +1318,9 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     run.raw = 1;
     run.ws = (const float*)workspace;
     run.nsplit = splits;
-    run.split_stride = (long long)d->m * nt;
-    run.counters = splitk_counters((long long)grid.x * grid.y, splits);
+    run.split_stride = (long long)d->m * ns;
+    // the in-launch combine reduces whole tiles only: the VALU row-sum chunk (outside every tile) needs the reducer
+    run.counters = ns != nt ? nullptr : splitk_counters((long long)grid.x * grid.y, splits);
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
@@ -1246,7 +1337,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     EpiArgs red = e;
     red.raw = 0;
     red.nsplit = splits;
-    red.split_stride = (long long)d->m * nt;
+    red.split_stride = (long long)d->m * ns;
     red.ws = (const float*)workspace;
     err = launch_reduce(red, s);
     if (err != hipSuccess) return (int)err;

@@ -113,3 +113,71 @@ extern "C" int sdmi_affine_step(const float* x, const float* eps, const float* z
   SDMI_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Device Gaussian noise for captured sampling loops: Philox4x32-10 (Salmon et al., SC'11) keyed by a 64-bit seed,
+// counter = (element quad index, 64-bit draw offset read from DEVICE memory), Box-Muller on pairs of 24-bit
+// uniforms in (0, 1]. The reference draws z with the host generator every step (scheduler :72); a replayed step
+// instead reads its draw offset on the device and (advance != 0) bumps it afterwards, so every replay of the same
+// recorded launches gets fresh, reproducible noise with no host round trip.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ void philox_round(uint32_t (&c)[4], const uint32_t (&k)[2]) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t hi0 = __umulhi(M0, c[0]), lo0 = M0 * c[0];
+  const uint32_t hi1 = __umulhi(M1, c[2]), lo1 = M1 * c[2];
+  c[0] = hi1 ^ c[1] ^ k[0];
+  c[1] = lo1;
+  c[2] = hi0 ^ c[3] ^ k[1];
+  c[3] = lo0;
+}
+
+__global__ void randn_kernel(float* out, long long n, unsigned long long seed, const unsigned long long* offset) {
+  const unsigned long long off = *offset;
+  const long long quads = (n + 3) / 4;
+  for (long long q = (long long)blockIdx.x * NT + threadIdx.x; q < quads; q += (long long)gridDim.x * NT) {
+    uint32_t c[4] = {(uint32_t)q, (uint32_t)((unsigned long long)q >> 32), (uint32_t)off, (uint32_t)(off >> 32)};
+    uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      philox_round(c, k);
+      k[0] += 0x9E3779B9u;
+      k[1] += 0xBB67AE85u;
+    }
+    float z[4];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float u1 = ((c[2 * p] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+      const float u2 = (c[2 * p + 1] >> 8) * (1.0f / 16777216.0f);    // [0, 1)
+      const float rad = sqrtf(-2.0f * logf(u1));
+      float s, co;
+      sincosf(6.28318530717958647692f * u2, &s, &co);
+      z[2 * p] = rad * co;
+      z[2 * p + 1] = rad * s;
+    }
+    const long long i0 = q * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (i0 + e < n) out[i0 + e] = z[e];
+  }
+}
+
+__global__ void advance_kernel(unsigned long long* offset) {
+  if (threadIdx.x == 0) *offset = *offset + 1;
+}
+
+}  // namespace
+
+extern "C" int sdmi_randn(float* out, long long n, unsigned long long seed, unsigned long long* offset_dev,
+                          int advance, sdmi_stream_t stream) {
+  if (!out || !offset_dev || n <= 0) return -1;
+  sdmi_rt::launch(randn_kernel, dim3(grid_for((n + 3) / 4)), dim3(NT), 0, (hipStream_t)stream, out, n, seed,
+                  (const unsigned long long*)offset_dev);
+  SDMI_CHECK_LAUNCH();
+  if (advance) {
+    sdmi_rt::launch(advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, offset_dev);
+    SDMI_CHECK_LAUNCH();
+  }
+  return 0;
+}
