@@ -71,6 +71,11 @@ def main():
                 ops[j + 1]["reduce_of"] = log[gi]
             gi += 1
     total = sum(o["us"] for o in ops)
+    if os.environ.get("PLAN_PROFILE_JSON"):
+        import json
+        json.dump([dict(i=o["i"], name=o["name"], grid=o["grid"], us=o["us"], gemm=o.get("gemm"),
+                        reduce=o.get("reduce_of") is not None) for o in ops],
+                  open(os.environ["PLAN_PROFILE_JSON"], "w"))
     print(f"{a.workload}: {n} ops, {nl} launches, {nc} callouts; isolated kernel time {total / 1e3:.2f} ms "
           f"(GEMM calls matched {gi}/{len(log)})")
     fam = {}
