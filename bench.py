@@ -36,6 +36,9 @@ WORKLOADS = {
     # VQVAE encode + decode (no grad) of a batch of 8 CelebHQ-256 images: 2.9497e11 FLOP per image
     "vqvae": dict(metric="VQVAE encode+decode steps/sec (celebhq.yaml autoencoder, 256x256, B=8) on MI355X",
                   flop=8 * 2.9497e11),
+    # VQVAE generator training step (train_vqvae_celebhq.py:405-466 without LPIPS / GAN): fwd + bwd ~ 3x the forward
+    "vqvae-train": dict(metric="VQVAE train steps/sec (celebhq autoencoder, 256x256, B=8, recon + codebook + "
+                               "commitment, Adam) on MI355X", flop=3 * 8 * 2.9497e11),
     # DDPM sampling (tools/sample_ddpm_text_image_cond.py loop, train_num_samples = 1 in the reference config):
     # one step = cond-UNet forward at batch --sample-batch + the reverse step; fwd 1.2988e12 FLOP at B=32
     "sample": dict(metric="DDPM sampling steps/sec (cond-UNet, CelebHQ-256 latents, captured loop) on MI355X",
@@ -240,6 +243,74 @@ def main_vqvae(args, wl, world, rank, device):
         dist.destroy_process_group()
 
 
+def cpu_baseline_vqvae_train(cfg, B=8):
+    """The VQVAE oracle's fp32 generator step (train_grads: forward, losses, autograd backward) on the host cores;
+    bounded sample: one timed step (no warm-up: ~15 s)."""
+    from oracle import sd_oracle as O, vqvae_oracle as VO
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = O.deterministic_state(VO.vqvae_param_shapes(cfg), seed=0)
+    x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1111)) * 2 - 1
+    t0 = time.perf_counter()
+    VO.train_grads(sd, cfg, x)
+    dt = time.perf_counter() - t0
+    return dict(value=1.0 / dt, unit="steps/s", cores=threads, kind="port",
+                sample=f"VQVAE oracle fp32 fwd + losses + bwd (no optimizer), B={B} at 256x256, 1 timed step, "
+                       f"{dt:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
+
+
+def main_vqvae_train(args, wl, world, rank, device):
+    """VQVAE generator training step (sdmi.vqvae_train.VQVAETrainer) on a synthetic CelebHQ-256 batch of 8 images per
+    GPU, recorded once and replayed (sdmi.plan); N > 1: data parallel with one bucketed all-reduce per step."""
+    from models.vqvae import VQVAE
+    from sdmi.plan import StepPlan
+    from sdmi.vqvae_train import VQVAETrainer
+    cfg = vqvae_config()
+    torch.manual_seed(1111)
+    init = VQVAE(3, cfg).state_dict()
+    B = 8
+    x = (torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1111 + rank)) * 2 - 1).to(device)
+    tr = VQVAETrainer(cfg, {k: v.to(device) for k, v in init.items()}, device,
+                      group=dist.group.WORLD if world > 1 else None)
+    for _ in range(2):
+        tr.step(x)
+    plan = StepPlan(lambda: tr.step(x), device) if args.issue == "plan" else None
+    step = plan.replay if plan is not None else (lambda: tr.step(x))
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = e.item()
+    sps = args.steps / elapsed
+    losses = tr.losses()
+    result = {"metric": wl["metric"], "value": sps * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+              "warmup": args.warmup, "ms_per_step": 1000.0 / sps, "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": "bf16", "data": "synthetic 256x256 images, random-init weights",
+              "config": {"workload": "VQVAE celebhq.yaml generator step: fwd, recon MSE + codebook + commitment, bwd, "
+                                     "Adam(2e-5, betas (0.5, 0.999)); LPIPS / GAN out of scope",
+                         "model": "VQVAE 22.0M", "per_gpu_batch": B, "image": [3, 256, 256], "latent": [4, 32, 32],
+                         "parallelism": f"dp{world}", "issue": args.issue},
+              "images_per_s": sps * B * world, "model_flops_utilization": wl["flop"] * sps / PEAK_BF16,
+              "last_losses": losses}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_vqvae_train(cfg)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main_sample(args, wl, world, rank, device):
     """Reverse-diffusion sampling throughput: the cond-UNet sampler loop recorded once and replayed (sdmi.sampling),
     against the same loop issued step by step (eager). Replicas for N > 1 (sampling does not shard)."""
@@ -297,7 +368,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="cond-unet", choices=sorted(WORKLOADS),
                     help="cond-unet (the headline metric, default), uncond-unet (celebhq.yaml), dit (DiT-12L training "
-                         "step), vqvae (encode + decode) or sample (captured DDPM sampling loop)")
+                         "step), vqvae (encode + decode), vqvae-train (VQVAE generator step) or sample (captured DDPM sampling loop)")
     ap.add_argument("--profile-gemm", action="store_true", default=True)
     ap.add_argument("--issue", default="plan", choices=("plan", "eager", "graph"),
                     help="plan (default): the step recorded once and its native calls replayed (sdmi.plan); eager: "
@@ -333,6 +404,8 @@ def main():
         return main_vqvae(args, wl, world, rank, device)
     if args.workload == "sample":
         return main_sample(args, wl, world, rank, device)
+    if args.workload == "vqvae-train":
+        return main_vqvae_train(args, wl, world, rank, device)
     cfg = dit_config() if is_dit else (uncond_config() if is_uncond else cond_config())
     torch.manual_seed(1111)  # identical initial weights on every rank (DDP broadcasts rank 0's)
     group = dist.group.WORLD if world > 1 else None

@@ -233,7 +233,18 @@ int sdmi_mse_patch(const float* pred, int ld, const float* target, int B, int C,
  *                     commitment loss mean((q - x)^2). ws: sdmi_vq_workspace(B*HW) bytes.
  *  sdmi_pointwise_in: post_quant_conv (1x1, fp32) of an NCHW fp32 latent into NHWC bf16 [P][ld] (tail zeroed).
  * ------------------------------------------------------------------------------------------- */
+/*  sdmi_vq_bwd      : training backward of the latent interface (train_vqvae_celebhq.py:405-430, recon + codebook
+ *                     + commitment terms; LPIPS / GAN out of scope): from dzin (gradient of post_quant_conv's output,
+ *                     NHWC bf16) -> post_quant_conv dW/db, the straight-through gradient of the pre-quantisation
+ *                     latent plus commitment_beta * 2 (x - q) / n, pre_quant_conv dW/db and dz_enc (NHWC bf16
+ *                     gradient of encoder_conv_out's output), and the codebook gradient codebook_weight * 2 (q - x) / n
+ *                     scattered to the selected rows (deterministic, no atomics). ws: sdmi_vq_bwd_workspace() bytes. */
 size_t sdmi_vq_workspace(long long pixels);
+size_t sdmi_vq_bwd_workspace(void);
+int sdmi_vq_bwd(const void* dzin, int ld_dzin, const float* zq, const float* w_post, const float* xq, const long long* idx,
+                const float* codebook, int K, const float* z_enc, int ldz, const float* w_pre, int B, int HW, int C,
+                float commitment_beta, float codebook_weight, void* dz_enc, int ld_out, float* ws, float* dw_post,
+                float* db_post, float* dw_pre, float* db_pre, float* demb, sdmi_stream_t stream);
 int sdmi_vq_quantize(const float* z, int ldz, const float* w, const float* b, const float* codebook, int K, int B,
                      int HW, int C, float* zq, long long* idx, float* xq, float* ws, float* loss, sdmi_stream_t stream);
 int sdmi_pointwise_in(const float* z, int B, int C, int HW, const float* w, const float* b, int cout, void* out,
@@ -295,7 +306,8 @@ int sdmi_pack_transpose(const sdmi_tpack_desc* descs_dev, const void* bmap_dev, 
  * Optimizer step over flat fp32 buffers (train_ddpm_cond_celebhq_multi_gpu.py:362-378):
  * GradScaler.unscale_ + clip_grad_norm_(max_norm) + non-finite skip + scaler.update (state on device:
  * float[8] = {norm, coef, scale, growth, step, skip, loss, -}), then Adam (torch defaults) + EMA.
- * grad_div = data-parallel world size (gradients arrive summed).
+ * grad_div = data-parallel world size (gradients arrive summed). growth_interval <= 0: no loss scaler (the
+ * plain fp32 VQVAE trainer, train_vqvae_celebhq.py:466): the scale in state[2] is left as is (keep it 1).
  * ------------------------------------------------------------------------------------------- */
 size_t sdmi_optim_workspace(void);
 int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws, int growth_interval,

@@ -52,7 +52,9 @@ __global__ void norm_finalize_kernel(const float* partial, int n, float max_norm
     float coef = max_norm / (norm + 1e-6f);
     coef = coef < 1.f ? coef : 1.f;
     state[1] = coef * inv;
-    if (!loss_bad) {  // reference: non-finite loss skips before scaler.update() (:348-352)
+    if (growth_interval <= 0) {  // no loss scaler (plain fp32 trainer): the scale stays 1, finite steps count
+      if (!bad) state[4] = state[4] + 1.f;
+    } else if (!loss_bad) {  // reference: non-finite loss skips before scaler.update() (:348-352)
       if (bad) {
         state[2] = scale * 0.5f;
         state[3] = 0.f;

@@ -10,6 +10,12 @@
 //                (codebook == commitment) loss mean((q - x)^2).
 //  pointwise_in: post_quant_conv (1x1, fp32) of an NCHW fp32 latent straight into the NHWC bf16 operand of
 //                decoder_conv_in (vqvae.py:141-144), zero-padding the channel tail.
+//  vq_bwd      : the training backward of the latent interface (train_vqvae_celebhq.py:405-430 without the
+//                LPIPS / GAN terms): post_quant_conv backward, the straight-through estimator (dL/dx += dL/dz_q),
+//                the commitment term beta * mean((sg[q] - x)^2), pre_quant_conv backward into the bf16 NHWC
+//                gradient of encoder_conv_out; the 1x1-conv weight / bias gradients as per-block partials summed in
+//                a fixed order (deterministic). vq_codebook_grad: the codebook term w * mean((q - sg[x])^2) into the
+//                embedding rows (index_select backward), one thread per code scanning the pixels in order.
 #include "common.h"
 #include "../../include/sdmi.h"
 #include <algorithm>
@@ -148,6 +154,145 @@ __global__ void pointwise_in_kernel(const float* z, int B, int C, int HW, const 
   }
 }
 
+constexpr int VQB_NT = 256;
+constexpr int VQB_PART = 2 * MAXC * MAXC + 2 * MAXC;  // dW_post, dW_pre, db_post, db_pre partials per block
+
+struct VqBwdArgs {
+  const bf16_t* dzin; int ld_dzin;      // gradient of decoder_conv_in's input, NHWC bf16 [P][ld] (post_quant output)
+  const float* zq;                      // quantised latent (NCHW fp32): post_quant_conv input
+  const float* w_post;                  // post_quant_conv weight (C, C)
+  const float* xq;                      // pre-quantisation latent (NCHW fp32)
+  const long long* idx;                 // code per pixel
+  const float* codebook;                // (K, C)
+  const float* z_enc; int ldz;          // encoder_conv_out output, NHWC fp32 [P][ldz]: pre_quant_conv input
+  const float* w_pre;                   // pre_quant_conv weight (C, C)
+  int B, HW, C;
+  float g_commit;                       // commitment_beta * 2 / (P * C)
+  bf16_t* dz_enc; int ld_out;           // gradient of encoder_conv_out's output, NHWC bf16 [P][ld_out]
+  float* partial;                       // [blocks][VQB_PART]
+};
+
+__global__ __launch_bounds__(VQB_NT) void vq_bwd_kernel(const VqBwdArgs a) {
+  __shared__ float red[VQB_NT / 64][VQB_PART];
+  const int C = a.C;
+  const long long P = (long long)a.B * a.HW;
+  float acc[VQB_PART];
+#pragma unroll
+  for (int i = 0; i < VQB_PART; ++i) acc[i] = 0.f;
+  for (long long pix = (long long)blockIdx.x * VQB_NT + threadIdx.x; pix < P; pix += (long long)gridDim.x * VQB_NT) {
+    const long long bb = pix / a.HW, p = pix - bb * a.HW;
+    float dzin[MAXC], zq[MAXC], x[MAXC], q[MAXC], ze[MAXC], dzq[MAXC], dx[MAXC];
+    const long long k = a.idx[pix];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const bool on = c < C;
+      dzin[c] = on ? bf2f(a.dzin[pix * a.ld_dzin + c]) : 0.f;
+      zq[c] = on ? a.zq[(bb * C + c) * a.HW + p] : 0.f;
+      x[c] = on ? a.xq[(bb * C + c) * a.HW + p] : 0.f;
+      q[c] = on ? a.codebook[k * C + c] : 0.f;
+      ze[c] = on ? a.z_enc[pix * a.ldz + c] : 0.f;
+    }
+    // post_quant_conv backward: dzq = W_post^T dzin (the straight-through gradient of x), dW_post, db_post
+#pragma unroll
+    for (int ci = 0; ci < MAXC; ++ci) {
+      float s = 0.f;
+#pragma unroll
+      for (int co = 0; co < MAXC; ++co)
+        if (co < C && ci < C) s = fmaf(a.w_post[co * C + ci], dzin[co], s);
+      dzq[ci] = s;
+    }
+#pragma unroll
+    for (int co = 0; co < MAXC; ++co) {
+#pragma unroll
+      for (int ci = 0; ci < MAXC; ++ci) acc[co * MAXC + ci] = fmaf(dzin[co], zq[ci], acc[co * MAXC + ci]);
+      acc[2 * MAXC * MAXC + co] += dzin[co];
+    }
+    // STE + commitment: dL/dx = dzq + beta * 2 (x - q) / n
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) dx[c] = fmaf(a.g_commit, x[c] - q[c], dzq[c]);
+    // pre_quant_conv backward
+#pragma unroll
+    for (int co = 0; co < MAXC; ++co) {
+#pragma unroll
+      for (int ci = 0; ci < MAXC; ++ci)
+        acc[MAXC * MAXC + co * MAXC + ci] = fmaf(dx[co], ze[ci], acc[MAXC * MAXC + co * MAXC + ci]);
+      acc[2 * MAXC * MAXC + MAXC + co] += dx[co];
+    }
+    for (int ci = 0; ci < a.ld_out; ++ci) {
+      float s = 0.f;
+      if (ci < C)
+        for (int co = 0; co < C; ++co) s = fmaf(a.w_pre[co * C + ci], dx[co], s);
+      a.dz_enc[pix * a.ld_out + ci] = f2bf(s);
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < VQB_PART; ++i) {
+    const float v = wave_sum(acc[i]);
+    if (lane == 0) red[wave][i] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < VQB_PART; i += VQB_NT) {
+    float v = 0.f;
+    for (int w = 0; w < VQB_NT / 64; ++w) v += red[w][i];
+    a.partial[(long long)blockIdx.x * VQB_PART + i] = v;
+  }
+}
+
+// sum the per-block partials in block order and scatter them to the four gradient tensors (C x C, C x C, C, C)
+__global__ void vq_bwd_finish_kernel(const float* partial, int blocks, int C, float* dw_post, float* db_post,
+                                     float* dw_pre, float* db_pre) {
+  for (int i = threadIdx.x; i < VQB_PART; i += blockDim.x) {
+    float v = 0.f;
+    for (int b = 0; b < blocks; ++b) v += partial[(long long)b * VQB_PART + i];
+    if (i < MAXC * MAXC) {
+      const int co = i / MAXC, ci = i % MAXC;
+      if (co < C && ci < C && dw_post) dw_post[co * C + ci] = v;
+    } else if (i < 2 * MAXC * MAXC) {
+      const int j = i - MAXC * MAXC, co = j / MAXC, ci = j % MAXC;
+      if (co < C && ci < C && dw_pre) dw_pre[co * C + ci] = v;
+    } else if (i < 2 * MAXC * MAXC + MAXC) {
+      const int co = i - 2 * MAXC * MAXC;
+      if (co < C && db_post) db_post[co] = v;
+    } else {
+      const int co = i - 2 * MAXC * MAXC - MAXC;
+      if (co < C && db_pre) db_pre[co] = v;
+    }
+  }
+}
+
+// demb[k] = g_codebook * sum over pixels p with idx[p] == k of (q_k - x_p), pixels in order: each workgroup streams
+// the index list once through LDS and every thread (one code) scans it
+__global__ __launch_bounds__(256) void vq_codebook_grad_kernel(const long long* idx, const float* xq, const float* codebook,
+                                                               int K, int B, int HW, int C, float g_codebook,
+                                                               float* demb) {
+  __shared__ int sidx[1024];
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  const long long P = (long long)B * HW;
+  float acc[MAXC];
+  int cnt = 0;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) acc[c] = 0.f;
+  for (long long p0 = 0; p0 < P; p0 += 1024) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < 1024; j += 256) sidx[j] = p0 + j < P ? (int)idx[p0 + j] : -1;
+    __syncthreads();
+    const int n = (int)min<long long>(1024, P - p0);
+    for (int j = 0; j < n; ++j) {
+      if (sidx[j] != k) continue;
+      const long long pix = p0 + j, bb = pix / HW, p = pix - bb * HW;
+      ++cnt;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < C) acc[c] -= xq[(bb * C + c) * HW + p];
+    }
+  }
+  if (k >= K) return;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+    if (c < C) demb[(long long)k * C + c] = g_codebook * fmaf((float)cnt, codebook[(long long)k * C + c], acc[c]);
+}
+
 }  // namespace
 
 extern "C" size_t sdmi_vq_workspace(long long pixels) { return (size_t)((pixels + 63) / 64) * sizeof(float); }
@@ -177,6 +322,35 @@ extern "C" int sdmi_pointwise_in(const float* z, int B, int C, int HW, const flo
   const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
   sdmi_rt::launch(pointwise_in_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, z, B, C, HW, w, b, cout,
                      (bf16_t*)out, ld);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" size_t sdmi_vq_bwd_workspace(void) { return (size_t)512 * VQB_PART * sizeof(float); }
+
+extern "C" int sdmi_vq_bwd(const void* dzin, int ld_dzin, const float* zq, const float* w_post, const float* xq,
+                           const long long* idx, const float* codebook, int K, const float* z_enc, int ldz,
+                           const float* w_pre, int B, int HW, int C, float commitment_beta, float codebook_weight,
+                           void* dz_enc, int ld_out, float* ws, float* dw_post, float* db_post, float* dw_pre,
+                           float* db_pre, float* demb, sdmi_stream_t stream) {
+  if (!dzin || !zq || !w_post || !xq || !idx || !codebook || !z_enc || !w_pre || !dz_enc || !ws || !demb ||
+      C <= 0 || C > MAXC || ld_out < C || ldz < C || ld_dzin < C || B <= 0 || HW <= 0 || K <= 0)
+    return -1;
+  const long long P = (long long)B * HW;
+  const float n = (float)(P * C);
+  VqBwdArgs a;
+  a.dzin = (const bf16_t*)dzin; a.ld_dzin = ld_dzin; a.zq = zq; a.w_post = w_post; a.xq = xq; a.idx = idx;
+  a.codebook = codebook; a.z_enc = z_enc; a.ldz = ldz; a.w_pre = w_pre; a.B = B; a.HW = HW; a.C = C;
+  a.g_commit = commitment_beta * 2.0f / n;
+  a.dz_enc = (bf16_t*)dz_enc; a.ld_out = ld_out; a.partial = ws;
+  const int blocks = (int)std::min<long long>(512, (P + VQB_NT - 1) / VQB_NT);
+  sdmi_rt::launch(vq_bwd_kernel, dim3(blocks), dim3(VQB_NT), 0, (hipStream_t)stream, a);
+  SDMI_CHECK_LAUNCH();
+  sdmi_rt::launch(vq_bwd_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (const float*)ws, blocks, C,
+                  dw_post, db_post, dw_pre, db_pre);
+  SDMI_CHECK_LAUNCH();
+  sdmi_rt::launch(vq_codebook_grad_kernel, dim3((K + 255) / 256), dim3(256), 0, (hipStream_t)stream, idx, xq,
+                  codebook, K, B, HW, C, codebook_weight * 2.0f / n, demb);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

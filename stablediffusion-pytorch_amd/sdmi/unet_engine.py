@@ -326,34 +326,15 @@ class UNetEngine:
     def _build_pack(self):
         P, L = self.P, self.L
         pk = PackPlan(self.device)
-
-        def conv(key, fwd=True, dgrad=True, ipad=None, opad=None):
-            w = P[key + ".weight"]
-            O, I, KH, KW = w.shape
-            Ip = ipad or I
-            if fwd:
-                pk.add(key + "#f", w, O, I, Ip, KH, KW, I * KH * KW, KH * KW, KW, 1, rows=opad)
-            if dgrad and fwd:  # stride-1 dgrad [I][KH][KW][O] with flipped taps = the forward layout transposed
-                pk.add_transpose(key + "#d", key + "#f", O, I, KH * KW, [KH * KW - 1 - t for t in range(KH * KW)], Ip,
-                                 rows=ipad, opad=opad)
-            elif dgrad:
-                pk.add(key + "#d", w, I, O, opad or O, KH, KW, KH * KW, I * KH * KW, KW, 1, KH - 1, -1, KW - 1, -1,
-                       rows=ipad)
-
-        def lin(key):
-            w = P[key + ".weight"] if key + ".weight" in P else P[key]
-            N, Kd = w.shape
-            pk.add(key + "#f", w, N, Kd, Kd, 1, 1, Kd, 1, 0, 0)
-            if self.dgrad_t:  # [Kd][N] for the data gradient (B_NK GEMM)
-                pk.add_transpose(key + "#t", key + "#f", N, Kd, 1, [0], 8)
+        conv, lin = self._pk_conv, self._pk_lin
 
         cin_img = self.im_channels + (L["im_out"] if L["image"] else 0)
         self.cin_pad = (cin_img + 7) // 8 * 8
         first = "conv_in_concat" if L["image"] else "conv_in"
         self.first = first
-        conv(first, ipad=self.cin_pad)
-        lin("t_proj.0")
-        lin("t_proj.2")
+        conv(pk, first, ipad=self.cin_pad)
+        lin(pk, "t_proj.0")
+        lin(pk, "t_proj.2")
         if L["klass"]:  # [classes (zero rows up to kpad)][T]: the B operand (k = class) of the class-embedding GEMM
             pk.add("class_emb#kn", P["class_emb.weight"], L["num_classes"], L["T"], L["T"], 1, 1, L["T"], 1, 0, 0,
                    rows=self.kpad)
@@ -363,70 +344,101 @@ class UNetEngine:
             w = P[f"{p}.t_emb_layers.{l}.1.weight"]
             pk.add(None, w, cout, L["T"], L["T"], 1, 1, L["T"], 1, 0, 0, into="temb_all", row0=self.temb_off[(p, l)])
         for (p, l, cin, cout) in self.resnets:
-            conv(f"{p}.resnet_conv_first.{l}.2")
-            # second conv and the 1x1 residual conv as one K-concatenated weight [cout][9*cout + cin]
-            w2 = P[f"{p}.resnet_conv_second.{l}.2.weight"]
-            wr = P[f"{p}.residual_input_conv.{l}.weight"]
-            cat = f"{p}.res{l}#cat"
-            pk.reserve(cat, cout, 9 * cout + cin)
-            pk.add(None, w2, cout, cout, cout, 3, 3, cout * 9, 9, 3, 1, into=cat)
-            pk.add(None, wr, cout, cin, cin, 1, 1, cin, 1, 0, 0, into=cat, col0=9 * cout)
-            # its dgrad layout: the conv part of the concatenated forward weight, transposed per (flipped) tap
-            pk.add_transpose(f"{p}.resnet_conv_second.{l}.2#d", cat, cout, cout, 9, [8 - t for t in range(9)], cout)
-            if self.dgrad_t:  # the 1x1 residual conv's weight transposed [cin][cout] for its data gradient
-                pk.add_transpose(f"{p}.res{l}#t", cat, cout, cin, 1, [0], 8, src_col0=9 * cout)
+            self._pk_resnet(pk, p, l, cin, cout)
         nd = len(L["down"]) - 1
         for i in range(nd):
             p = f"downs.{i}"
             for l in range(L["n_down"]):
                 if L["attn"][i]:
-                    lin(f"{p}.attentions.{l}.in_proj_weight")
-                    lin(f"{p}.attentions.{l}.out_proj")
+                    lin(pk, f"{p}.attentions.{l}.in_proj_weight")
+                    lin(pk, f"{p}.attentions.{l}.out_proj")
                 if L["text"]:
-                    lin(f"{p}.cross_attentions.{l}.in_proj_weight")
-                    lin(f"{p}.cross_attentions.{l}.out_proj")
-                    lin(f"{p}.context_proj.{l}")
+                    lin(pk, f"{p}.cross_attentions.{l}.in_proj_weight")
+                    lin(pk, f"{p}.cross_attentions.{l}.out_proj")
+                    lin(pk, f"{p}.context_proj.{l}")
             if L["down_sample"][i]:
-                key = f"{p}.down_sample_conv"
-                w = P[key + ".weight"]
-                C = w.shape[0]
-                conv(key, dgrad=False)
-                for ph in range(2):
-                    for pw in range(2):  # dgrad phases: [ci][a][b][co] = W[co][ci][3-ph-2a][3-pw-2b] = #f[co][tap][ci]
-                        pk.add_transpose(f"{key}#d{ph}{pw}", key + "#f", C, C, 4,
-                                         [(3 - ph - 2 * a) * 4 + (3 - pw - 2 * b) for a in range(2) for b in range(2)], C)
+                self._pk_down(pk, f"{p}.down_sample_conv")
         for i in range(len(L["mid"]) - 1):
             p = f"mids.{i}"
             for l in range(L["n_mid"]):
-                lin(f"{p}.attentions.{l}.in_proj_weight")
-                lin(f"{p}.attentions.{l}.out_proj")
+                lin(pk, f"{p}.attentions.{l}.in_proj_weight")
+                lin(pk, f"{p}.attentions.{l}.out_proj")
                 if L["text"]:
-                    lin(f"{p}.cross_attentions.{l}.in_proj_weight")
-                    lin(f"{p}.cross_attentions.{l}.out_proj")
-                    lin(f"{p}.context_proj.{l}")
+                    lin(pk, f"{p}.cross_attentions.{l}.in_proj_weight")
+                    lin(pk, f"{p}.cross_attentions.{l}.out_proj")
+                    lin(pk, f"{p}.context_proj.{l}")
         for j, i in enumerate(reversed(range(nd))):
             p = f"ups.{j}"
             for l in range(L["n_up"]):
-                lin(f"{p}.attentions.{l}.in_proj_weight")
-                lin(f"{p}.attentions.{l}.out_proj")
+                lin(pk, f"{p}.attentions.{l}.in_proj_weight")
+                lin(pk, f"{p}.attentions.{l}.out_proj")
                 if L["text"]:
-                    lin(f"{p}.cross_attentions.{l}.in_proj_weight")
-                    lin(f"{p}.cross_attentions.{l}.out_proj")
-                    lin(f"{p}.context_proj.{l}")
+                    lin(pk, f"{p}.cross_attentions.{l}.in_proj_weight")
+                    lin(pk, f"{p}.cross_attentions.{l}.out_proj")
+                    lin(pk, f"{p}.context_proj.{l}")
             if L["down_sample"][i]:
-                key = f"{p}.up_sample_conv"
-                w = P[key + ".weight"]  # (Cx, Cy, 4, 4)
-                Cx, Cy = w.shape[0], w.shape[1]
-                # dgrad = stride-2 conv over dY: [ci][kh][kw][co] = W[ci][co][kh][kw]
-                pk.add(f"{key}#d", w, Cx, Cy, Cy, 4, 4, Cy * 16, 16, 4, 1)
-                for ph in range(2):
-                    for pw in range(2):  # fwd phases: [co][a][b][ci] = W[ci][co][3-ph-2a][3-pw-2b] = #d[ci][tap][co]
-                        pk.add_transpose(f"{key}#f{ph}{pw}", f"{key}#d", Cx, Cy, 4,
-                                         [(3 - ph - 2 * a) * 4 + (3 - pw - 2 * b) for a in range(2) for b in range(2)],
-                                         Cy)
-        conv("conv_out", ipad=None, opad=8)
+                self._pk_up(pk, f"{p}.up_sample_conv")
+        conv(pk, "conv_out", opad=8)
         pk.finalize()
         self.pack = pk
+
+    # ---- packed layouts (shared with the VQVAE training engine) --------------------------------------------
+    def _pk_conv(self, pk, key, fwd=True, dgrad=True, ipad=None, opad=None):
+        """key#f [O][KH][KW][Ipad] (forward) and key#d (stride-1 data gradient: flipped taps, transposed)."""
+        w = self.P[key + ".weight"]
+        O, I, KH, KW = w.shape
+        Ip = ipad or I
+        if fwd:
+            pk.add(key + "#f", w, O, I, Ip, KH, KW, I * KH * KW, KH * KW, KW, 1, rows=opad)
+        if dgrad and fwd:  # stride-1 dgrad [I][KH][KW][O] with flipped taps = the forward layout transposed
+            pk.add_transpose(key + "#d", key + "#f", O, I, KH * KW, [KH * KW - 1 - t for t in range(KH * KW)], Ip,
+                             rows=ipad, opad=opad)
+        elif dgrad:
+            pk.add(key + "#d", w, I, O, opad or O, KH, KW, KH * KW, I * KH * KW, KW, 1, KH - 1, -1, KW - 1, -1,
+                   rows=ipad)
+
+    def _pk_lin(self, pk, key):
+        w = self.P[key + ".weight"] if key + ".weight" in self.P else self.P[key]
+        N, Kd = w.shape
+        pk.add(key + "#f", w, N, Kd, Kd, 1, 1, Kd, 1, 0, 0)
+        if self.dgrad_t:  # [Kd][N] for the data gradient (B_NK GEMM)
+            pk.add_transpose(key + "#t", key + "#f", N, Kd, 1, [0], 8)
+
+    def _pk_resnet(self, pk, p, l, cin, cout):
+        P = self.P
+        self._pk_conv(pk, f"{p}.resnet_conv_first.{l}.2")
+        # second conv and the 1x1 residual conv as one K-concatenated weight [cout][9*cout + cin]
+        w2 = P[f"{p}.resnet_conv_second.{l}.2.weight"]
+        wr = P[f"{p}.residual_input_conv.{l}.weight"]
+        cat = f"{p}.res{l}#cat"
+        pk.reserve(cat, cout, 9 * cout + cin)
+        pk.add(None, w2, cout, cout, cout, 3, 3, cout * 9, 9, 3, 1, into=cat)
+        pk.add(None, wr, cout, cin, cin, 1, 1, cin, 1, 0, 0, into=cat, col0=9 * cout)
+        # its dgrad layout: the conv part of the concatenated forward weight, transposed per (flipped) tap
+        pk.add_transpose(f"{p}.resnet_conv_second.{l}.2#d", cat, cout, cout, 9, [8 - t for t in range(9)], cout)
+        if self.dgrad_t:  # the 1x1 residual conv's weight transposed [cin][cout] for its data gradient
+            pk.add_transpose(f"{p}.res{l}#t", cat, cout, cin, 1, [0], 8, src_col0=9 * cout)
+
+    def _pk_down(self, pk, key):
+        """Stride-2 4x4 conv: key#f, plus its data gradient as four sub-pixel phases key#d{ph}{pw}."""
+        C = self.P[key + ".weight"].shape[0]
+        self._pk_conv(pk, key, dgrad=False)
+        for ph in range(2):
+            for pw in range(2):  # dgrad phases: [ci][a][b][co] = W[co][ci][3-ph-2a][3-pw-2b] = #f[co][tap][ci]
+                pk.add_transpose(f"{key}#d{ph}{pw}", key + "#f", C, C, 4,
+                                 [(3 - ph - 2 * a) * 4 + (3 - pw - 2 * b) for a in range(2) for b in range(2)], C)
+
+    def _pk_up(self, pk, key):
+        """ConvTranspose2d(4, 2, 1): key#d (its data gradient = a stride-2 conv over dY) and the forward as four
+        sub-pixel phases key#f{ph}{pw}."""
+        w = self.P[key + ".weight"]  # (Cx, Cy, 4, 4)
+        Cx, Cy = w.shape[0], w.shape[1]
+        # dgrad = stride-2 conv over dY: [ci][kh][kw][co] = W[ci][co][kh][kw]
+        pk.add(f"{key}#d", w, Cx, Cy, Cy, 4, 4, Cy * 16, 16, 4, 1)
+        for ph in range(2):
+            for pw in range(2):  # fwd phases: [co][a][b][ci] = W[ci][co][3-ph-2a][3-pw-2b] = #d[ci][tap][co]
+                pk.add_transpose(f"{key}#f{ph}{pw}", f"{key}#d", Cx, Cy, 4,
+                                 [(3 - ph - 2 * a) * 4 + (3 - pw - 2 * b) for a in range(2) for b in range(2)], Cy)
 
     def W(self, name):
         if self._pending:
@@ -667,9 +679,9 @@ class UNetEngine:
         h0 = self._new(B * Pn, cin)
         t1 = K.gn_fwd(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"], True, h0)
         h1 = self._new(B * Pn, cout)
-        off = self.temb_off[(p, l)]
+        off = self.temb_off.get((p, l))  # None: no time embedding (the VQVAE's blocks, t_emb_dim=None)
         K.conv_fwd(h0, B, h, w, cin, cin, self.W(a + ".2#f"), cout, 3, 3, 1, 1, h1, cout, bias=P[a + ".2.bias"],
-                   rowbias=st["temb_all"][:, off:], rb_ld=self.temb_total)
+                   rowbias=st["temb_all"][:, off:] if off is not None else None, rb_ld=self.temb_total)
         h2 = self._new(B * Pn, cout)
         t2 = K.gn_fwd(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"], True, h2)
         rc = f"{p}.residual_input_conv.{l}"
@@ -703,13 +715,14 @@ class UNetEngine:
             K.linear_dgrad(dy, self.W(f"{p}.res{l}#cat")[:, 9 * cout:], dx, resid=None if fresh else dx)
         K.gn_bwd(c["h1"], dh2, dh2, c["t2"], P[b + ".0.weight"], B, Pn, cout, G, True,
                  self.g(b + ".0.weight"), self.g(b + ".0.bias"))
-        off = self.temb_off[(p, l)]
+        off = self.temb_off.get((p, l))
         with self._wg(dh2):
             # conv1 bias, t_emb_layers bias and the per-sample time-embedding gradient (blocks.py:117-118) are
             # reductions of dh2 computed by the weight-gradient launch itself
             K.conv_wgrad(dh2, cout, c["h0"], B, h, w, cin, cin, cout, 3, 3, 1, 1, self.g(a + ".2.weight"), h, w,
-                         bias_grad=self.g(a + ".2.bias"), bias_grad2=self.g(f"{p}.t_emb_layers.{l}.1.bias"),
-                         group_sums=self.dtemb_all[:, off:off + cout])
+                         bias_grad=self.g(a + ".2.bias"),
+                         bias_grad2=self.g(f"{p}.t_emb_layers.{l}.1.bias") if off is not None else None,
+                         group_sums=self.dtemb_all[:, off:off + cout] if off is not None else None)
         dh0 = self._new(B * Pn, cin)
         K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin)
         K.gn_bwd(c["x"], dh0, dx, c["t1"], P[a + ".0.weight"], B, Pn, cin, G, True,

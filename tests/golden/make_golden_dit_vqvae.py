@@ -2,7 +2,7 @@
 implementation (read-only at /root/reference) in THIS container. Only input/output tensors are
 committed (safetensors); weights regenerate from oracle.sd_oracle.deterministic_state.
 
-Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae] [vqvae256] [sampler] [class]
+Run:  PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_dit_vqvae.py [dit] [vqvae] [vqvae256] [vqvae_train] [sampler] [class]
 
 The reference DIT zero-initialises adaptive_norm_layer and proj_out (models/transformer.py:147-151,
 transformer_layer.py:70-71), so a freshly built reference model outputs exactly 0; the fixtures load
@@ -185,6 +185,56 @@ def gen_vqvae256():
     save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, "vqvae_celebhq256.safetensors"))
 
 
+GRAD_KEYS_VQVAE = ("encoder_conv_in.weight", "encoder_conv_in.bias", "encoder_layers.0.resnet_conv_first.0.0.weight",
+                   "encoder_layers.0.down_sample_conv.weight", "encoder_layers.1.attentions.0.in_proj_weight",
+                   "encoder_layers.1.attention_norms.0.weight", "encoder_mids.0.resnet_conv_second.1.2.bias",
+                   "encoder_mids.0.attentions.0.out_proj.bias", "encoder_norm_out.weight", "encoder_conv_out.weight",
+                   "encoder_conv_out.bias", "pre_quant_conv.weight", "pre_quant_conv.bias", "embedding.weight",
+                   "post_quant_conv.weight", "post_quant_conv.bias", "decoder_conv_in.weight", "decoder_conv_in.bias",
+                   "decoder_mids.0.resnet_conv_first.0.2.weight", "decoder_layers.0.up_sample_conv.weight",
+                   "decoder_layers.0.up_sample_conv.bias", "decoder_layers.0.attentions.0.out_proj.weight",
+                   "decoder_layers.1.residual_input_conv.0.weight", "decoder_norm_out.weight",
+                   "decoder_conv_out.weight", "decoder_conv_out.bias")
+
+
+def gen_vqvae_train():
+    """Generator step of train_vqvae_celebhq.py:414-466 on the small config (no LPIPS / GAN): loss terms, every
+    parameter's gradient norm, selected gradients, and the parameters after two Adam(2e-5, (0.5, 0.999)) steps."""
+    from tests.golden.configs import SMALL_VQVAE
+    model, sd = make_vqvae(SMALL_VQVAE, 9)
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=2e-5, betas=(0.5, 0.999))
+    f = {}
+    for step in range(2):
+        g = torch.Generator().manual_seed(60 + step)
+        im = torch.rand(2, 3, 64, 64, generator=g) * 2 - 1
+        pre = {}
+        h = model.pre_quant_conv.register_forward_hook(lambda m, i, o: pre.__setitem__("z", o.detach().clone()))
+        opt.zero_grad()
+        out, _, ql = model(im)
+        h.remove()
+        recon = torch.nn.functional.mse_loss(out, im)
+        cb, cm = 1.0 * ql["codebook_loss"], 0.2 * ql["commitment_loss"]
+        total = recon + cb + cm
+        total.backward()
+        with torch.no_grad():
+            _, _, idx = model.quantize(pre["z"])
+        f.update({f"s{step}.im": im, f"s{step}.recon": recon.detach().reshape(1), f"s{step}.codebook": cb.detach().reshape(1),
+                  f"s{step}.commitment": cm.detach().reshape(1), f"s{step}.indices": idx, f"s{step}.pre_quant": pre["z"]})
+        if step == 0:
+            f["s0.out"] = out.detach()
+            f["s0.grad_norms"] = torch.stack([p.grad.norm() if p.grad is not None else torch.zeros(())
+                                              for _, p in model.named_parameters()])
+            for k, p in model.named_parameters():
+                if k in GRAD_KEYS_VQVAE:
+                    f["grad." + k] = p.grad.detach().reshape(-1)[:8192].clone()
+        opt.step()
+    for k, p in model.named_parameters():
+        if k in GRAD_KEYS_VQVAE:
+            f["param." + k] = p.detach().reshape(-1)[:8192].clone()
+    save_file({k: v.contiguous() for k, v in f.items()}, os.path.join(HERE, "vqvae_train.safetensors"))
+
+
 def gen_sampler():
     """DDIMSampler / DDPMSampler steps (scheduler/linear_noise_scheduler.py:93-232) with a fixed-output model
     and fixed noise (torch.randn_like patched), so the step arithmetic alone is pinned."""
@@ -254,6 +304,8 @@ def main():
         gen_vqvae()
     if "vqvae256" in what:
         gen_vqvae256()
+    if "vqvae_train" in what:
+        gen_vqvae_train()
     if "sampler" in what:
         gen_sampler()
     if "class" in what:

@@ -47,3 +47,34 @@ def test_encode_decode(name, cfg, seed):
         out = VO.decode(sd, cfg, zq)
         assert rel(out, f["out"]) <= 1e-5
     assert rel(losses["codebook_loss"].reshape(1), f["codebook_loss"]) <= 1e-4
+
+
+def test_train_step_grads_and_adam():
+    """The training restatement (quantize_train / train_grads / adam_steps) against the reference's own generator
+    step (train_vqvae_celebhq.py:414-466 without LPIPS / GAN): the three loss terms, the indices, every parameter's
+    gradient norm, selected full gradients, and the parameters after two Adam(2e-5, (0.5, 0.999)) steps."""
+    f = fx("vqvae_train")
+    sd = O.deterministic_state(VO.vqvae_param_shapes(SMALL_VQVAE), seed=9)
+    seq = []
+    cur = sd
+    for step in range(2):
+        losses, grads, out, idx = VO.train_grads(cur, SMALL_VQVAE, f[f"s{step}.im"])
+        assert torch.equal(idx, f[f"s{step}.indices"])
+        for k in ("recon", "codebook", "commitment"):
+            assert rel(losses[k].reshape(1), f[f"s{step}.{k}"]) <= 1e-5, (step, k)
+        if step == 0:
+            assert rel(out, f["s0.out"]) <= 1e-5
+            norms = torch.stack([grads[k].norm() for k in sd])
+            assert ((norms - f["s0.grad_norms"]).abs() <= 1e-4 * f["s0.grad_norms"] + 1e-9).all()
+            for k in sd:
+                if "grad." + k in f:
+                    g = grads[k].reshape(-1)[:8192]
+                    assert rel(g, f["grad." + k]) <= 1e-4, k
+        seq.append(grads)
+        cur = VO.adam_steps(sd, seq)
+    for k in sd:
+        if "param." + k in f:
+            p = cur[k].reshape(-1)[:8192]
+            # Adam normalises each element's update to ~lr: gradients equal to ~1e-4 relative move an element's
+            # update by a small fraction of lr (2e-5), hence an absolute bound of 5 % of one step
+            assert (p - f["param." + k]).abs().max().item() <= 1e-6, k

@@ -1,0 +1,160 @@
+"""VQVAE training on the HIP path (sdmi.vqvae_train; reference train_vqvae_celebhq.py:414-466 without LPIPS / GAN,
+models/vqvae.py:93-158):
+* sdmi_vq_bwd (quantiser backward: post_quant_conv, straight-through + commitment, pre_quant_conv, codebook rows)
+  against torch autograd of the same fp32 formulas on the same inputs;
+* the engine's gradients of every parameter against the oracle (oracle.vqvae_oracle.train_grads, pinned to the
+  reference's own step by tests/test_oracle_vqvae.py) given the engine's own code choice -- bf16 activations:
+  per-parameter cosine >= 0.99 and the global norm within 5 %, as the UNet tests;
+* two trainer steps (Adam 2e-5, betas (0.5, 0.999)) against the reference fixture: losses and parameters;
+* the recorded plan replays the eager step bit-identically."""
+import os
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+from oracle import sd_oracle as O
+from oracle import vqvae_oracle as VO
+from tests.golden.configs import SMALL_VQVAE
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def cos(a, b):
+    a, b = a.reshape(-1).double(), b.reshape(-1).double()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
+def test_vq_bwd_kernel_matches_autograd():
+    import ctypes  # noqa: F401
+    from sdmi import _lib, kernels as K
+    g = torch.Generator().manual_seed(5)
+    B, h, w, C, Kc = 2, 9, 7, 4, 37
+    P = B * h * w
+    z_enc = torch.randn(P, C, generator=g)
+    w_pre, b_pre = torch.randn(C, C, generator=g) * 0.5, torch.randn(C, generator=g) * 0.1
+    w_post = torch.randn(C, C, generator=g) * 0.5
+    emb = torch.randn(Kc, C, generator=g)
+    dzin = (torch.randn(P, C, generator=g) * 1e-3).bfloat16()
+    cw, beta = 1.0, 0.2
+    # autograd reference: x = pre_quant(z_enc); q = emb[argmin]; losses; STE; post_quant; <dzin, y>
+    zl, wl, bl, el, wpl = (t.clone().requires_grad_(True) for t in (z_enc, w_pre, b_pre, emb, w_post))
+    x = zl @ wl.t() + bl
+    idx = torch.argmin(torch.cdist(x.detach(), emb), dim=-1)
+    q = el[idx]
+    loss = cw * torch.mean((q - x.detach()) ** 2) + beta * torch.mean((q.detach() - x) ** 2)
+    zq = x + (q - x).detach()
+    y = zq @ wpl.t()
+    (loss + (y * dzin.float()).sum()).backward()
+    # device inputs (NCHW fp32 for zq / pre, NHWC [P][8] for z_enc / dzin)
+    nchw = lambda t: t.detach().reshape(B, h * w, C).permute(0, 2, 1).contiguous().cuda()  # noqa: E731
+    pad8 = lambda t, dt: torch.nn.functional.pad(t.detach(), (0, 8 - C)).to(dt).contiguous().cuda()  # noqa: E731
+    d_zq, d_pre = nchw(zq), nchw(x)
+    d_z, d_dzin = pad8(z_enc, torch.float32), pad8(dzin.float(), torch.bfloat16)
+    d_idx = idx.reshape(B, h, w).cuda()
+    d_emb, d_wpre, d_wpost = emb.cuda(), w_pre.cuda(), w_post.cuda()
+    dz = torch.full((P, 8), float("nan"), dtype=torch.bfloat16, device="cuda")
+    outs = [torch.full(s, float("nan"), device="cuda") for s in ((C, C), (C,), (C, C), (C,), (Kc, C))]
+    L = _lib.lib()
+    ws = torch.empty(L.sdmi_vq_bwd_workspace() // 4, device="cuda")
+    _lib.check(L.sdmi_vq_bwd(d_dzin.data_ptr(), 8, d_zq.data_ptr(), d_wpost.data_ptr(), d_pre.data_ptr(),
+                             d_idx.data_ptr(), d_emb.data_ptr(), Kc, d_z.data_ptr(), 8, d_wpre.data_ptr(), B, h * w, C,
+                             beta, cw, dz.data_ptr(), 8, ws.data_ptr(), *[o.data_ptr() for o in outs], K._stream()),
+               "sdmi_vq_bwd")
+    torch.cuda.synchronize()
+    dw_post, db_post, dw_pre, db_pre, demb = (o.cpu() for o in outs)
+    assert torch.allclose(dw_post, wpl.grad, rtol=1e-4, atol=1e-7)
+    assert torch.allclose(db_post, dzin.float().sum(0), rtol=1e-4, atol=1e-7)
+    assert torch.allclose(dw_pre, wl.grad, rtol=1e-4, atol=1e-7)
+    assert torch.allclose(db_pre, bl.grad, rtol=1e-4, atol=1e-7)
+    assert torch.allclose(demb, el.grad, rtol=1e-5, atol=1e-8)
+    used = torch.zeros(Kc, dtype=torch.bool)
+    used[idx] = True
+    assert (demb[~used] == 0).all()
+    dzc = dz.float().cpu()
+    assert (dzc[:, C:] == 0).all()
+    ref = zl.grad
+    assert ((dzc[:, :C] - ref).abs() <= 1e-2 * ref.abs() + 1e-6).all()
+
+
+def _trainer(seed=9):
+    from sdmi.vqvae_train import VQVAETrainer
+    sd = O.deterministic_state(VO.vqvae_param_shapes(SMALL_VQVAE), seed=seed)
+    return VQVAETrainer(SMALL_VQVAE, {k: v.cuda() for k, v in sd.items()}, "cuda"), sd
+
+
+def test_engine_gradients_vs_oracle():
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    f = load_file(os.path.join(G, "vqvae_train.safetensors"))
+    tr, sd = _trainer()
+    im = f["s0.im"]
+    tr.step(im.cuda())
+    torch.cuda.synchronize()
+    idx = tr.indices.cpu()
+    # the bf16 encoder picks the reference's code for most latent pixels (random weights: many near ties)
+    agree = (idx == f["s0.indices"]).float().mean().item()
+    assert agree >= 0.8, agree
+    losses, grads, out, _ = VO.train_grads(sd, SMALL_VQVAE, im, indices=idx)
+    got = tr.losses()
+    assert abs(got["recon"] - losses["recon"].item()) <= 2e-2 * losses["recon"].item()
+    assert abs(got["codebook"] - losses["codebook"].item()) <= 5e-2 * losses["codebook"].item()
+    worst = (1.0, None)
+    for k in sd:
+        r, gk = grads[k], tr.store.g[k].cpu()
+        assert torch.isfinite(gk).all(), k
+        if r.norm() > 1e-6:
+            worst = min(worst, (cos(gk, r), k))
+    assert worst[0] >= 0.99, worst
+    gn = torch.norm(torch.stack([tr.store.g[k].norm() for k in sd])).item()
+    rn = torch.norm(torch.stack([grads[k].norm() for k in sd])).item()
+    assert abs(gn - rn) <= 0.05 * rn, (gn, rn)
+    # the codebook gradient exactly follows the engine's own code choice: rows of unused codes are zero
+    used = torch.zeros(SMALL_VQVAE["codebook_size"], dtype=torch.bool)
+    used[idx.reshape(-1)] = True
+    assert (tr.store.g["embedding.weight"].cpu()[~used] == 0).all()
+
+
+def test_two_trainer_steps_vs_reference():
+    f = load_file(os.path.join(G, "vqvae_train.safetensors"))
+    tr, sd = _trainer()
+    for step in range(2):
+        tr.step(f[f"s{step}.im"].cuda())
+        got = tr.losses()
+        ref = f[f"s{step}.recon"].item()
+        assert abs(got["recon"] - ref) <= 2e-2 * ref, (step, got, ref)
+        ref_cb = f[f"s{step}.codebook"].item()
+        assert abs(got["codebook"] - ref_cb) <= 0.1 * ref_cb, (step, got, ref_cb)
+    lr = 2e-5
+    st = tr.state_dict()
+    for k in sd:
+        if "param." + k not in f:
+            continue
+        p = st[k].detach().reshape(-1)[:8192].cpu()
+        r = f["param." + k]
+        p0 = sd[k].reshape(-1)[:8192]
+        # each Adam step moves an element by ~lr; bf16 gradient noise may flip the sign of near-zero elements
+        d = (p - r).abs()
+        assert d.max().item() <= 6 * lr, (k, d.max().item())
+        moved = (r - p0).abs() > 0.5 * lr
+        if moved.any():
+            ok = (d[moved] <= 0.5 * lr).float().mean().item()
+            assert ok >= 0.9, (k, ok)
+
+
+def test_plan_replay_matches_eager():
+    from sdmi.plan import StepPlan
+    f = load_file(os.path.join(G, "vqvae_train.safetensors"))
+    im = f["s0.im"].cuda()
+    a, _ = _trainer()
+    b, _ = _trainer()
+    a.step(im)
+    b.step(im)
+    plan = StepPlan(lambda: a.step(im))
+    b.step(im)
+    plan.replay()
+    b.step(im)
+    torch.cuda.synchronize()
+    assert torch.equal(a.store.params, b.store.params)
+    assert torch.equal(a.store.grads, b.store.grads)
+    assert torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
