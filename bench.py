@@ -108,6 +108,37 @@ def dit_config():
     return dit12l_config()
 
 
+def cpu_model():
+    """The host CPU as /proc/cpuinfo names it, with its logical CPU count (lscpu's 'Model name' / 'CPU(s)')."""
+    name = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                name = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return f"{name}, {os.cpu_count()} logical CPUs visible"
+
+
+def timed_cpu(fn, warmup=1, timed=3):
+    """Median wall time of `timed` calls of fn after `warmup` calls (1 warm-up + 3 timed)."""
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(timed):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2], ts
+
+
+def _cpu_result(per, ts, threads, what):
+    return dict(value=1.0 / per, unit="steps/s", cores=threads, kind="port", cpu=cpu_model(),
+                sample=f"{what}; median of {len(ts)} timed steps {per:.2f} s/step (all: "
+                       f"{', '.join(f'{t:.2f}' for t in ts)}), torch CPU {torch.__version__} with {threads} threads")
+
+
 def cpu_baseline_dit(cfg, B=32):
     """The DiT oracle's fp32 training step (Model_DiT_12L_train.py:300-375) on the host cores."""
     from oracle import sd_oracle as O, dit_oracle as DO
@@ -120,17 +151,13 @@ def cpu_baseline_dit(cfg, B=32):
     x0 = torch.randn(B, 4, 32, 32, generator=g)
     cmap = torch.randint(0, 19, (B, 512, 512), generator=g)
     mask = torch.nn.functional.one_hot(cmap, 19).movedim(-1, 1)[:, 1:].float()
-    times = []
-    for i in range(3):  # 1 warm-up + 2 timed
+
+    def step():
         noise = torch.randn(x0.shape, generator=g)
         t = torch.randint(0, 1000, (B,), generator=g)
-        t0 = time.perf_counter()
         DO.dit_train_step(sd, opt, cfg, sched, x0, noise, t, {"image": mask})
-        times.append(time.perf_counter() - t0)
-    per = sum(times[1:]) / 2
-    return dict(value=1.0 / per, unit="steps/s", cores=threads, kind="port",
-                sample=f"DiT oracle fp32 train step (fwd+bwd+clip+Adam), B={B}, 1 warm-up + 2 timed steps, "
-                       f"{per:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
+    per, ts = timed_cpu(step)
+    return _cpu_result(per, ts, threads, f"DiT oracle fp32 train step (fwd+bwd+clip+Adam), B={B}, 1 warm-up")
 
 
 def vqvae_config():
@@ -139,52 +166,54 @@ def vqvae_config():
 
 
 def cpu_baseline_vqvae(cfg, B=8):
-    """The VQVAE oracle's fp32 encode + decode on the host cores (bounded sample: 1 warm-up + 1 timed)."""
+    """The VQVAE oracle's fp32 encode + decode on the host cores."""
     from oracle import sd_oracle as O, vqvae_oracle as VO
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     sd = O.deterministic_state(VO.vqvae_param_shapes(cfg), seed=0)
     x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1111)) * 2 - 1
-    times = []
-    with torch.no_grad():
-        for i in range(2):
-            t0 = time.perf_counter()
+
+    def step():
+        with torch.no_grad():
             zq, _, _ = VO.encode(sd, cfg, x)
             VO.decode(sd, cfg, zq)
-            times.append(time.perf_counter() - t0)
-    return dict(value=1.0 / times[-1], unit="steps/s", cores=threads, kind="port",
-                sample=f"VQVAE oracle fp32 encode+decode, B={B} at 256x256, 1 warm-up + 1 timed, {times[-1]:.2f} s/step, "
-                       f"torch CPU {torch.__version__} with {threads} threads")
+    per, ts = timed_cpu(step)
+    return _cpu_result(per, ts, threads, f"VQVAE oracle fp32 encode+decode, B={B} at 256x256, 1 warm-up")
 
 
-def cpu_baseline(cfg, B=32, uncond=False):
-    """The oracle (CPU fp32 restatement of the reference step) on the host cores; bounded sample."""
+def cpu_baseline(cfg, B=32, uncond=False, small_batch=4):
+    """The oracle (CPU fp32 restatement of the reference step) on the host cores: B=32 (the bench workload) and
+    B=small_batch, each 1 warm-up + 3 timed, median."""
     from oracle import sd_oracle as O
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    sd = O.deterministic_state(O.unet_param_shapes(cfg, base="uncond" if uncond else None), seed=0)
-    ema = {k: v.clone() for k, v in sd.items()}
-    opt = O.AdamState(sd)
-    sched = O.SchedulerTables(1000, 0.0015, 0.0195) if uncond else O.SchedulerTables(1000, 0.00085, 0.012)
-    g = torch.Generator().manual_seed(1111)
-    x0 = torch.randn(B, 4, 32, 32, generator=g)
-    text = torch.randn(B, 77, 512, generator=g)
-    cmap = torch.randint(0, 19, (B, 512, 512), generator=g)
-    mask = torch.nn.functional.one_hot(cmap, 19).movedim(-1, 1)[:, 1:].float()
-    times = []
-    for i in range(2):  # 1 warm-up + 1 timed
-        noise = torch.randn(x0.shape, generator=g)
-        t = torch.randint(0, 1000, (B,), generator=g)
-        t0 = time.perf_counter()
-        if uncond:  # tools/train_ddpm_vqvae.py: no clip (inf), no EMA (decay 0: a copy, negligible)
-            O.train_step(sd, ema, opt, cfg, sched, x0, noise, t, None, lr=5e-6, clip=float("inf"), ema_decay=0.0)
+    res = None
+    for b in (B, small_batch):
+        sd = O.deterministic_state(O.unet_param_shapes(cfg, base="uncond" if uncond else None), seed=0)
+        ema = {k: v.clone() for k, v in sd.items()}
+        opt = O.AdamState(sd)
+        sched = O.SchedulerTables(1000, 0.0015, 0.0195) if uncond else O.SchedulerTables(1000, 0.00085, 0.012)
+        g = torch.Generator().manual_seed(1111)
+        x0 = torch.randn(b, 4, 32, 32, generator=g)
+        text = torch.randn(b, 77, 512, generator=g)
+        cmap = torch.randint(0, 19, (b, 512, 512), generator=g)
+        mask = torch.nn.functional.one_hot(cmap, 19).movedim(-1, 1)[:, 1:].float()
+
+        def step():
+            noise = torch.randn(x0.shape, generator=g)
+            t = torch.randint(0, 1000, (b,), generator=g)
+            if uncond:  # tools/train_ddpm_vqvae.py: no clip (inf), no EMA (decay 0: a copy, negligible)
+                O.train_step(sd, ema, opt, cfg, sched, x0, noise, t, None, lr=5e-6, clip=float("inf"), ema_decay=0.0)
+            else:
+                O.train_step(sd, ema, opt, cfg, sched, x0, noise, t, {"text": text, "image": mask})
+        per, ts = timed_cpu(step)
+        what = "fwd+bwd+Adam" if uncond else "fwd+bwd+clip+Adam+EMA"
+        r = _cpu_result(per, ts, threads, f"oracle fp32 train step ({what}), B={b}, 1 warm-up")
+        if res is None:
+            res = r
         else:
-            O.train_step(sd, ema, opt, cfg, sched, x0, noise, t, {"text": text, "image": mask})
-        times.append(time.perf_counter() - t0)
-    what = "fwd+bwd+Adam" if uncond else "fwd+bwd+clip+Adam+EMA"
-    return dict(value=1.0 / times[-1], unit="steps/s", cores=threads, kind="port",
-                sample=f"oracle fp32 train step ({what}), B={B}, 1 warm-up + 1 timed step, "
-                       f"{times[-1]:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
+            res[f"b{b}"] = {"value": r["value"], "unit": "steps/s", "sample": r["sample"]}
+    return res
 
 
 def main_vqvae(args, wl, world, rank, device):
@@ -245,18 +274,15 @@ def main_vqvae(args, wl, world, rank, device):
 
 def cpu_baseline_vqvae_train(cfg, B=8):
     """The VQVAE oracle's fp32 generator step (train_grads: forward, losses, autograd backward) on the host cores;
-    bounded sample: one timed step (no warm-up: ~15 s)."""
+    3 timed steps, no warm-up (~11 s each)."""
     from oracle import sd_oracle as O, vqvae_oracle as VO
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     sd = O.deterministic_state(VO.vqvae_param_shapes(cfg), seed=0)
     x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1111)) * 2 - 1
-    t0 = time.perf_counter()
-    VO.train_grads(sd, cfg, x)
-    dt = time.perf_counter() - t0
-    return dict(value=1.0 / dt, unit="steps/s", cores=threads, kind="port",
-                sample=f"VQVAE oracle fp32 fwd + losses + bwd (no optimizer), B={B} at 256x256, 1 timed step, "
-                       f"{dt:.2f} s/step, torch CPU {torch.__version__} with {threads} threads")
+    per, ts = timed_cpu(lambda: VO.train_grads(sd, cfg, x), warmup=0)
+    return _cpu_result(per, ts, threads, f"VQVAE oracle fp32 fwd + losses + bwd (no optimizer), B={B} at 256x256, "
+                                         "no warm-up")
 
 
 def main_vqvae_train(args, wl, world, rank, device):
