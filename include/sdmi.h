@@ -238,13 +238,17 @@ int sdmi_mse_patch(const float* pred, int ld, const float* target, int B, int C,
  *                     NHWC bf16) -> post_quant_conv dW/db, the straight-through gradient of the pre-quantisation
  *                     latent plus commitment_beta * 2 (x - q) / n, pre_quant_conv dW/db and dz_enc (NHWC bf16
  *                     gradient of encoder_conv_out's output), and the codebook gradient codebook_weight * 2 (q - x) / n
- *                     scattered to the selected rows (deterministic, no atomics). ws: sdmi_vq_bwd_workspace() bytes. */
+ *                     scattered to the selected rows (deterministic, no atomics). ws: sdmi_vq_bwd_workspace() bytes.
+ *                     dzq_add (nullable, NCHW fp32): an extra gradient of the quantised latent (the module's returned
+ *                     z); loss_w (nullable, device {codebook, commitment}): multiplies the two host weights (the
+ *                     autograd gradients of the two loss outputs, read on the device). */
 size_t sdmi_vq_workspace(long long pixels);
 size_t sdmi_vq_bwd_workspace(void);
 int sdmi_vq_bwd(const void* dzin, int ld_dzin, const float* zq, const float* w_post, const float* xq, const long long* idx,
                 const float* codebook, int K, const float* z_enc, int ldz, const float* w_pre, int B, int HW, int C,
                 float commitment_beta, float codebook_weight, void* dz_enc, int ld_out, float* ws, float* dw_post,
-                float* db_post, float* dw_pre, float* db_pre, float* demb, sdmi_stream_t stream);
+                float* db_post, float* dw_pre, float* db_pre, float* demb, const float* dzq_add, const float* loss_w,
+                sdmi_stream_t stream);
 int sdmi_vq_quantize(const float* z, int ldz, const float* w, const float* b, const float* codebook, int K, int B,
                      int HW, int C, float* zq, long long* idx, float* xq, float* ws, float* loss, sdmi_stream_t stream);
 int sdmi_pointwise_in(const float* z, int B, int C, int HW, const float* w, const float* b, int cout, void* out,

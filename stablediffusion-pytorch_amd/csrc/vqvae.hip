@@ -168,6 +168,8 @@ struct VqBwdArgs {
   const float* w_pre;                   // pre_quant_conv weight (C, C)
   int B, HW, C;
   float g_commit;                       // commitment_beta * 2 / (P * C)
+  const float* dzq_add;                 // optional extra gradient of the quantised latent (NCHW fp32), or null
+  const float* loss_w;                  // optional device loss weights {codebook, commitment} (scale the host ones)
   bf16_t* dz_enc; int ld_out;           // gradient of encoder_conv_out's output, NHWC bf16 [P][ld_out]
   float* partial;                       // [blocks][VQB_PART]
 };
@@ -176,6 +178,7 @@ __global__ __launch_bounds__(VQB_NT) void vq_bwd_kernel(const VqBwdArgs a) {
   __shared__ float red[VQB_NT / 64][VQB_PART];
   const int C = a.C;
   const long long P = (long long)a.B * a.HW;
+  const float g_commit = a.loss_w ? a.g_commit * a.loss_w[1] : a.g_commit;
   float acc[VQB_PART];
 #pragma unroll
   for (int i = 0; i < VQB_PART; ++i) acc[i] = 0.f;
@@ -199,6 +202,7 @@ __global__ __launch_bounds__(VQB_NT) void vq_bwd_kernel(const VqBwdArgs a) {
 #pragma unroll
       for (int co = 0; co < MAXC; ++co)
         if (co < C && ci < C) s = fmaf(a.w_post[co * C + ci], dzin[co], s);
+      if (a.dzq_add && ci < C) s += a.dzq_add[(bb * C + ci) * a.HW + p];
       dzq[ci] = s;
     }
 #pragma unroll
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(VQB_NT) void vq_bwd_kernel(const VqBwdArgs a) {
     }
     // STE + commitment: dL/dx = dzq + beta * 2 (x - q) / n
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) dx[c] = fmaf(a.g_commit, x[c] - q[c], dzq[c]);
+    for (int c = 0; c < MAXC; ++c) dx[c] = fmaf(g_commit, x[c] - q[c], dzq[c]);
     // pre_quant_conv backward
 #pragma unroll
     for (int co = 0; co < MAXC; ++co) {
@@ -265,7 +269,7 @@ __global__ void vq_bwd_finish_kernel(const float* partial, int blocks, int C, fl
 // the index list once through LDS and every thread (one code) scans it
 __global__ __launch_bounds__(256) void vq_codebook_grad_kernel(const long long* idx, const float* xq, const float* codebook,
                                                                int K, int B, int HW, int C, float g_codebook,
-                                                               float* demb) {
+                                                               const float* loss_w, float* demb) {
   __shared__ int sidx[1024];
   const int k = blockIdx.x * 256 + threadIdx.x;
   const long long P = (long long)B * HW;
@@ -288,6 +292,7 @@ __global__ __launch_bounds__(256) void vq_codebook_grad_kernel(const long long* 
     }
   }
   if (k >= K) return;
+  if (loss_w) g_codebook *= loss_w[0];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c)
     if (c < C) demb[(long long)k * C + c] = g_codebook * fmaf((float)cnt, codebook[(long long)k * C + c], acc[c]);
@@ -332,7 +337,8 @@ extern "C" int sdmi_vq_bwd(const void* dzin, int ld_dzin, const float* zq, const
                            const long long* idx, const float* codebook, int K, const float* z_enc, int ldz,
                            const float* w_pre, int B, int HW, int C, float commitment_beta, float codebook_weight,
                            void* dz_enc, int ld_out, float* ws, float* dw_post, float* db_post, float* dw_pre,
-                           float* db_pre, float* demb, sdmi_stream_t stream) {
+                           float* db_pre, float* demb, const float* dzq_add, const float* loss_w,
+                           sdmi_stream_t stream) {
   if (!dzin || !zq || !w_post || !xq || !idx || !codebook || !z_enc || !w_pre || !dz_enc || !ws || !demb ||
       C <= 0 || C > MAXC || ld_out < C || ldz < C || ld_dzin < C || B <= 0 || HW <= 0 || K <= 0)
     return -1;
@@ -342,6 +348,7 @@ extern "C" int sdmi_vq_bwd(const void* dzin, int ld_dzin, const float* zq, const
   a.dzin = (const bf16_t*)dzin; a.ld_dzin = ld_dzin; a.zq = zq; a.w_post = w_post; a.xq = xq; a.idx = idx;
   a.codebook = codebook; a.z_enc = z_enc; a.ldz = ldz; a.w_pre = w_pre; a.B = B; a.HW = HW; a.C = C;
   a.g_commit = commitment_beta * 2.0f / n;
+  a.dzq_add = dzq_add; a.loss_w = loss_w;
   a.dz_enc = (bf16_t*)dz_enc; a.ld_out = ld_out; a.partial = ws;
   const int blocks = (int)std::min<long long>(512, (P + VQB_NT - 1) / VQB_NT);
   sdmi_rt::launch(vq_bwd_kernel, dim3(blocks), dim3(VQB_NT), 0, (hipStream_t)stream, a);
@@ -350,7 +357,7 @@ extern "C" int sdmi_vq_bwd(const void* dzin, int ld_dzin, const float* zq, const
                   dw_post, db_post, dw_pre, db_pre);
   SDMI_CHECK_LAUNCH();
   sdmi_rt::launch(vq_codebook_grad_kernel, dim3((K + 255) / 256), dim3(256), 0, (hipStream_t)stream, idx, xq,
-                  codebook, K, B, HW, C, codebook_weight * 2.0f / n, demb);
+                  codebook, K, B, HW, C, codebook_weight * 2.0f / n, loss_w, demb);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -6,7 +6,11 @@ embedding, post_quant_conv, decoder_conv_in, decoder_mids, decoder_layers (UpBlo
 decoder_conv_out), so gen_vqvae_latents.py / sample_ddpm_*.py load a reference checkpoint and call
 `encode(im)` -> (z, {'codebook_loss', 'commitment_loss'}), `decode(z)` and `forward(x)` -> (out, z, losses)
 unchanged. encode / decode run as one schedule of gfx950 kernels (sdmi.vqvae_engine) in inference mode
-(the reference's latent-generation and decoding path); gradients through the VQVAE are not provided.
+(the reference's latent-generation and decoding path). forward(x) with autograd enabled runs the training
+engine (sdmi.vqvae_train) as one autograd Function: train_vqvae_celebhq.py:414-441 then computes its losses on
+the returned (out, z, {'codebook_loss', 'commitment_loss'}) and calls .backward() unchanged -- the gradients of
+the reconstruction (MSE, LPIPS, GAN terms: any torch loss), of z and of both quantiser losses flow back through
+the straight-through estimator into every parameter.
 """
 import torch
 import torch.nn as nn
@@ -14,6 +18,39 @@ import torch.nn as nn
 from models.blocks import DownBlock, MidBlock, UpBlock
 from sdmi import _lib
 from sdmi.vqvae_engine import VQVAEEngine
+from sdmi.vqvae_train import VQVAETrainEngine
+
+
+class VQVAEFunction(torch.autograd.Function):
+    """(x, *params) -> (reconstruction, z_q, codebook_loss, commitment_loss) on the HIP training engine."""
+
+    @staticmethod
+    def forward(ctx, mod, x, *params):
+        eng = mod._train_eng(x)
+        B, C, H, W = x.shape
+        out, c = eng.forward(x)
+        ctx.mod, ctx.c, ctx.hw = mod, c, (B, H, W)
+        vq = c["vq_loss"].reshape(())
+        return eng.pred_to_nchw(out, B, H, W), c["zq"], vq.clone(), vq.clone()
+
+    @staticmethod
+    def backward(ctx, dimg, dz, dcb, dcm):
+        mod = ctx.mod
+        eng = mod._tengine
+        B, H, W = ctx.hw
+        dev = eng.device
+        dout = (eng.dpred_from_nchw(dimg.float().contiguous()) if dimg is not None
+                else torch.zeros(B * H * W, 8, dtype=torch.bfloat16, device=dev))
+        zero = torch.zeros((), device=dev)
+        loss_w = torch.stack([(dcb if dcb is not None else zero).float().reshape(()),
+                              (dcm if dcm is not None else zero).float().reshape(())])
+        names = [k for k, _ in mod.named_parameters()]
+        params = dict(mod.named_parameters())
+        grads = {k: torch.empty_like(params[k]) for k in names}
+        eng.backward(ctx.c, dout, 1.0, 1.0, grads=grads, dzq=dz.float().contiguous() if dz is not None else None,
+                     loss_w=loss_w)
+        ctx.c = None
+        return (None, None) + tuple(grads[k] for k in names)
 
 
 class VQVAE(nn.Module):
@@ -79,6 +116,23 @@ class VQVAE(nn.Module):
         self._engine.refresh_weights()  # bf16 GEMM-layout copies of the (possibly updated) fp32 weights
         return self._engine
 
+    def _train_eng(self, t):
+        if not t.is_cuda:
+            raise RuntimeError("the sdmi VQVAE runs on the MI355X HIP path only (move the model and inputs to cuda)")
+        _lib.lib()
+        params = dict(self.named_parameters())
+        ptrs = [p.data_ptr() for p in params.values()]
+        if getattr(self, "_tengine", None) is None or ptrs != self._tptrs:
+            self._tengine = VQVAETrainEngine(self.model_config_dict(), {k: v.detach() for k, v in params.items()},
+                                             im_channels=self.im_channels)
+            self._tptrs = ptrs
+            self._tsig = None
+        sig = tuple(p._version for p in params.values())
+        if sig != self._tsig:  # repack only after an update (optimizer.step / load_state_dict bump the versions)
+            self._tengine.refresh_weights()
+            self._tsig = sig
+        return self._tengine
+
     def model_config_dict(self):
         return {"down_channels": self.down_channels, "mid_channels": self.mid_channels,
                 "down_sample": self.down_sample, "attn_down": self.attns, "num_down_layers": self.num_down_layers,
@@ -101,5 +155,8 @@ class VQVAE(nn.Module):
         return self._eng(z).decode(z)
 
     def forward(self, x):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            out, z, cb, cm = VQVAEFunction.apply(self, x, *self.parameters())
+            return out, z, {"codebook_loss": cb, "commitment_loss": cm}
         z, quant_losses = self.encode(x)
         return self.decode(z), z, quant_losses

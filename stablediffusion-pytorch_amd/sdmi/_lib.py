@@ -118,7 +118,7 @@ SIGNATURES = {
     "sdmi_randn": ([_P, _L, ctypes.c_ulonglong, _P, _I, _P], _I),
     "sdmi_vq_bwd_workspace": ([], _SZ),
     "sdmi_vq_bwd": ([_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _F, _F, _P, _I, _P, _P, _P, _P, _P, _P,
-                     _P], _I),
+                     _P, _P, _P], _I),
     "sdmi_plan_begin": ([], _I),
     "sdmi_plan_end": ([ctypes.POINTER(ctypes.c_void_p)], _I),
     "sdmi_plan_recording": ([], _I),

@@ -16,6 +16,8 @@ This module replaces both with flat binary shards that load without unpickling:
 * mask shard (`*.sdmsk`): same header + names + a uint8 class map `(N, MH, MW)` (values already clamped to
   [0, mask_channels]): 262 KB per image instead of 18.9 MB. The HIP input staging consumes class maps
   directly (`sdmi_prep_input_cmap` / `sdmi_cond_wgrad_cmap`, bit-identical to the one-hot path).
+* `generate_latents`: the reference's latent generation (gen_vqvae_latents.py:89-106) batched through the HIP
+  VQVAE encoder, written as `.sdlat` shards of 1000 images.
 * `ResidentLatentSet`: the whole training set (latents + class maps) copied to HBM once (30k CelebHQ images =
   0.5 GB latents + 7.9 GB class maps, a few % of 288 GB); a batch is a device-side gather of row indices, no
   per-step host work or H2D copies.
@@ -84,10 +86,18 @@ def read_latent_shard(path):
     return _read(path, MAGIC_LAT)
 
 
+def _shards(d, ext):
+    """Shard files of a directory in part order: numbered parts ({part}.sdlat) numerically, then the rest by name."""
+    def key(f):
+        stem = os.path.splitext(os.path.basename(f))[0]
+        return (0, int(stem), "") if stem.isdigit() else (1, 0, f)
+    return sorted(glob.glob(os.path.join(d, "*" + ext)), key=key)
+
+
 def load_latents(latent_path):
     """Mirror of utils/diffusion_utils.py:7-18 over `*.sdlat` shards: {name: (C, H, W) fp32 tensor}."""
     out = {}
-    for fname in sorted(glob.glob(os.path.join(latent_path, "*.sdlat"))):
+    for fname in _shards(latent_path, ".sdlat"):
         names, arr = read_latent_shard(fname)
         for i, k in enumerate(names):
             out[k] = torch.from_numpy(np.array(arr[i]))
@@ -123,6 +133,41 @@ def read_mask_shard(path):
     return _read(path, MAGIC_MSK)
 
 
+def generate_latents(encode, images, names, latent_dir, shard_size=1000, batch_size=32):
+    """gen_vqvae_latents.py:89-106 as a batched pipeline: encode every image with `encode` (a VQVAE module's
+    `encode` -- models.vqvae.VQVAE on the HIP path -- or any callable (B, C, H, W) -> (z, ...) / z) batch_size images
+    at a time, and write the quantised latents as `{part}.sdlat` shards of `shard_size` records in image order (the
+    reference pickles `{image path: (1, C, h, w)}` every 1000 images as `{part}.pkl`). `images`: a (N, C, H, W)
+    tensor (host or device) or a sequence of (C, H, W) / (1, C, H, W) tensors. Returns the shard paths."""
+    if len(images) != len(names):
+        raise ValueError(f"{len(images)} images for {len(names)} names")
+    os.makedirs(latent_dir, exist_ok=True)
+    paths, part, pending = [], 0, {}
+
+    def flush():
+        nonlocal part, pending
+        path = os.path.join(latent_dir, f"{part}.sdlat")
+        write_latent_shard(path, pending)
+        paths.append(path)
+        part += 1
+        pending = {}
+
+    for s in range(0, len(names), batch_size):
+        chunk = images[s:s + batch_size]
+        if not isinstance(chunk, torch.Tensor):
+            chunk = torch.stack([c[0] if c.dim() == 4 else c for c in chunk])
+        with torch.no_grad():
+            z = encode(chunk)
+        z = (z[0] if isinstance(z, (tuple, list)) else z).detach().to("cpu", torch.float32)
+        for i in range(z.shape[0]):
+            pending[names[s + i]] = z[i]
+            if len(pending) == shard_size:
+                flush()
+    if pending:
+        flush()
+    return paths
+
+
 class ResidentLatentSet:
     """Every latent (and class map) of the training set resident in HBM; `batch(idx)` gathers rows on device.
 
@@ -131,7 +176,7 @@ class ResidentLatentSet:
 
     def __init__(self, latent_dir, names=None, mask_dir=None, device="cuda"):
         table = {}
-        for fname in sorted(glob.glob(os.path.join(latent_dir, "*.sdlat"))):
+        for fname in _shards(latent_dir, ".sdlat"):
             ns, arr = read_latent_shard(fname)
             for i, k in enumerate(ns):
                 table[k] = (arr, i)
@@ -155,7 +200,7 @@ class ResidentLatentSet:
         self.class_maps = None
         if mask_dir is not None:
             mt = {}
-            for fname in sorted(glob.glob(os.path.join(mask_dir, "*.sdmsk"))):
+            for fname in _shards(mask_dir, ".sdmsk"):
                 ns, arr = read_mask_shard(fname)
                 for i, k in enumerate(ns):
                     mt[k] = (arr, i)

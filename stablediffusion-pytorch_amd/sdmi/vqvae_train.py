@@ -268,8 +268,8 @@ class VQVAETrainEngine(UNetEngine):
             P["pre_quant_conv.weight"].data_ptr(), B, h * w, L["z"], self.commitment_beta, self.codebook_weight,
             dz.data_ptr(), 8, ws.data_ptr(), self.g("post_quant_conv.weight").data_ptr(),
             self.g("post_quant_conv.bias").data_ptr(), self.g("pre_quant_conv.weight").data_ptr(),
-            self.g("pre_quant_conv.bias").data_ptr(), self.g("embedding.weight").data_ptr(), K._stream()),
-            "sdmi_vq_bwd")
+            self.g("pre_quant_conv.bias").data_ptr(), self.g("embedding.weight").data_ptr(), K._p(self.dzq_add),
+            K._p(self.loss_w), K._stream()), "sdmi_vq_bwd")
 
     def _bwd_enc_out(self, c, grads):
         P, G = self.P, self.L["G"]
@@ -297,11 +297,15 @@ class VQVAETrainEngine(UNetEngine):
                          bias_grad=self.g("encoder_conv_in.bias"))
 
     # ------------------------------------------------------------------------------------------
-    def backward(self, ctx, dout, codebook_weight=1.0, commitment_beta=0.2, grads=None, on_progress=None):
+    def backward(self, ctx, dout, codebook_weight=1.0, commitment_beta=0.2, grads=None, on_progress=None,
+                 dzq=None, loss_w=None):
         """dout: NHWC bf16 [B*H*W, 8] = dL/d(reconstruction). The codebook / commitment terms enter at the
-        quantiser with their weights. Every parameter gradient is fully overwritten."""
+        quantiser with their weights (times the device scalars loss_w = {d codebook, d commitment} when given);
+        dzq (NCHW fp32, optional): a gradient of the quantised latent from outside the decoder. Every parameter
+        gradient is fully overwritten."""
         self.codebook_weight = float(codebook_weight)
         self.commitment_beta = float(commitment_beta)
+        self.dzq_add, self.loss_w = dzq, loss_w
         if grads is not None:
             self.Gd = grads
         assert self.Gd is not None, "engine built without gradient buffers"

@@ -70,3 +70,29 @@ def test_mask_shard_and_resident_set(tmp_path):
         k = names[i]
         assert torch.equal(x[j], lat[k][0])
         assert torch.equal(m[j], cms[k.split("/")[-1]])  # basename lookup (celeb_dataset.py:143-146)
+
+
+def test_generate_latents_shards_in_image_order(tmp_path):
+    """gen_vqvae_latents.py:89-106: one record per image, a shard every `shard_size` images ({part} numbering),
+    the remainder in a last shard; the encoder is any batch callable here (the HIP VQVAE in test_latent_gen_gpu)."""
+    g = torch.Generator().manual_seed(3)
+    ims = torch.randn(70, 3, 16, 16, generator=g)
+    names = [f"celeb/{i}.jpg" for i in range(70)]
+    enc = lambda x: (torch.nn.functional.avg_pool2d(x, 4).repeat(1, 2, 1, 1)[:, :4], None)  # noqa: E731
+    paths = LT.generate_latents(enc, ims, names, str(tmp_path / "lat"), shard_size=8, batch_size=6)
+    assert [p.split("/")[-1] for p in paths] == [f"{i}.sdlat" for i in range(9)]
+    sizes = [LT.read_latent_shard(p)[1].shape[0] for p in paths]
+    assert sizes == [8] * 8 + [6]
+    ref = enc(ims)[0]
+    got = LT.load_latents(str(tmp_path / "lat"))
+    assert list(got) == names  # part order is numeric (0, 1, ..., 8), records in image order
+    for i, k in enumerate(names):
+        assert torch.equal(got[k], ref[i])
+    rs = LT.ResidentLatentSet(str(tmp_path / "lat"), device="cpu")
+    assert rs.names == names
+    x, _ = rs.batch(torch.tensor([69, 0, 33]))
+    assert torch.equal(x, ref[[69, 0, 33]])
+    # a list of (1, C, H, W) images (the reference data loader's batch of one) gives the same shards
+    LT.generate_latents(enc, [im[None] for im in ims], names, str(tmp_path / "lat2"), shard_size=8, batch_size=5)
+    got2 = LT.load_latents(str(tmp_path / "lat2"))
+    assert all(torch.equal(got2[k], got[k]) for k in names)
