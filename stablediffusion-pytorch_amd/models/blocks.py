@@ -1,14 +1,17 @@
 """Drop-in mirror of the reference's models/blocks.py module surface.
 
-The blocks hold parameters only: the same attribute names, leaf module types (nn.GroupNorm,
-nn.Conv2d, nn.ConvTranspose2d, nn.Linear, nn.MultiheadAttention) and default initialisation as the
-reference (blocks.py:27-499), so state dicts and reference checkpoints load unchanged and a
-layer-swap tool that replaces exact nn.Conv2d / nn.Linear leaves still finds them.  The compute
-for a whole UNet runs in sdmi.unet_engine on the HIP kernels (see models/unet_cond_base.py);
-calling a block on its own is not a supported path of this build.
+The blocks have the same attribute names, leaf module types (nn.GroupNorm, nn.Conv2d, nn.ConvTranspose2d,
+nn.Linear, nn.MultiheadAttention) and default initialisation as the reference (blocks.py:27-499), so state dicts
+and reference checkpoints load unchanged and a layer-swap tool that replaces exact nn.Conv2d / nn.Linear leaves
+still finds them. A whole UNet / VQVAE whose leaves are all exact torch types runs as one fused schedule (the
+engines of sdmi); a block called on its own, or any block of a model with a swapped leaf, runs the forwards below:
+the reference's composition (blocks.py:111-146, 225-267, 343-370, 461-499) with every leaf executed by
+sdmi.leaf.call -- exact torch types on the HIP per-op kernels, swapped layers through their own forward.
 """
 import torch
 import torch.nn as nn
+
+from sdmi import leaf as LF
 
 
 def get_time_embedding(time_steps, temb_dim):
@@ -48,9 +51,37 @@ def _add_residual(m, n, cin, cout):
     m.residual_input_conv = nn.ModuleList([nn.Conv2d(cin if i == 0 else cout, cout, 1) for i in range(n)])
 
 
+def _resnet(blk, i, x, t_emb):
+    """GN-SiLU-conv, + t_emb_layers(t_emb) per channel, GN-SiLU-conv, + 1x1 residual conv (blocks.py:114-120)."""
+    out = LF.call(blk.resnet_conv_first[i], x)
+    if blk.t_emb_dim is not None:
+        out = out + LF.call(blk.t_emb_layers[i], t_emb)[:, :, None, None]
+    out = LF.call(blk.resnet_conv_second[i], out)
+    return out + LF.call(blk.residual_input_conv[i], x)
+
+
+def _attend(norm, attn, out, context=None, proj=None):
+    """out + attention(GroupNorm(out) as tokens [, context_proj(context)]) (blocks.py:122-142)."""
+    B, C, h, w = out.shape
+    a = LF.call(norm, out.reshape(B, C, h * w)).transpose(1, 2)
+    if proj is None:
+        o, _ = LF.call(attn, a, a, a)
+    else:
+        cp = LF.call(proj, context)
+        o, _ = LF.call(attn, a, cp, cp)
+    return out + o.transpose(1, 2).reshape(B, C, h, w)
+
+
+def _cross(blk, i, out, x, context):
+    assert context is not None, "context cannot be None if cross attention layers are used"
+    assert len(context.shape) == 3, "Context shape does not match B,_,CONTEXT_DIM"
+    assert context.shape[0] == x.shape[0] and context.shape[-1] == blk.context_dim, \
+        "Context shape does not match B,_,CONTEXT_DIM"
+    return _attend(blk.cross_attention_norms[i], blk.cross_attentions[i], out, context, blk.context_proj[i])
+
+
 class _ParamBlock(nn.Module):
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("blocks are parameter holders; run the whole Unet (HIP engine)")
+    pass
 
 
 class DownBlock(_ParamBlock):
@@ -69,6 +100,16 @@ class DownBlock(_ParamBlock):
         _add_residual(self, num_layers, in_channels, out_channels)
         self.down_sample_conv = nn.Conv2d(out_channels, out_channels, 4, 2, 1) if down_sample else nn.Identity()
 
+    def forward(self, x, t_emb=None, context=None):
+        out = x
+        for i in range(self.num_layers):
+            out = _resnet(self, i, out, t_emb)
+            if self.attn:
+                out = _attend(self.attention_norms[i], self.attentions[i], out)
+            if self.cross_attn:
+                out = _cross(self, i, out, x, context)
+        return LF.call(self.down_sample_conv, out)
+
 
 class MidBlock(_ParamBlock):
     """resnet, then num_layers x (self-attention, [cross-attention], resnet) (blocks.py:149-267)."""
@@ -83,6 +124,15 @@ class MidBlock(_ParamBlock):
             _add_cross(self, num_layers, out_channels, num_heads, norm_channels, context_dim)
         _add_residual(self, num_layers + 1, in_channels, out_channels)
 
+    def forward(self, x, t_emb=None, context=None):
+        out = _resnet(self, 0, x, t_emb)
+        for i in range(self.num_layers):
+            out = _attend(self.attention_norms[i], self.attentions[i], out)
+            if self.cross_attn:
+                out = _cross(self, i, out, x, context)
+            out = _resnet(self, i + 1, out, t_emb)
+        return out
+
 
 class UpBlock(_ParamBlock):
     """VQVAE decoder block: ConvTranspose(4, 2, 1) of the full input, num_layers x (resnet, [self-attn])
@@ -96,6 +146,17 @@ class UpBlock(_ParamBlock):
             _add_attention(self, num_layers, out_channels, num_heads, norm_channels)
         _add_residual(self, num_layers, in_channels, out_channels)
         self.up_sample_conv = nn.ConvTranspose2d(in_channels, in_channels, 4, 2, 1) if up_sample else nn.Identity()
+
+    def forward(self, x, out_down=None, t_emb=None):
+        x = LF.call(self.up_sample_conv, x)
+        if out_down is not None:
+            x = torch.cat([x, out_down], dim=1)
+        out = x
+        for i in range(self.num_layers):
+            out = _resnet(self, i, out, t_emb)
+            if self.attn:
+                out = _attend(self.attention_norms[i], self.attentions[i], out)
+        return out
 
 
 class UpBlockUnet(_ParamBlock):
@@ -114,3 +175,15 @@ class UpBlockUnet(_ParamBlock):
         _add_residual(self, num_layers, in_channels, out_channels)
         self.up_sample_conv = (nn.ConvTranspose2d(in_channels // 2, in_channels // 2, 4, 2, 1) if up_sample
                                else nn.Identity())
+
+    def forward(self, x, out_down=None, t_emb=None, context=None):
+        x = LF.call(self.up_sample_conv, x)
+        if out_down is not None:
+            x = torch.cat([x, out_down], dim=1)
+        out = x
+        for i in range(self.num_layers):
+            out = _resnet(self, i, out, t_emb)
+            out = _attend(self.attention_norms[i], self.attentions[i], out)
+            if self.cross_attn:
+                out = _cross(self, i, out, x, context)
+        return out

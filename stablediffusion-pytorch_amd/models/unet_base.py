@@ -5,6 +5,7 @@ t_proj before conv_in, unet_base.py:33-39); compute runs in sdmi.unet_engine."""
 import torch.nn as nn
 
 from models.blocks import DownBlock, MidBlock, UpBlockUnet, get_time_embedding  # noqa: F401
+from sdmi import leaf as LF
 from sdmi.module_glue import EngineHolder, run_unet
 
 
@@ -48,4 +49,10 @@ class Unet(nn.Module):
         self._sdmi = EngineHolder(self, cfg, "uncond")
 
     def forward(self, x, t):
+        if getattr(self, "sdmi_leaf_path", False) or not LF.engine_ok(self, (Unet, DownBlock, MidBlock, UpBlockUnet)):
+            # a swapped leaf: unet_base.py:68-100 leaf by leaf
+            from models.unet_cond_base import _leaf_body
+            out = LF.call(self.conv_in, x)
+            t_emb = LF.call(self.t_proj, LF.time_embedding(t, x.shape[0], self.t_emb_dim, x.device))
+            return _leaf_body(self, out, t_emb, None)
         return run_unet(self, self._sdmi, x, t)

@@ -4,7 +4,9 @@ Same constructor, forward signature, assertions and state-dict keys as the refer
 as train_ddpm_cond_celebhq_multi_gpu.py:235-238 and tools/sample_ddpm_text_image_cond.py construct
 `Unet(im_channels, model_config)` and call `model(x, t, cond_input)` unchanged. The forward and
 backward run as one explicit schedule of gfx950 kernels (sdmi.unet_engine); parameters live in a
-flat fp32 store the first time the model runs on the GPU.
+flat fp32 store the first time the model runs on the GPU. Once a leaf is no longer an exact torch type (a
+swapped quantised layer) -- or with `sdmi_leaf_path = True` -- the forward composes the blocks
+and leaves like the reference (unet_cond_base.py:124-183) on the per-op HIP path of sdmi.leaf instead.
 """
 import torch
 import torch.nn as nn
@@ -12,6 +14,7 @@ import torch.nn as nn
 from models.blocks import DownBlock, MidBlock, UpBlockUnet, get_time_embedding  # noqa: F401
 from utils.config_utils import (get_config_value, validate_class_config, validate_text_config,
                                 validate_image_conditional_input, validate_class_conditional_input)
+from sdmi import leaf as LF
 from sdmi.module_glue import EngineHolder, run_unet
 
 
@@ -97,4 +100,36 @@ class Unet(nn.Module):
             assert "text" in cond_input, \
                 "Model initialized with text conditioning but cond_input has no text information"
             text = cond_input["text"]
+        if getattr(self, "sdmi_leaf_path", False) or not LF.engine_ok(self, (Unet, DownBlock, MidBlock, UpBlockUnet)):
+            return self._leaf_forward(x, t, text, mask, klass)
         return run_unet(self, self._sdmi, x, t, text, mask, klass)
+
+    def _leaf_forward(self, x, t, text, mask, klass):
+        """unet_cond_base.py:131-183, leaf by leaf (sdmi.leaf.call)."""
+        if self.image_cond:
+            im_cond = torch.nn.functional.interpolate(mask.float(), size=x.shape[-2:])
+            im_cond = LF.call(self.cond_conv_in, im_cond)
+            assert im_cond.shape[-2:] == x.shape[-2:]
+            out = LF.call(self.conv_in_concat, torch.cat([x, im_cond], dim=1))
+        else:
+            out = LF.call(self.conv_in, x)
+        t_emb = LF.call(self.t_proj, LF.time_embedding(t, x.shape[0], self.t_emb_dim, x.device))
+        if self.class_cond:
+            t_emb = t_emb + LF.class_embed(self.class_emb, klass)
+        return _leaf_body(self, out, t_emb, text)
+
+
+def _leaf_body(self, out, t_emb, context):
+    down_outs = []
+    for down in self.downs:
+        down_outs.append(out)
+        out = down(out, t_emb, context)
+    for mid in self.mids:
+        out = mid(out, t_emb, context)
+    for up in self.ups:
+        out = up(out, down_outs.pop(), t_emb, context)
+    if type(self.norm_out) is torch.nn.GroupNorm:
+        out = LF.group_norm(self.norm_out, out, silu=True)
+    else:
+        out = LF.call(torch.nn.SiLU(), self.norm_out(out))
+    return LF.call(self.conv_out, out)

@@ -17,6 +17,7 @@ import torch.nn as nn
 
 from models.blocks import DownBlock, MidBlock, UpBlock
 from sdmi import _lib
+from sdmi import leaf as LF
 from sdmi.vqvae_engine import VQVAEEngine
 from sdmi.vqvae_train import VQVAETrainEngine
 
@@ -140,21 +141,59 @@ class VQVAE(nn.Module):
                 "z_channels": self.z_channels, "codebook_size": self.codebook_size,
                 "norm_channels": self.norm_channels, "num_heads": self.num_heads}
 
+    def _leaf(self):
+        """Leaf-by-leaf path (sdmi.leaf): a swapped leaf or sdmi_leaf_path = True."""
+        return getattr(self, "sdmi_leaf_path", False) or not LF.engine_ok(self, (VQVAE, DownBlock, MidBlock, UpBlock))
+
+    def quantize(self, x):
+        """vqvae.py:93-126 on its own (pre-quantisation latent -> z_q, losses, indices)."""
+        return LF.quantize(self.embedding, x)
+
+    def _leaf_encode(self, x):
+        out = LF.call(self.encoder_conv_in, x)
+        for down in self.encoder_layers:
+            out = down(out)
+        for mid in self.encoder_mids:
+            out = mid(out)
+        out = LF.call(nn.Sequential(self.encoder_norm_out, nn.SiLU()), out)
+        out = LF.call(self.pre_quant_conv, LF.call(self.encoder_conv_out, out))
+        return self.quantize(out)
+
+    def _leaf_decode(self, z):
+        out = LF.call(self.decoder_conv_in, LF.call(self.post_quant_conv, z))
+        for mid in self.decoder_mids:
+            out = mid(out)
+        for up in self.decoder_layers:
+            out = up(out)
+        out = LF.call(nn.Sequential(self.decoder_norm_out, nn.SiLU()), out)
+        return LF.call(self.decoder_conv_out, out)
+
     @torch.no_grad()
     def quantize_indices(self, x):
         """Encode and also return the codebook indices (B, h, w) int64 (vqvae.py:124-125)."""
+        if self._leaf():
+            zq, losses, idx = self._leaf_encode(x)
+            return zq, losses["codebook_loss"].reshape(1), idx
         return self._eng(x).encode(x)
 
-    @torch.no_grad()
     def encode(self, x):
-        zq, loss, _ = self._eng(x).encode(x)
+        if self._leaf():
+            zq, losses, _ = self._leaf_encode(x)
+            return zq, losses
+        with torch.no_grad():
+            zq, loss, _ = self._eng(x).encode(x)
         return zq, {"codebook_loss": loss[0], "commitment_loss": loss[0]}
 
-    @torch.no_grad()
     def decode(self, z):
-        return self._eng(z).decode(z)
+        if self._leaf():
+            return self._leaf_decode(z)
+        with torch.no_grad():
+            return self._eng(z).decode(z)
 
     def forward(self, x):
+        if self._leaf():
+            z, losses, _ = self._leaf_encode(x)
+            return self._leaf_decode(z), z, losses
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             out, z, cb, cm = VQVAEFunction.apply(self, x, *self.parameters())
             return out, z, {"codebook_loss": cb, "commitment_loss": cm}
