@@ -187,6 +187,8 @@ int sdmi_mse(const float* pred, int ld, const float* target, int B, int C, int H
 int sdmi_time_embedding(const long long* t, int tstride, int B, int dim, void* out, int ld, float* out_f32,
                         sdmi_stream_t stream);
 int sdmi_silu(const void* x, const void* dy, void* y, long long n, sdmi_stream_t stream);
+/* fp32 ReLU (dy NULL) or its backward dx = dy * (x > 0) (the leaf path's nn.ReLU, transformer.py:72,80) */
+int sdmi_relu(const float* x, const float* dy, float* y, long long n, sdmi_stream_t stream);
 int sdmi_copy_slice(const void* src, int lds, void* dst, int ldd, long long P, int C, int accumulate,
                     sdmi_stream_t stream);
 

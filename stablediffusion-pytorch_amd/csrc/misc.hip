@@ -239,6 +239,14 @@ __global__ void silu_kernel(const bf16_t* x, const bf16_t* dy, bf16_t* y, long l
   }
 }
 
+// ReLU on fp32 (the leaf path's nn.ReLU, transformer.py:72,80): y = max(x, 0); with dy: dx = dy where x > 0
+__global__ void relu_kernel(const float* x, const float* dy, float* y, long long n) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const float v = x[i];
+    y[i] = dy ? (v > 0.f ? dy[i] : 0.f) : (v > 0.f ? v : 0.f);
+  }
+}
+
 // dst[p][0:C] (+)= src[p][0:C]  (bf16 NHWC channel slices, C % 8 == 0)
 __global__ void copy_slice_kernel(const bf16_t* src, int lds, bf16_t* dst, int ldd, long long P, int C, int accumulate) {
   int C8 = C >> 3;
@@ -445,6 +453,14 @@ extern "C" int sdmi_time_embedding(const long long* t, int tstride, int B, int d
 extern "C" int sdmi_silu(const void* x, const void* dy, void* y, long long n, sdmi_stream_t stream) {
   sdmi_rt::launch(silu_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, (const bf16_t*)x,
                      (const bf16_t*)dy, (bf16_t*)y, n);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_relu(const float* x, const float* dy, float* y, long long n, sdmi_stream_t stream) {
+  if (!x || !y || n < 0) return -1;
+  if (n == 0) return 0;
+  sdmi_rt::launch(relu_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, x, dy, y, n);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

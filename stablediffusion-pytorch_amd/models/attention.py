@@ -2,9 +2,13 @@
 
 Parameter holder with the reference's attribute names, shapes and initialisation (qkv_proj packed as
 (3 * heads * head_dim, hidden), output_proj = Sequential(Linear)); the compute (one QKV GEMM, the fused
-flash-attention kernel with the d^-0.5 scale, the output GEMM) runs inside sdmi.dit_engine for the whole DIT.
+flash-attention kernel with the d^-0.5 scale, the output GEMM) runs inside sdmi.dit_engine for the whole DIT;
+called on its own (or inside a DIT with a swapped leaf) it composes its leaves like attention.py:33-78 on the
+HIP per-op path (sdmi.leaf).
 """
 import torch.nn as nn
+
+from sdmi import leaf as LF
 
 
 class Attention(nn.Module):
@@ -22,4 +26,5 @@ class Attention(nn.Module):
         nn.init.constant_(self.output_proj[0].bias, 0)
 
     def forward(self, x):
-        raise NotImplementedError("Attention is a parameter holder; run the whole DIT (HIP engine)")
+        q, k, v = LF.call(self.qkv_proj, x).split(self.att_dim, dim=-1)
+        return LF.call(self.output_proj, LF.attention_core(q, k, v, self.n_heads))

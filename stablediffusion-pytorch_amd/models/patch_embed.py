@@ -2,9 +2,12 @@
 
 get_patch_position_embedding is the reference's 2-D sin/cos table (patch_embed.py:5-34) as a host-side
 API; PatchEmbedding (:37-96) holds the patch Linear with the reference's initialisation. Inside the DIT
-the patchify + Linear + position add is ONE implicit-GEMM launch (sdmi.dit_engine)."""
+the patchify + Linear + position add is ONE implicit-GEMM launch (sdmi.dit_engine); on its own it runs
+patch_embed.py:75-96 with the Linear on the HIP leaf path (sdmi.leaf)."""
 import torch
 import torch.nn as nn
+
+from sdmi import leaf as LF
 
 
 def get_patch_position_embedding(pos_emb_dim, grid_size, device):
@@ -34,4 +37,12 @@ class PatchEmbedding(nn.Module):
         nn.init.constant_(self.patch_embed[0].bias, 0)
 
     def forward(self, x):
-        raise NotImplementedError("PatchEmbedding is a parameter holder; run the whole DIT (HIP engine)")
+        B, C, H, W = x.shape
+        ph, pw = self.patch_height, self.patch_width
+        assert H % ph == 0, "Input height must be divisible by patch height"
+        assert W % pw == 0, "Input width must be divisible by patch width"
+        nh, nw = H // ph, W // pw
+        # 'b c (nh ph) (nw pw) -> b (nh nw) (ph pw c)'
+        tok = x.reshape(B, C, nh, ph, nw, pw).permute(0, 2, 4, 3, 5, 1).reshape(B, nh * nw, ph * pw * C)
+        out = LF.call(self.patch_embed, tok)
+        return out + get_patch_position_embedding(self.hidden_size, (nh, nw), x.device).to(out.dtype)

@@ -4,7 +4,8 @@ Same constructor, forward signature, assertions, initialisation and state-dict k
 callers such as Model_DiT_12L_train.py:478-481 construct `DIT(im_channels, model_config)` and call
 `model(x, t, cond_input)` unchanged. The whole forward and backward run as one explicit schedule of
 gfx950 kernels (sdmi.dit_engine); parameters live in a flat fp32 store the first time the model runs on
-the GPU. There is no CPU path: CPU inputs raise.
+the GPU. There is no CPU path: CPU inputs raise. With a swapped leaf or sdmi_leaf_path = True
+the forward composes the layers like transformer.py:153-213, every leaf on the HIP per-op path (sdmi.leaf).
 """
 import torch
 import torch.nn as nn
@@ -13,6 +14,7 @@ from models.patch_embed import PatchEmbedding
 from models.transformer_layer import TransformerLayer
 from utils.config_utils import (get_config_value, validate_class_config, validate_class_conditional_input,
                                 validate_image_config, validate_image_conditional_input, validate_text_config)
+from sdmi import leaf as LF
 from sdmi.module_glue import EngineHolder, run_denoiser
 
 
@@ -101,4 +103,31 @@ class DIT(nn.Module):
             assert "text" in cond_input, \
                 "Model initialized with text conditioning but cond_input has no text information"
             text = cond_input["text"]
+        from models.attention import Attention
+        from models.multihead_attention import CustomMultiheadAttention
+        if getattr(self, "sdmi_leaf_path", False) or not LF.engine_ok(
+                self, (DIT, PatchEmbedding, TransformerLayer, Attention, CustomMultiheadAttention)):
+            return self._leaf_forward(x, t, text, mask, klass)
         return run_denoiser(self, self._sdmi, x, t, text, mask, klass)
+
+    def _leaf_forward(self, x, t, text, mask, klass):
+        patch_source = x
+        if self.image_cond:
+            im_cond = torch.nn.functional.interpolate(mask.to(device=x.device, dtype=x.dtype), size=x.shape[-2:])
+            patch_source = torch.cat([patch_source, LF.call(self.cond_conv_in, im_cond)], dim=1)
+        out = self.patch_embed_layer(patch_source)
+        t_emb = LF.time_embedding(t, x.shape[0], self.timestep_emb_dim, x.device)
+        if self.class_cond:
+            t_emb = t_emb + LF.class_embed(self.class_emb, klass)
+        t_emb = LF.call(self.t_proj, t_emb)
+        for layer in self.transformer_layers:
+            out = layer(out, t_emb, text)
+        shift, scale = LF.call(self.adaptive_norm_layer, t_emb).chunk(2, dim=1)
+        out = LF.call(self.norm, out) * (1 + scale.unsqueeze(1)) + shift.unsqueeze(1)
+        out = LF.call(self.proj_out, out)
+        B, _, H, W = x.shape
+        ph, pw = self.patch_height, self.patch_width
+        nh, nw = H // ph, W // pw
+        # 'b (nh nw) (ph pw c) -> b c (nh ph) (nw pw)'
+        return out.reshape(B, nh, nw, ph, pw, self.im_channels).permute(0, 5, 1, 3, 2, 4).reshape(
+            B, self.im_channels, H, W)

@@ -4,8 +4,11 @@ Parameter holder with the reference's attribute names (att_norm / ff_norm / cros
 affine-free LayerNorms, attn_block, mlp_block = Linear-ReLU-Linear, optional cross_attn_block +
 context_proj, adaptive_norm_layer = ReLU-Linear(6*hidden)) and initialisation (xavier MLP, zero
 adaLN). The forward of every layer runs inside sdmi.dit_engine: LayerNorm + adaLN modulation and the
-gated residual adds are fused row kernels, the Linears are MFMA GEMMs, attention is the flash kernel."""
+gated residual adds are fused row kernels, the Linears are MFMA GEMMs, attention is the flash kernel.
+Called on its own (or in a DIT with a swapped leaf) it runs transformer_layer.py:80-106 leaf by leaf (sdmi.leaf)."""
 import torch.nn as nn
+
+from sdmi import leaf as LF
 
 from models.attention import Attention
 from models.multihead_attention import CustomMultiheadAttention
@@ -40,4 +43,14 @@ class TransformerLayer(nn.Module):
             nn.init.constant_(self.context_proj.bias, 0)
 
     def forward(self, x, condition, context=None):
-        raise NotImplementedError("TransformerLayer is a parameter holder; run the whole DIT (HIP engine)")
+        (pre_attn_shift, pre_attn_scale, post_attn_scale, pre_mlp_shift, pre_mlp_scale,
+         post_mlp_scale) = LF.call(self.adaptive_norm_layer, condition).chunk(6, dim=1)
+        out = x
+        h = LF.call(self.att_norm, out) * (1 + pre_attn_scale.unsqueeze(1)) + pre_attn_shift.unsqueeze(1)
+        out = out + post_attn_scale.unsqueeze(1) * self.attn_block(h)
+        if self.cross_attn and context is not None:
+            ctx = LF.call(self.context_proj, context)
+            o, _ = self.cross_attn_block(LF.call(self.cross_attn_norm, out), ctx, ctx, need_weights=False)
+            out = out + o
+        h = LF.call(self.ff_norm, out) * (1 + pre_mlp_scale.unsqueeze(1)) + pre_mlp_shift.unsqueeze(1)
+        return out + post_mlp_scale.unsqueeze(1) * LF.call(self.mlp_block, h)

@@ -238,9 +238,14 @@ class _Linear(torch.autograd.Function):
         Kp, Np = _r8(Kd), _r8(N)
         pk = _pack_linear(ctx.mod, ctx.weight)
         dyb = _rows(dy.reshape(M, N), Np)
-        dw = torch.empty_like(ctx.weight)
         db = torch.empty(N, dtype=torch.float32, device=dy.device) if ctx.has_bias else None
-        K.linear_wgrad(dyb[:, :N], ctx.xb[:, :Kd], dw, bias_grad=db)
+        if Kd == Kp:
+            dw = torch.empty_like(ctx.weight)
+            K.linear_wgrad(dyb, ctx.xb, dw, bias_grad=db, m_store=N)
+        else:  # the GEMM's row / column counts are multiples of 8: a padded gradient, then its first Kd columns
+            dwp = torch.empty(N, Kp, dtype=torch.float32, device=dy.device)
+            K.linear_wgrad(dyb, ctx.xb, dwp, bias_grad=db, m_store=N)
+            dw = _unrows(dwp, Kp, N, Kd)
         dx = None
         if ctx.needs_input_grad[1]:
             dxf = torch.empty(M, Kp, dtype=torch.float32, device=dy.device)
@@ -303,6 +308,93 @@ class _SiLU(torch.autograd.Function):
         _lib.check(_lib.lib().sdmi_silu(ctx.xb.data_ptr(), dyb.data_ptr(), dx.data_ptr(), n, K._stream()), "silu")
         ctx.xb = None
         return _unrows(dx, 1, n, 1).reshape(ctx.shape)
+
+
+# ---- ReLU (fp32) --------------------------------------------------------------------------------------------------
+class _ReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.float().contiguous()
+        y = torch.empty_like(x)
+        _lib.check(_lib.lib().sdmi_relu(x.data_ptr(), None, y.data_ptr(), x.numel(), K._stream()), "sdmi_relu")
+        ctx.x = x
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.float().contiguous()
+        dx = torch.empty_like(dy)
+        _lib.check(_lib.lib().sdmi_relu(ctx.x.data_ptr(), dy.data_ptr(), dx.data_ptr(), dy.numel(), K._stream()),
+                   "sdmi_relu")
+        ctx.x = None
+        return dx
+
+
+# ---- LayerNorm without affine (the DiT's norms, transformer_layer.py:21-28) ---------------------------------------
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, eps):
+        C = x.shape[-1]
+        x2 = x.float().contiguous().reshape(-1, C)
+        rows = x2.shape[0]
+        N = x.shape[-2] if x.dim() >= 3 else rows  # rows per sample
+        y = torch.empty(rows, C, dtype=torch.bfloat16, device=x.device)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        _lib.check(_lib.lib().sdmi_ln_mod_fwd(x2.data_ptr(), C, None, 0, None, None, 0, None, None, 0, y.data_ptr(), C,
+                                              mean.data_ptr(), rstd.data_ptr(), rows, C, N, eps, 1, K._stream()),
+                   "sdmi_ln_mod_fwd")
+        ctx.save = (x2, mean, rstd, rows, C, N, x.shape)
+        return _unrows(y, C, rows, C).reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, mean, rstd, rows, C, N, shape = ctx.save
+        dyb = _rows(dy.reshape(rows, C), C)
+        dx = torch.empty(rows, C, dtype=torch.float32, device=dy.device)
+        _lib.check(_lib.lib().sdmi_ln_mod_bwd(x2.data_ptr(), C, mean.data_ptr(), rstd.data_ptr(), dyb.data_ptr(), C,
+                                              None, 0, None, 0, dx.data_ptr(), C, None, None, 0, None, None, 0, None,
+                                              0, None, rows, C, N, 1, None, 0, K._stream()), "sdmi_ln_mod_bwd")
+        ctx.save = None
+        return dx.reshape(shape), None
+
+
+def layer_norm(mod, x):
+    C = x.shape[-1]
+    if mod.elementwise_affine or tuple(mod.normalized_shape) != (C,) or C % 8 or C > 512:
+        raise NotImplementedError(f"HIP leaf LayerNorm: unsupported {mod}")
+    return _LayerNorm.apply(x, mod.eps)
+
+
+# ---- attention core: softmax(q k^T / sqrt(d)) v over heads (attention.py:41-73, multihead_attention.py:56-67) -----
+class _AttnCore(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, heads):
+        B, N, E = q.shape
+        S = k.shape[1]
+        d = E // heads
+        qb, kb, vb = (_rows(t.reshape(-1, E), E) for t in (q, k, v))
+        o = torch.empty(B * N, E, dtype=torch.bfloat16, device=q.device)
+        lse = K.attn_fwd(qb, kb, vb, o, B, heads, N, S, d)
+        ctx.save = (qb, kb, vb, o, lse, (B, N, S, E, heads, d))
+        return _unrows(o, E, B * N, E).reshape(B, N, E)
+
+    @staticmethod
+    def backward(ctx, dy):
+        qb, kb, vb, o, lse, (B, N, S, E, H, d) = ctx.save
+        dyb = _rows(dy.reshape(B * N, E), E)
+        dq, dk, dv = (torch.empty(n, E, dtype=torch.bfloat16, device=dy.device) for n in (B * N, B * S, B * S))
+        K.attn_bwd(qb, kb, vb, o, dyb, lse, dq, dk, dv, B, H, N, S, d)
+        ctx.save = None
+        return (_unrows(dq, E, B * N, E).reshape(B, N, E), _unrows(dk, E, B * S, E).reshape(B, S, E),
+                _unrows(dv, E, B * S, E).reshape(B, S, E), None)
+
+
+def attention_core(q, k, v, heads):
+    E = q.shape[-1]
+    if E % heads or (E // heads) % 8 or E // heads > 64 or E % 8:
+        raise NotImplementedError("HIP attention: head_dim must be a multiple of 8 and <= 64")
+    return _AttnCore.apply(q.contiguous(), k.contiguous(), v.contiguous(), heads)
 
 
 # ---- nn.MultiheadAttention (batch_first, packed in-projection) ----------------------------------------------------
@@ -502,7 +594,11 @@ def call(mod, x, *rest):
         return group_norm(mod, x)
     if t is nn.SiLU:
         return _SiLU.apply(x)
-    if t is nn.Identity:
+    if t is nn.ReLU:
+        return _ReLU.apply(x)
+    if t is nn.LayerNorm:
+        return layer_norm(mod, x)
+    if t is nn.Identity or (t is nn.Dropout and not mod.training):
         return x
     if t is nn.MultiheadAttention:
         return multihead_attention(mod, x, *rest)

@@ -220,3 +220,43 @@ def test_vqvae_with_swapped_layers_vs_reference():
     for k, p in model.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all(), k
     assert model.encoder_conv_in.weight.grad.norm() > 0 and model.embedding.weight.grad.norm() > 0
+
+
+@pytest.mark.parametrize("swap", [False, True])
+def test_dit_leaf_path_vs_oracle(swap):
+    """The DIT forced onto the leaf path (sdmi_leaf_path) or with its nn.Linear / nn.Conv2d leaves swapped:
+    TransformerLayer / Attention / CustomMultiheadAttention / PatchEmbedding forwards (transformer_layer.py:80-106,
+    attention.py:33-78, multihead_attention.py:41-80, patch_embed.py:75-96) against the oracle and the reference
+    fixture (text + image conditioning)."""
+    from models.transformer import DIT
+    from oracle import dit_oracle as DO
+    from tests.golden.configs import SMALL_DIT
+    f = load_file(os.path.join(G, "dit_small.safetensors"))
+    sd = O.deterministic_state(DO.dit_param_shapes(SMALL_DIT), 4)
+    model = DIT(4, SMALL_DIT).cuda()
+    model.load_state_dict(sd)
+    if swap:
+        assert _swap_like_cim(model) > 10
+    else:
+        model.sdmi_leaf_path = True
+    c = {"text": f["text"], "image": F.one_hot(f["classmap"].long(), 19).movedim(-1, 1)[:, 1:].float()}
+    _SwappedLinear.calls = 0
+    out = model(f["x"].cuda(), f["t"].cuda(), {k: v.cuda() for k, v in c.items()})
+    assert (_SwappedLinear.calls > 0) == swap
+    leaves = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    ref = DO.dit_forward(leaves, SMALL_DIT, f["x"], f["t"], c)
+    assert ((out.detach().cpu() - ref.detach()) ** 2).mean().item() <= 1e-4
+    assert ((out.detach().cpu() - f["out"]) ** 2).mean().item() <= 1e-4
+    F.mse_loss(out, f["noise"].cuda()).backward()
+    F.mse_loss(ref, f["noise"]).backward()
+    worst = min((cos(p.grad, leaves[k].grad), k) for k, p in model.named_parameters()
+                if leaves[k].grad is not None and leaves[k].grad.norm() > 1e-6)
+    assert worst[0] >= 0.99, worst
+
+
+def test_linear_leaf_ragged_features():
+    """Linear with in / out features that are not multiples of 8 (the DiT patch embedding: 2*2*(4+3) = 28)."""
+    from sdmi import leaf as LF
+    torch.manual_seed(8)
+    lin = nn.Linear(28, 13).cuda()
+    _check(lin, [torch.randn(2, 9, 28)], lambda a: LF.linear(lin, a), lambda a: F.linear(a, lin.weight, lin.bias))
