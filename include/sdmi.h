@@ -105,6 +105,10 @@ typedef struct sdmi_gemm_desc {
   void* gsum_out;
   int gsum_ld;
   int sum_group;
+  /* mainloop request (0 = built-in choice): 1 register-staged operands, 2 / 3 LDS-DMA ring of that many stages.
+   * Ignored where the mode does not support it (the reduction columns need register staging). Used with the
+   * measured per-shape table of sdmi/tuned_gemm.json. */
+  int variant_hint;
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */

@@ -19,6 +19,9 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
+SPLITS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, 24, 32, 40, 48, 64, 96, 128)
+
+
 def time_launch(L, d, ws, stream, iters=10, rounds=3):
     import ctypes
     res = []
@@ -69,7 +72,9 @@ def main():
     step = lambda: tr.step(x0, noise, t, text, mask, mask_keep=keep)  # noqa: E731
     for _ in range(2):
         step()
-    plan = StepPlan(step, dev)
+    K.GEMM_CAPTURE = []
+    plan = StepPlan(step, dev)  # its private pool keeps every captured operand pointer valid
+    descs, K.GEMM_CAPTURE = K.GEMM_CAPTURE, None
     L = _lib.lib()
     ws = torch.empty(1 << 28, dtype=torch.float32, device=dev)  # 1 GiB split-K slabs
     stream = torch.cuda.current_stream().cuda_stream
@@ -78,10 +83,7 @@ def main():
         table = json.load(open(args.out))
     seen = {}
     tot_def = tot_best = 0.0
-    for fn, a in plan.ops:
-        if getattr(fn, "__name__", "") != "sdmi_gemm":
-            continue
-        d = a[0]._obj
+    for d in descs:
         key = K.gemm_key(d)
         nkt = (d.k + 63) // 64
         if key in seen:
@@ -89,17 +91,22 @@ def main():
             seen[key] = (n + 1, td, tb)
             continue
         d.splits_hint = 0
+        d.variant_hint = 0
         t_def = time_launch(L, d, ws, stream)
         best, t_best = 0, t_def
-        s = 1
-        while s <= min(128, nkt):
-            if s * d.m * d.n * 4 < min(ws.numel() * 4, 1 << 31):
-                d.splits_hint = s
+        # mainloops: register staging (1) and the LDS-DMA rings (2, 3 stages); the library ignores a request the
+        # mode cannot take (reduction columns are register-staged only), so those shapes time variant 1 only
+        variants = (1, 2, 3)
+        for v in variants:
+            for s in SPLITS:
+                if s > nkt or s * d.m * d.n * 4 >= min(ws.numel() * 4, 1 << 31):
+                    continue
+                d.splits_hint, d.variant_hint = s, v
                 ts = time_launch(L, d, ws, stream)
                 if ts < t_best * 0.97:
-                    best, t_best = s, ts
-            s *= 2
+                    best, t_best = [s, v], ts
         d.splits_hint = 0
+        d.variant_hint = 0
         seen[key] = (1, t_def, t_best)
         if best:
             table[key] = best

@@ -713,6 +713,39 @@ __device__ __forceinline__ s16x8 frag_tr(const char* tile, int cbase, int ks, in
   return r;
 }
 
+// Transposed fragment read for the LDS-DMA kernels, as inline asm. hipcc (ROCm 7.2) cannot prove a
+// ds_read_b64_tr_b16 builtin disjoint from the LDS-DMA writes in flight and emits s_waitcnt vmcnt(0) before it --
+// which drains the prefetch of the NEXT k-tile issued just before (measured: every DMA kernel with an MN-contiguous
+// operand ran fully serialised). The asm reads are invisible to hipcc's lgkmcnt bookkeeping, so the caller waits
+// for them explicitly (lds_wait_frags) before the MFMAs that consume them.
+__device__ __forceinline__ s16x4 ds_tr_asm(const char* p) {
+  s16x4 r;
+  const unsigned a = (unsigned)(uintptr_t)(SDMI_LDS const char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+
+__device__ __forceinline__ s16x8 frag_tr_asm(const char* tile, int cbase, int ks, int lane) {
+  int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  int r1 = ks * 32 + gq * 8 + q;
+  int c = (cbase >> 3) + (p >> 1);
+  s16x4 lo = ds_tr_asm(tile + tr_off(r1, c) + (p & 1) * 8);
+  s16x4 hi = ds_tr_asm(tile + tr_off(r1 + 4, c) + (p & 1) * 8);
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// all LDS reads issued so far have landed; the fragments are re-defined after the wait so no consumer (an MFMA is
+// register-only and would otherwise be hoisted above an asm wait) reads them earlier
+template <int N>
+__device__ __forceinline__ void lds_wait_frags(s16x8 (&f)[N]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(f[i]));
+}
+
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_base, int off) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (SDMI_LDS void*)lds_wave_base, 16, off, 0, 0, 0);
 }
@@ -919,10 +952,12 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
         s16x8 fa[4], fb[NJ];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          fa[i] = (AM == SDMI_A_COLMAJOR) ? frag_tr(ta, wm + 16 * i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
+          fa[i] = (AM == SDMI_A_COLMAJOR) ? frag_tr_asm(ta, wm + 16 * i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          fb[j] = (BMODE == SDMI_B_NK) ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_tr(tb, wn + 16 * j, ks, lane);
+          fb[j] = (BMODE == SDMI_B_NK) ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_tr_asm(tb, wn + 16 * j, ks, lane);
+        if constexpr (AM == SDMI_A_COLMAJOR) lds_wait_frags(fa);
+        if constexpr (BMODE != SDMI_B_NK) lds_wait_frags(fb);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1060,6 +1095,7 @@ int gemm_variant() {
 
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 3) v = d->variant_hint == 1 ? 0 : d->variant_hint;
   if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
   if (has_reductions(d)) v = 0;  // reduction columns are synthesised in the register-staged loader
   // the DMA path needs a tile-uniform second source (k_split % BK == 0)

@@ -44,6 +44,7 @@ class GemmDesc(ctypes.Structure):
         ("tile_n_hint", ctypes.c_int),
         ("sum_out", ctypes.c_void_p), ("sum_out2", ctypes.c_void_p), ("gsum_out", ctypes.c_void_p),
         ("gsum_ld", ctypes.c_int), ("sum_group", ctypes.c_int),
+        ("variant_hint", ctypes.c_int),
     ]
 
 

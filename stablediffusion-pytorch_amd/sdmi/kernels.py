@@ -26,13 +26,17 @@ def _stream():
 PROFILE = None
 # optional GEMM call log (scripts/plan_profile.py): list of (m, n, k, a_mode, b_mode, splits, tile_n, phase, kernel info)
 GEMM_LOG = None
+# optional descriptor capture (scripts/tune_gemm.py): copies of every GemmDesc issued while set (operands stay valid as
+# long as the memory they point into does, e.g. a StepPlan's private pool)
+GEMM_CAPTURE = None
 PHASE = ""  # label prefixed to profiled launches ("fwd" / "bwd" / "wg" ...; set by the engines)
 # phases whose GEMMs may take the 192-column tile (measured per phase: faster in fwd / bwd; in the weight-gradient
 # phase its 80 KiB of LDS per workgroup crowds out the concurrent streams and the step ran 0.4 ms slower)
 # elsewhere the 128-column tile is requested
 TILE192_PHASES = set(os.environ.get("SDMI_TILE192_PHASES", "fwd,bwd").split(","))
 
-# measured split-K slice counts per GEMM shape (scripts/tune_gemm.py -> sdmi/tuned_gemm.json); None = not loaded
+# measured split-K slice counts (or [splits, mainloop variant]) per GEMM shape (scripts/tune_gemm.py ->
+# sdmi/tuned_gemm.json); None = not loaded
 TUNED = None
 _TUNED_PATH = os.environ.get("SDMI_TUNED_GEMM") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gemm.json")
 
@@ -116,7 +120,13 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     d.tile_n_hint = 0 if (not PHASE or PHASE in TILE192_PHASES) else 128
     tuned = _tuned()
     if tuned:
-        d.splits_hint = tuned.get(gemm_key(d), 0)
+        e = tuned.get(gemm_key(d), 0)  # splits, or [splits, mainloop variant]
+        if isinstance(e, list):
+            d.splits_hint, d.variant_hint = e[0], e[1]
+        else:
+            d.splits_hint = e
+    if GEMM_CAPTURE is not None:
+        GEMM_CAPTURE.append(GemmDesc.from_buffer_copy(d))
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
