@@ -258,20 +258,21 @@ struct Epi {
   }
 };
 
-// Shared epilogue of the GEMM kernels: acc = this wave's 64x64 sub-tile (4x4 MFMA tiles), smem >= 34 KB
-// of LDS that no wave reads any more (the caller synchronises before).
-template <int TBN = BN, bool XCOL = false>
-__device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][TBN / 32], char* smem, int m0, int n0,
+// Shared epilogue of the GEMM kernels: acc = this wave's 64 x (NJ*16) sub-tile (4 x NJ MFMA tiles) at (wm, wn) of a
+// TBM x TBN workgroup tile computed by NT threads; smem >= 64 x (TBN + 4) fp32 of LDS that no wave reads any more (the
+// caller synchronises before).
+template <int TBN = BN, bool XCOL = false, int TBM = BM, int NJ = TBN / 32, int NTH = NT>
+__device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][NJ], char* smem, int m0, int n0,
                                               int wm, int wn, int lane, int z) {
-  constexpr int NJ = TBN / 32;  // 16-column MFMA tiles per wave
-  // Stage the fp32 tile through LDS in two 64-row halves; each thread then owns runs of 8 consecutive columns of one
+  // Stage the fp32 tile through LDS in 64-row parts; each thread then owns runs of 8 consecutive columns of one
   // row: 16-B stores (8 bf16 or 2 x 4 fp32) on the aligned paths, and a ROLLED per-element loop on the rare general
   // path (column permutes of weight gradients, unaligned outputs) instead of 4 x NJ x 4 unrolled scattered stores,
   // whose code and register footprint pushed the 192-column tile's accumulators to scratch.
-  float* st = (float*)smem;      // [64][SROW] fp32, 33 KB (TBN 128) / 49 KB (TBN 192)
+  float* st = (float*)smem;      // [64][SROW] fp32, 33 KB (TBN 128) / 49 KB (TBN 192) / 97 KB (TBN 384)
   constexpr int SROW = TBN + 4;  // +4 floats: lanes of one ds_write hit distinct banks
+  static_assert((64 * TBN / 8) % NTH == 0, "epilogue chunks per thread");
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int half = 0; half < TBM / 64; ++half) {
     if (wm == half * 64) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -284,8 +285,8 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
     }
     __syncthreads();
 #pragma unroll 1
-    for (int it = 0; it < TBN / 32; ++it) {  // 64 rows x TBN/8 chunks of 8 columns
-      const int ch = threadIdx.x + it * NT;
+    for (int it = 0; it < 64 * TBN / 8 / NTH; ++it) {  // 64 rows x TBN/8 chunks of 8 columns
+      const int ch = threadIdx.x + it * NTH;
       const int rl = ch / (TBN / 8), c8 = (ch - rl * (TBN / 8)) * 8;
       const int row = m0 + half * 64 + rl, col = n0 + c8;
       float v[8];
@@ -348,7 +349,7 @@ struct TileId {
   int m0, n0, z, tile;  // tile = logical (m, n) index within the split slice
 };
 
-template <int TBN = BN>
+template <int TBN = BN, int TBM = BM>
 __device__ __forceinline__ TileId tile_id() {
   const int gx = gridDim.x, per = gridDim.x * gridDim.y;
   const int total = per * gridDim.z;
@@ -359,7 +360,7 @@ __device__ __forceinline__ TileId tile_id() {
   t.z = l / per;
   t.tile = l - t.z * per;
   const int mt = t.tile / gx;
-  t.m0 = mt * BM;
+  t.m0 = mt * TBM;
   t.n0 = (t.tile - mt * gx) * TBN;
   return t;
 }
@@ -750,21 +751,51 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (SDMI_LDS void*)lds_wave_base, 16, off, 0, 0, 0);
 }
 
-// TBN = 192 (B_NK only): 128 x 192 tiles, each wave 64 x 96 -- 2 x 80 KiB of LDS still fits two workgroups per CU,
-// and N = 384 outputs split into 2 (not 3) column tiles, so a 32768 x 384 conv is exactly 512 tiles = one round
-template <int AM, int BMODE, int STAGES, int TBN = BN>
-__global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(const Args g, const EpiArgs e) {
-  static_assert(TBN == BN || ((TBN == 192 || TBN == 64) && BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR),
-                "64 / 192-column tiles: B_NK");
-  constexpr int NJ = TBN / 32;                       // 16-column MFMA tiles per wave
-  constexpr int B_BYTES = TBN * BK * 2;              // B tile bytes
-  constexpr int STAGE_BYTES = TILE_BYTES + B_BYTES;  // A | B
-  extern __shared__ __attribute__((aligned(16))) char smem[];  // STAGES x (A 16 KiB | B 16 / 24 KiB)
+// Tile shapes (TBM x TBN, NWN waves along N, TBM / 64 along M; every wave owns 64 x TBN/NWN):
+//   128 x {64, 128, 192}, 4 waves (2 x 2): the default family -- 2 x <= 80 KiB of LDS fits two workgroups per CU;
+//     N = 384 outputs split into 2 (not 3) 192-column tiles, so a 32768 x 384 conv is exactly 512 tiles = one round
+//   256 x {128, 192}, 8 waves (4 x 2), B_NK: the large-M convolutions / linears -- 1.5x the MFMA work per byte staged
+//   128 x {256, 384}, 8 waves (2 x 4), MN-contiguous B: weight gradients, whose N = 9 * cin is a multiple of 384
+// The MN-contiguous (ds_read_b64_tr_b16) LDS images are kept as 128-column sub-tiles [64 k][128] (256-B rows).
+// RED (col-major A only): reduction columns as extra MFMA tiles against synthesised B fragments (see reduce_frag).
+template <int TBM, int NWN>
+constexpr int dma_threads() { return 64 * (TBM / 64) * NWN; }
+
+// B fragment (8 k-values of one column, lane layout of mfma_f32_16x16x32_bf16: k = kb .. kb+7, column = lane & 15)
+// of reduction tile r: column 0 all ones (row sums: bias gradient), column 8 + j the indicator of group j = k / grp
+// (per-sample sums: time-embedding gradient; needs grp % 8 == 0 so 8 consecutive k share one group)
+template <int RED>
+__device__ __forceinline__ s16x8 reduce_frag(const Args& g, int r, int kb, int lane) {
+  const int col = r * 16 + (lane & 15);
+  bool one = col == 0;
+  if (RED == 2 && col >= 8) one = (int)g.grp_d.div((unsigned)kb) == col - 8;
+  const short v = one ? (short)0x3F80 : (short)0;
+  return (s16x8){v, v, v, v, v, v, v, v};
+}
+
+template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0>
+__global__ __launch_bounds__((dma_threads<TBM, NWN>()), ((dma_threads<TBM, NWN>() == 256 && STAGES == 2) ? 2 : 1))
+void gemm_dma_kernel(const Args g, const EpiArgs e) {
+  constexpr int NTH = dma_threads<TBM, NWN>();
+  constexpr int NW = NTH / 64;
+  constexpr int WTN = TBN / NWN;                     // columns per wave
+  constexpr int NJ = WTN / 16;                       // 16-column MFMA tiles per wave
+  constexpr bool A_MN = AM == SDMI_A_COLMAJOR, B_MN = BMODE != SDMI_B_NK;
+  constexpr int A_BYTES = TBM * BK * 2, B_BYTES = TBN * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;     // A | B
+  constexpr int A_PW = A_BYTES / 1024 / NW, B_PW = B_BYTES / 1024 / NW;  // DMA wave-instructions per tile
+  static_assert(A_PW * NW * 1024 == A_BYTES && B_PW * NW * 1024 == B_BYTES, "DMA pieces per wave");
+  static_assert(!A_MN || TBM % 128 == 0, "MN-contiguous A: 128-column sub-tiles");
+  static_assert(!B_MN || TBN % 128 == 0, "MN-contiguous B: 128-column sub-tiles");
+  static_assert(WTN % 16 == 0 && TBM % 64 == 0, "wave tile");
+  static_assert(RED == 0 || A_MN, "reductions: col-major A only");
+  constexpr int RPW = RED == 0 ? 0 : (RED == 1 ? 1 : (3 + NWN - 1) / NWN);  // reduction tiles per wave (<= 3 total)
+  extern __shared__ __attribute__((aligned(16))) char smem[];  // STAGES x (A | B)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (TBN / 2);
-  const TileId tl = tile_id<TBN>();
+  const int wm = (wave / NWN) * 64, wn = (wave % NWN) * WTN;
+  const TileId tl = tile_id<TBN, TBM>();
   const int m0 = tl.m0, n0 = tl.n0;
   const int z = tl.z;
   const int nkt_total = (g.K + BK - 1) / BK;
@@ -777,26 +808,28 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
   const __amdgpu_buffer_rsrc_t rsA2 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.A2 ? g.A2 : g.A), (short)0, 0x7fffffff, 0x00020000);
 
-  // ---- per-lane, per-instruction (j = 0..3) coordinates, fixed over the K loop ----
-  // K-contiguous image: instruction j of wave w fills rows (w*4+j)*8 .. +8, lane -> row +lane>>3, slot lane&7
-  // MN-contiguous image: fills k-rows (w*4+j)*4 .. +4, lane -> k-row +lane>>4, slot lane&15
-  int a_base[4], b_base[NJ];   // element offsets (without the k / pixel part)
-  int a_kk[4], b_kk[NJ];       // k offset inside the tile (KC: chunk*8) or k-row (MN)
-  bool a_ok[4], b_ok[NJ];
-  int a_iy[4], a_ix[4], a_pb[4], a_pix[4];
-  int b_ty[NJ], b_tx[NJ];
+  // ---- per-lane, per-instruction coordinates, fixed over the K loop ----
+  // instruction q = wave * PW + j writes 1 KiB at tile + q * 1024 (lane-linear):
+  //   K-contiguous image: rows q*8 .. +8, lane -> row + lane>>3, physical slot lane&7
+  //   MN-contiguous image: 128-column sub-tile q >> 4, k-rows (q & 15)*4 .. +4, lane -> k-row + lane>>4, slot lane&15
+  int a_base[A_PW], b_base[B_PW];  // element offsets (without the k / pixel part)
+  int a_kk[A_PW], b_kk[B_PW];      // k offset inside the tile (KC: chunk*8) or k-row (MN)
+  bool a_ok[A_PW], b_ok[B_PW];
+  int a_iy[A_PW], a_ix[A_PW], a_pb[A_PW], a_pix[A_PW];
+  int b_ty[B_PW], b_tx[B_PW];
   const bool cin64 = AM == SDMI_A_CONV && (g.cin & 63) == 0;  // k tile lies inside one tap
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (AM == SDMI_A_COLMAJOR) {
-      int kr = (wave * 4 + j) * 4 + (lane >> 4);
+  for (int j = 0; j < A_PW; ++j) {
+    const int q = wave * A_PW + j;
+    if (A_MN) {
+      int kr = (q & 15) * 4 + (lane >> 4);
       int c = (lane & 15) ^ tr_swz(kr);
-      int m = m0 + c * 8;
+      int m = m0 + (q >> 4) * 128 + c * 8;
       a_ok[j] = m < g.M;
       a_base[j] = m;
       a_kk[j] = kr;
     } else {
-      int r = (wave * 4 + j) * 8 + (lane >> 3);
+      int r = q * 8 + (lane >> 3);
       int c = (lane & 7) ^ (r & 7);
       int m = m0 + r;
       a_ok[j] = m < g.M;
@@ -815,18 +848,19 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
     }
   }
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    if (BMODE == SDMI_B_NK) {
-      int r = (wave * NJ + j) * 8 + (lane >> 3);
+  for (int j = 0; j < B_PW; ++j) {
+    const int q = wave * B_PW + j;
+    if (!B_MN) {
+      int r = q * 8 + (lane >> 3);
       int c = (lane & 7) ^ (r & 7);
       int n = n0 + r;
       b_ok[j] = n < g.N;
       b_base[j] = n * g.ldb;
       b_kk[j] = c * 8;
     } else {
-      int kr = (wave * 4 + j) * 4 + (lane >> 4);
+      int kr = (q & 15) * 4 + (lane >> 4);
       int c = (lane & 15) ^ tr_swz(kr);
-      int n = n0 + c * 8;
+      int n = n0 + (q >> 4) * 128 + c * 8;
       b_ok[j] = n < g.N;
       b_kk[j] = kr;
       b_base[j] = n;
@@ -851,25 +885,24 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
   }
   auto issue = [&](int kt, int stage) __attribute__((always_inline)) {
     char* sa = smem + stage * STAGE_BYTES;
-    char* sb = sa + TILE_BYTES;
+    char* sb = sa + A_BYTES;
     const int k0 = kt * BK;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      char* dst = sa + (wave * 4 + j) * 1024;
+    for (int j = 0; j < A_PW; ++j) {
+      char* dst = sa + (wave * A_PW + j) * 1024;
       int off;
       if (AM == SDMI_A_ROWMAJOR) {
         int k = k0 + a_kk[j];
         off = (a_ok[j] && k < g.K) ? (a_base[j] + k) * 2 : OOB;
-        dma16(rsA, dst, off);
-      } else if (AM == SDMI_A_COLMAJOR) {
+      } else if (A_MN) {
         int k = k0 + a_kk[j];
         off = (a_ok[j] && k < g.K) ? (k * g.lda + a_base[j]) * 2 : OOB;
-        dma16(rsA, dst, off);
       } else {
         int k = k0 + a_kk[j];
         if (k0 >= g.k_split) {  // fused 1x1 second source, tile-uniform (k_split % 64 == 0 on this path)
           off = (a_ok[j] && k < g.K) ? (a_base[j] + (k - g.k_split)) * 2 : OOB;
           dma16(rsA2, dst, off);
+          continue;
         } else if (cin64) {
           // tap, and with it the (ty, tx) shift, is uniform over the tile (tracked incrementally)
           const int ty = c_ty, tx = c_tx;
@@ -877,7 +910,6 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
           int iy = a_iy[j] + ty, ix = a_ix[j] + tx;
           bool ok = a_ok[j] && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
           off = ok ? (a_pix[j] + sh + a_kk[j]) * 2 : OOB;
-          dma16(rsA, dst, off);
         } else {
           int tap = k / g.cin;
           int ci = k - tap * g.cin;
@@ -885,9 +917,9 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
           int iy = a_iy[j] + ty, ix = a_ix[j] + tx;
           bool ok = a_ok[j] && k < g.k_split && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw;
           off = ok ? (((a_pb[j] + iy) * g.iw + ix) * g.ldx + ci) * 2 : OOB;
-          dma16(rsA, dst, off);
         }
       }
+      dma16(rsA, dst, off);
     }
     if (AM == SDMI_A_CONV && cin64 && k0 < g.k_split) {
       c_ci += BK;
@@ -900,8 +932,8 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
       }
     }
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      char* dst = sb + (wave * NJ + j) * 1024;
+    for (int j = 0; j < B_PW; ++j) {
+      char* dst = sb + (wave * B_PW + j) * 1024;
       int off;
       if (BMODE == SDMI_B_NK) {
         int k = k0 + b_kk[j];
@@ -926,6 +958,14 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // reduction tiles r = (wave % NWN) + rr * NWN of the tiles in column-tile 0 (workgroup-uniform)
+  const bool red_tile = RED != 0 && n0 == 0;
+  const int nred = RED == 0 ? 0 : (RED == 1 ? 1 : (8 + e.ngrp + 15) / 16);
+  f32x4 accr[RPW > 0 ? RPW : 1][4];
+#pragma unroll
+  for (int rr = 0; rr < (RPW > 0 ? RPW : 1); ++rr)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) accr[rr][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nt = kt1 - kt0;
   if (nt > 0) {
@@ -934,35 +974,48 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
     for (int s = 0; s < STAGES - 1; ++s)
       if (s < nt) issue(kt0 + s, s);
     for (int t = 0; t < nt; ++t) {
-      // tile t landed for this thread: at most (tiles issued after t) x (4 + NJ) DMA instructions outstanding
+      // tile t landed for this thread: at most (tiles issued after t) x (A_PW + B_PW) DMA instructions outstanding
       const int after = min(STAGES - 2, nt - 1 - t);
-      if (after >= 1) {
-        if constexpr (NJ == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if constexpr (NJ == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      }
+      if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(A_PW + B_PW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMA for tile t done; every wave done with tile t-1
       if (t + STAGES - 1 < nt) issue(kt0 + t + STAGES - 1, (t + STAGES - 1) % STAGES);
       const char* ta = smem + (t % STAGES) * STAGE_BYTES;
-      const char* tb = ta + TILE_BYTES;
+      const char* tb = ta + A_BYTES;
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         s16x8 fa[4], fb[NJ];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          fa[i] = (AM == SDMI_A_COLMAJOR) ? frag_tr_asm(ta, wm + 16 * i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
+        for (int i = 0; i < 4; ++i) {
+          const int mb = wm + 16 * i;
+          fa[i] = A_MN ? frag_tr_asm(ta + (mb >> 7) * 16384, mb & 127, ks, lane) : frag_kc(ta, mb, ks, lane);
+        }
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          fb[j] = (BMODE == SDMI_B_NK) ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_tr_asm(tb, wn + 16 * j, ks, lane);
-        if constexpr (AM == SDMI_A_COLMAJOR) lds_wait_frags(fa);
-        if constexpr (BMODE != SDMI_B_NK) lds_wait_frags(fb);
+        for (int j = 0; j < NJ; ++j) {
+          const int nb = wn + 16 * j;
+          fb[j] = B_MN ? frag_tr_asm(tb + (nb >> 7) * 16384, nb & 127, ks, lane) : frag_kc(tb, nb, ks, lane);
+        }
+        if constexpr (A_MN) lds_wait_frags(fa);
+        if constexpr (B_MN) lds_wait_frags(fb);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        if (RED != 0 && red_tile) {
+          const int kb = (kt0 + t) * BK + ks * 32 + (lane >> 4) * 8;
+#pragma unroll
+          for (int rr = 0; rr < RPW; ++rr) {
+            const int r = wave % NWN + rr * NWN;
+            if (r < nred) {
+              const s16x8 fr = reduce_frag<RED>(g, r, kb, lane);
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                accr[rr][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fr, accr[rr][i], 0, 0, 0);
+            }
+          }
+        }
       }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -970,8 +1023,28 @@ __global__ __launch_bounds__(NT, (STAGES == 2 ? 2 : 1)) void gemm_dma_kernel(con
   __syncthreads();
   const EpiArgs ev = epi_args_late();  // epilogue arguments loaded only from here on (see gemm_kernel)
   const EpiArgs* ep = &ev;
-  gemm_epilogue<TBN>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
-  if (ep->raw && ep->counters) splitk_tail<TBN>(*ep, smem, m0, n0, tl.tile);
+  if (RED != 0 && red_tile) {
+    // lane holds C[wm + 16i + 4(lane>>4) + q][r*16 + (lane & 15)]: column 0 = row sums, 8 + j = group j
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int col = (wave % NWN + rr * NWN) * 16 + (lane & 15);
+      if (!(col == 0 || (RED == 2 && col >= 8 && col - 8 < ep->ngrp))) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + q;
+          if (row >= ep->M) continue;
+          const float v = accr[rr][i][q];
+          if (ep->raw) ((float*)ep->ws)[(long long)z * ep->split_stride + (long long)row * ep->N + ep->n_x0 + col] = v;
+          else Epi::extra(*ep, row, ep->n_x0 + col, &v, 1);
+        }
+    }
+  }
+  gemm_epilogue<TBN, false, TBM, NJ, NTH>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
+  if constexpr (TBM == BM && NTH == NT) {
+    if (ep->raw && ep->counters) splitk_tail<TBN>(*ep, smem, m0, n0, tl.tile);
+  }
 }
 
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
@@ -1080,28 +1153,51 @@ int n_total(const sdmi_gemm_desc* d) {
 // slab row width with split-K: the produced columns, plus one 8-column chunk carrying the VALU row sums
 int slab_n(const sdmi_gemm_desc* d) { return n_total(d) + ((has_reductions(d) && !d->gsum_out) ? 8 : 0); }
 
-// Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged, 2 / 3 LDS-DMA ring
-// with that many stages, -1 (default) per mode: the DMA ring where it measured faster on the step's
-// shapes (row-major and implicit-conv A), register staging for the col-major (weight-gradient) A.
+// Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged, 2 / 3 LDS-DMA ring with that many
+// stages (128-row tiles), 4 LDS-DMA 2-stage ring with the large 8-wave tiles (256 x {128, 192} for B_NK, 128 x
+// {256, 384} for col-major A with MN-contiguous B). -1 (default) per mode: the DMA ring where it measured faster on
+// the step's shapes (row-major and implicit-conv A), register staging for the col-major (weight-gradient) A; the
+// per-shape table sdmi/tuned_gemm.json overrides it through variant_hint.
 int gemm_variant() {
   static int v = -2;
   if (v == -2) {
     const char* s = getenv("SDMI_GEMM_VARIANT");
     v = s ? atoi(s) : -1;
-    if (v != 0 && v != 2 && v != 3) v = -1;
+    if (v != 0 && v != 2 && v != 3 && v != 4) v = -1;
   }
   return v;
 }
 
+// the DMA kernels form the reduction columns from synthesised B fragments: every group of 8 consecutive k in one
+// group (sum_group % 8 == 0) and at most 3 reduction tiles (8 + groups <= 48)
+bool dma_reductions_ok(const sdmi_gemm_desc* d) {
+  if (!d->gsum_out) return true;
+  return d->sum_group % 8 == 0 && 8 + reduction_groups(d) <= 48;
+}
+
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 3) v = d->variant_hint == 1 ? 0 : d->variant_hint;
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 4) v = d->variant_hint == 1 ? 0 : d->variant_hint;
   if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
-  if (has_reductions(d)) v = 0;  // reduction columns are synthesised in the register-staged loader
+  if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
+  if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
   // the DMA path needs a tile-uniform second source (k_split % BK == 0)
   if (d->a_mode == SDMI_A_CONV && d->a2 && d->k_split % BK) v = 0;
+  if (v == 4) {  // large tiles: B_NK with row-major / conv A, or col-major A with MN-contiguous B and N % 256 == 0
+    const bool ok = d->a_mode == SDMI_A_COLMAJOR ? (d->b_mode != SDMI_B_NK && d->n % 256 == 0)
+                                                 : (d->b_mode == SDMI_B_NK && d->n >= 128);
+    if (!ok) v = 2;
+  }
+  if (v != 0 && d->a_mode == SDMI_A_COLMAJOR && d->b_mode == SDMI_B_NK) v = 0;  // no DMA instantiation
   return v;
 }
+
+int tile_m(const sdmi_gemm_desc* d, int variant) {
+  return variant == 4 && d->a_mode != SDMI_A_COLMAJOR ? 256 : BM;
+}
+
+// columns the grid covers: the DMA kernels compute the reduction columns outside the column tiles
+int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total(d) : d->n; }
 
 // Column-tile width: 192 (2-stage DMA, B_NK, N % 192 == 0) when it needs fewer rounds x columns of the
 // 512 workgroup slots (2 per CU) than 128 -- e.g. 32768 x 384: 768 tiles = 1.5 rounds at 128, 512 = 1 at 192.
@@ -1110,6 +1206,10 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
   if (force == -2) {
     const char* s = getenv("SDMI_GEMM_TBN");
     force = s ? atoi(s) : -1;
+  }
+  if (variant == 4) {
+    if (d->a_mode == SDMI_A_COLMAJOR) return d->n % 384 == 0 ? 384 : 256;
+    return d->n % 192 == 0 ? 192 : BN;
   }
   if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR) return BN;
   // narrow outputs (N <= 64: the VQVAE's 64-channel convs at 256^2, 4-channel heads, DiT proj_out): a 128-column
@@ -1138,34 +1238,56 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
   return r192 * 192 <= r128 * 128 ? 192 : BN;
 }
 
-template <int AM, int BMODE>
-hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
-  if constexpr (AM == SDMI_A_COLMAJOR) {
-    if (a.rowsum) {
-      sdmi_rt::launch((gemm_kernel<AM, BMODE, 1>), grid, dim3(NT), 0, s, a, e);
-      return hipGetLastError();
+template <int AM, int BMODE, int STAGES, int TBN, int TBM, int NWN, int RED>
+hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
+  constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * BK * 2, epi = (size_t)64 * (TBN + 4) * 4;
+  sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED>), grid, dim3(dma_threads<TBM, NWN>()),
+                  ring > epi ? ring : epi, s, a, e);
+  return hipGetLastError();
+}
+
+template <int AM, int BMODE, int RED>
+hipError_t launch_dma_red(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
+  if (v == 3 && RED == 0) return launch_dma<AM, BMODE, 3, BN, BM, 2, 0>(a, e, grid, s);
+  if (v == 4) {
+    if constexpr (AM == SDMI_A_COLMAJOR) {
+      if (tbn == 384) return launch_dma<AM, BMODE, 2, 384, BM, 4, RED>(a, e, grid, s);
+      if (tbn == 256) return launch_dma<AM, BMODE, 2, 256, BM, 4, RED>(a, e, grid, s);
+    } else if constexpr (BMODE == SDMI_B_NK && RED == 0) {
+      if (tbn == 192) return launch_dma<AM, BMODE, 2, 192, 256, 2, 0>(a, e, grid, s);
+      if (tbn == BN) return launch_dma<AM, BMODE, 2, BN, 256, 2, 0>(a, e, grid, s);
     }
-    if (a.n_x0) {
-      sdmi_rt::launch((gemm_kernel<AM, BMODE, 2>), grid, dim3(NT), 0, s, a, e);
-      return hipGetLastError();
-    }
-  }
-  if (v == 0) {
-    sdmi_rt::launch((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
-  } else if (v == 3) {
-    sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, 3>), grid, dim3(NT), 3 * 2 * TILE_BYTES, s, a, e);
-  } else if (tbn == BN) {
-    sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, 2>), grid, dim3(NT), 2 * 2 * TILE_BYTES, s, a, e);
-  } else if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR) {
-    if (tbn == 64)
-      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, 2, 64>), grid, dim3(NT), 2 * (TILE_BYTES + 64 * BK * 2), s, a, e);
-    else
-      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, 2, 192>), grid, dim3(NT), 2 * (TILE_BYTES + 192 * BK * 2), s, a,
-                         e);
-  } else {
     return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  if (tbn == BN) return launch_dma<AM, BMODE, 2, BN, BM, 2, RED>(a, e, grid, s);
+  if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR && RED == 0) {
+    if (tbn == 64) return launch_dma<AM, BMODE, 2, 64, BM, 2, 0>(a, e, grid, s);
+    if (tbn == 192) return launch_dma<AM, BMODE, 2, 192, BM, 2, 0>(a, e, grid, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <int AM, int BMODE>
+hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
+  if (v == 0) {
+    if constexpr (AM == SDMI_A_COLMAJOR) {
+      if (a.rowsum) {
+        sdmi_rt::launch((gemm_kernel<AM, BMODE, 1>), grid, dim3(NT), 0, s, a, e);
+        return hipGetLastError();
+      }
+      if (a.n_x0) {
+        sdmi_rt::launch((gemm_kernel<AM, BMODE, 2>), grid, dim3(NT), 0, s, a, e);
+        return hipGetLastError();
+      }
+    }
+    sdmi_rt::launch((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
+    return hipGetLastError();
+  }
+  if constexpr (AM == SDMI_A_COLMAJOR && BMODE != SDMI_B_NK) {
+    if (a.n_x0) return launch_dma_red<AM, BMODE, 2>(a, e, grid, s, v, tbn);
+    if (a.rowsum) return launch_dma_red<AM, BMODE, 1>(a, e, grid, s, v, tbn);
+  }
+  return launch_dma_red<AM, BMODE, 0>(a, e, grid, s, v, tbn);
 }
 
 // Split-K arrival counters: SK_SLOTS regions of SK_SLOT_TILES, one region per launch, round-robin, so split
@@ -1278,10 +1400,22 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   return 0;
 }
 
+int plan_splits_uncapped(const sdmi_gemm_desc* d, long long tiles, int nkt);
+
 int plan_splits(const sdmi_gemm_desc* d) {
-  const int tbn = pick_tbn(d, pick_variant(d));
-  long long tiles = (long long)((d->m + BM - 1) / BM) * ((n_total(d) + tbn - 1) / tbn);
+  const int v = pick_variant(d), tbn = pick_tbn(d, v), tbm = tile_m(d, v);
+  long long tiles = (long long)((d->m + tbm - 1) / tbm) * ((n_grid(d, v) + tbn - 1) / tbn);
   int nkt = (d->k + BK - 1) / BK;
+  static int cap = -1;  // SDMI_SPLIT_CAP: upper bound on the split count of col-major-A (weight-gradient) launches
+  if (cap < 0) {
+    const char* e = getenv("SDMI_SPLIT_CAP");
+    cap = e ? std::max(1, atoi(e)) : 1 << 30;
+  }
+  const int s = plan_splits_uncapped(d, tiles, nkt);
+  return d->a_mode == SDMI_A_COLMAJOR ? std::min(s, cap) : s;
+}
+
+int plan_splits_uncapped(const sdmi_gemm_desc* d, long long tiles, int nkt) {
   if (d->splits_hint > 0) {
     int s = std::min(d->splits_hint, nkt);
     while (s > 1 && (long long)s * d->m * slab_n(d) * 4 >= (1LL << 31)) s >>= 1;
@@ -1313,7 +1447,8 @@ int plan_splits(const sdmi_gemm_desc* d) {
 }  // namespace
 
 // which mainloop / column-tile width a launch of this descriptor uses (variant: 0 register-staged, 2 / 3 LDS-DMA
-// ring stages; tile_n: 128 or 192) -- for profiling / roofline attribution
+// ring stages with 128-row tiles, 4 the large 8-wave tiles; tile_n: 64 .. 384) -- for profiling / roofline
+// attribution
 extern "C" int sdmi_gemm_kernel_info(const sdmi_gemm_desc* d, int* variant, int* tile_n) {
   if (!d) return -1;
   const int v = pick_variant(d);
@@ -1348,15 +1483,18 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
   splits = (nkt + a.ktiles_per_split - 1) / a.ktiles_per_split;
   a.nsplit = splits;
   EpiArgs run = e;
-  const int variant = pick_variant(d), tbn = pick_tbn(d, variant);
-  dim3 grid((nt + tbn - 1) / tbn, (d->m + BM - 1) / BM, splits);
+  const int variant = pick_variant(d), tbn = pick_tbn(d, variant), tbm = tile_m(d, variant);
+  const int ng = n_grid(d, variant);
+  dim3 grid((ng + tbn - 1) / tbn, (d->m + tbm - 1) / tbm, splits);
   if (splits > 1) {
     run.raw = 1;
     run.ws = (const float*)workspace;
     run.nsplit = splits;
     run.split_stride = (long long)d->m * ns;
     // the in-launch combine reduces whole tiles only: the VALU row-sum chunk (outside every tile) needs the reducer
-    run.counters = ns != nt ? nullptr : splitk_counters((long long)grid.x * grid.y, splits);
+    // (and only the 128-row, 4-wave tiles carry it)
+    run.counters = (ns != nt || variant == 4 || (variant != 0 && has_reductions(d)))
+                       ? nullptr : splitk_counters((long long)grid.x * grid.y, splits);
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
