@@ -694,6 +694,22 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
 // fragment reads are unchanged. Out-of-range lanes (conv padding, ragged tiles) use an offset beyond
 // the buffer record and the hardware writes zeros.
 // ---------------------------------------------------------------------------------------------
+// K-contiguous LDS image with KBK-deep rows: 128-B rows (KBK 64), chunk c of row r at slot c ^ (r & 7); 64-B rows
+// (KBK 32), chunk c at slot c ^ f((r >> 2) & 3) with f = {0, 2, 3, 1}: the four ds_read_b128 lane groups of a
+// fragment read (rows 0-15 x chunks 0-3) then each hit 16 distinct 16-B slots of the 256-B bank row
+template <int KBK>
+__device__ __forceinline__ int kc_off_k(int r, int c) {
+  if constexpr (KBK == 64) return r * 128 + ((c ^ (r & 7)) << 4);
+  return r * 64 + ((c ^ ((0x1320 >> (((r >> 2) & 3) * 4)) & 3)) << 4);
+}
+
+template <int KBK>
+__device__ __forceinline__ s16x8 frag_kc_k(const char* tile, int rbase, int ks, int lane) {
+  int r = rbase + (lane & 15);
+  int c = ks * 4 + (lane >> 4);
+  return *(const s16x8*)(tile + kc_off_k<KBK>(r, c));
+}
+
 __device__ __forceinline__ s16x8 frag_kc(const char* tile, int rbase, int ks, int lane) {
   int r = rbase + (lane & 15);
   int c = ks * 4 + (lane >> 4);
@@ -773,15 +789,23 @@ __device__ __forceinline__ s16x8 reduce_frag(const Args& g, int r, int kb, int l
   return (s16x8){v, v, v, v, v, v, v, v};
 }
 
-template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0>
-__global__ __launch_bounds__((dma_threads<TBM, NWN>()), ((dma_threads<TBM, NWN>() == 256 && STAGES == 2) ? 2 : 1))
+// KBK: k depth of one staged tile (64, or 32 for deeper rings in the same LDS: more bytes in flight per CU). Split-K
+// slices stay in units of 64 (host k-tiles).
+template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0, int KBK = BK>
+__global__ __launch_bounds__((dma_threads<TBM, NWN>()),
+                             ((dma_threads<TBM, NWN>() == 256 && STAGES * (TBM + TBN) * KBK * 2 <= 80 * 1024) ? 2 : 1))
 void gemm_dma_kernel(const Args g, const EpiArgs e) {
   constexpr int NTH = dma_threads<TBM, NWN>();
   constexpr int NW = NTH / 64;
   constexpr int WTN = TBN / NWN;                     // columns per wave
   constexpr int NJ = WTN / 16;                       // 16-column MFMA tiles per wave
   constexpr bool A_MN = AM == SDMI_A_COLMAJOR, B_MN = BMODE != SDMI_B_NK;
-  constexpr int A_BYTES = TBM * BK * 2, B_BYTES = TBN * BK * 2;
+  static_assert(KBK == 64 || KBK == 32, "staged k depth");
+  constexpr int KS = KBK / 32;                        // MFMA k-steps per staged tile
+  constexpr int RB = KBK * 2;                         // K-contiguous image row bytes
+  constexpr int RPI = 1024 / RB, CPR = KBK / 8;       // rows per DMA wave-instruction, 16-B chunks per row
+  constexpr int SUB = KBK * 256, IPS = KBK / 4;       // MN image: 128-column sub-tile bytes, DMA pieces per sub-tile
+  constexpr int A_BYTES = TBM * KBK * 2, B_BYTES = TBN * KBK * 2;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;     // A | B
   constexpr int A_PW = A_BYTES / 1024 / NW, B_PW = B_BYTES / 1024 / NW;  // DMA wave-instructions per tile
   static_assert(A_PW * NW * 1024 == A_BYTES && B_PW * NW * 1024 == B_BYTES, "DMA pieces per wave");
@@ -793,14 +817,14 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) char smem[];  // STAGES x (A | B)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform: scalar LDS bases / M0
   const int wm = (wave / NWN) * 64, wn = (wave % NWN) * WTN;
   const TileId tl = tile_id<TBN, TBM>();
   const int m0 = tl.m0, n0 = tl.n0;
   const int z = tl.z;
-  const int nkt_total = (g.K + BK - 1) / BK;
-  const int kt0 = z * g.ktiles_per_split;
-  const int kt1 = min(nkt_total, kt0 + g.ktiles_per_split);
+  const int nkt_total = (g.K + KBK - 1) / KBK;
+  const int kt0 = z * g.ktiles_per_split * (BK / KBK);
+  const int kt1 = min(nkt_total, kt0 + g.ktiles_per_split * (BK / KBK));
   constexpr int OOB = (int)0x80000000;
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
@@ -817,20 +841,20 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   bool a_ok[A_PW], b_ok[B_PW];
   int a_iy[A_PW], a_ix[A_PW], a_pb[A_PW], a_pix[A_PW];
   int b_ty[B_PW], b_tx[B_PW];
-  const bool cin64 = AM == SDMI_A_CONV && (g.cin & 63) == 0;  // k tile lies inside one tap
+  const bool cin64 = AM == SDMI_A_CONV && g.cin % KBK == 0;  // k tile lies inside one tap
 #pragma unroll
   for (int j = 0; j < A_PW; ++j) {
     const int q = wave * A_PW + j;
     if (A_MN) {
-      int kr = (q & 15) * 4 + (lane >> 4);
+      int kr = (q % IPS) * 4 + (lane >> 4);
       int c = (lane & 15) ^ tr_swz(kr);
-      int m = m0 + (q >> 4) * 128 + c * 8;
+      int m = m0 + (q / IPS) * 128 + c * 8;
       a_ok[j] = m < g.M;
       a_base[j] = m;
       a_kk[j] = kr;
     } else {
-      int r = q * 8 + (lane >> 3);
-      int c = (lane & 7) ^ (r & 7);
+      int r = q * RPI + lane / CPR;
+      int c = (kc_off_k<KBK>(r, lane % CPR) - r * RB) >> 4;  // logical chunk of the lane's physical slot (involution)
       int m = m0 + r;
       a_ok[j] = m < g.M;
       a_kk[j] = c * 8;
@@ -851,16 +875,16 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   for (int j = 0; j < B_PW; ++j) {
     const int q = wave * B_PW + j;
     if (!B_MN) {
-      int r = q * 8 + (lane >> 3);
-      int c = (lane & 7) ^ (r & 7);
+      int r = q * RPI + lane / CPR;
+      int c = (kc_off_k<KBK>(r, lane % CPR) - r * RB) >> 4;
       int n = n0 + r;
       b_ok[j] = n < g.N;
       b_base[j] = n * g.ldb;
       b_kk[j] = c * 8;
     } else {
-      int kr = (q & 15) * 4 + (lane >> 4);
+      int kr = (q % IPS) * 4 + (lane >> 4);
       int c = (lane & 15) ^ tr_swz(kr);
-      int n = n0 + (q >> 4) * 128 + c * 8;
+      int n = n0 + (q / IPS) * 128 + c * 8;
       b_ok[j] = n < g.N;
       b_kk[j] = kr;
       b_base[j] = n;
@@ -877,16 +901,44 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   // implicit-conv tap state (cin % 64 == 0): the (ty, tx, channel offset) of the next k-tile to issue, advanced
   // incrementally -- issue() is called for consecutive k-tiles -- instead of two runtime divisions per tile
   int c_ty = 0, c_tx = 0, c_ci = 0;
-  if (AM == SDMI_A_CONV && cin64 && kt0 * BK < g.k_split) {
-    const int tap = (kt0 * BK) / g.cin;
-    c_ci = kt0 * BK - tap * g.cin;
+  if (AM == SDMI_A_CONV && cin64 && kt0 * KBK < g.k_split) {
+    const int tap = (kt0 * KBK) / g.cin;
+    c_ci = kt0 * KBK - tap * g.cin;
     c_ty = tap / g.kw;
     c_tx = tap - c_ty * g.kw;
   }
-  auto issue = [&](int kt, int stage) __attribute__((always_inline)) {
-    char* sa = smem + stage * STAGE_BYTES;
-    char* sb = sa + A_BYTES;
-    const int k0 = kt * BK;
+  // Fast issue path for full k-tiles: every per-lane part of a DMA source offset is fixed over the K loop, the
+  // per-tile part is wave-uniform (k0, or the conv tap shift), so a piece costs an add and a select instead of the
+  // general path's coordinate math and bounds checks. Invalid lanes keep OOB (+ a uniform offset < 2^31: still out
+  // of the 2^31 - 1 byte buffer record). Conv A (cin % KBK == 0): tap validity per lane is a precomputed bit mask.
+  int a_v[A_PW], b_v[B_PW];
+  unsigned a_tm[A_PW];
+#pragma unroll
+  for (int j = 0; j < A_PW; ++j) {
+    a_tm[j] = 0u;
+    if (AM == SDMI_A_ROWMAJOR) a_v[j] = a_ok[j] ? (a_base[j] + a_kk[j]) * 2 : OOB;
+    else if (A_MN) a_v[j] = a_ok[j] ? (a_kk[j] * g.lda + a_base[j]) * 2 : OOB;
+    else {
+      a_v[j] = (a_pix[j] + a_kk[j]) * 2;
+      if (cin64) {
+        const int taps = g.k_split / g.cin;  // <= 16 (4x4 kernels)
+        for (int tp = 0, ty = 0, tx = 0; tp < taps; ++tp) {
+          const int iy = a_iy[j] + ty, ix = a_ix[j] + tx;
+          if (a_ok[j] && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw) a_tm[j] |= 1u << tp;
+          if (++tx == g.kw) { tx = 0; ++ty; }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < B_PW; ++j) {
+    if (BMODE == SDMI_B_NK) b_v[j] = b_ok[j] ? (b_base[j] + b_kk[j]) * 2 : OOB;
+    else if (BMODE == SDMI_B_KN) b_v[j] = b_ok[j] ? (b_kk[j] * g.ldb + b_base[j]) * 2 : OOB;
+    else b_v[j] = 0;
+  }
+
+  // general issue path (ragged k-tiles, the fused second source, conv with cin % KBK != 0, the B im2col gather)
+  auto issue_general_a = [&](int k0, char* sa) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < A_PW; ++j) {
       char* dst = sa + (wave * A_PW + j) * 1024;
@@ -899,7 +951,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
         off = (a_ok[j] && k < g.K) ? (k * g.lda + a_base[j]) * 2 : OOB;
       } else {
         int k = k0 + a_kk[j];
-        if (k0 >= g.k_split) {  // fused 1x1 second source, tile-uniform (k_split % 64 == 0 on this path)
+        if (k0 >= g.k_split) {  // fused 1x1 second source, tile-uniform (k_split % KBK == 0 on this path)
           off = (a_ok[j] && k < g.K) ? (a_base[j] + (k - g.k_split)) * 2 : OOB;
           dma16(rsA2, dst, off);
           continue;
@@ -922,7 +974,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
       dma16(rsA, dst, off);
     }
     if (AM == SDMI_A_CONV && cin64 && k0 < g.k_split) {
-      c_ci += BK;
+      c_ci += KBK;
       if (c_ci >= g.cin) {
         c_ci = 0;
         if (++c_tx == g.kw) {
@@ -931,6 +983,8 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
         }
       }
     }
+  };
+  auto issue_general_b = [&](int k0, char* sb) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < B_PW; ++j) {
       char* dst = sb + (wave * B_PW + j) * 1024;
@@ -951,6 +1005,44 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
       }
       dma16(rsB, dst, off);
     }
+  };
+
+  auto issue = [&](int kt, int stage) __attribute__((always_inline)) {
+    char* sa = smem + stage * STAGE_BYTES;
+    char* sb = sa + A_BYTES;
+    const int k0 = kt * KBK;
+    if (k0 + KBK <= g.K && (AM != SDMI_A_CONV || (cin64 && k0 + KBK <= g.k_split))) {
+      const int tap = c_ty * g.kw + c_tx;
+      const int ash = AM == SDMI_A_ROWMAJOR ? k0 * 2
+                      : A_MN              ? k0 * g.lda * 2
+                                          : ((c_ty * g.iw + c_tx) * g.ldx + c_ci) * 2;
+#pragma unroll
+      for (int j = 0; j < A_PW; ++j) {
+        int off;
+        if (AM == SDMI_A_CONV) off = ((a_tm[j] >> tap) & 1u) ? a_v[j] + ash : OOB;
+        else off = a_v[j] + ash;
+        dma16(rsA, sa + (wave * A_PW + j) * 1024, off);
+      }
+      if (AM == SDMI_A_CONV) {
+        c_ci += KBK;
+        if (c_ci >= g.cin) {
+          c_ci = 0;
+          if (++c_tx == g.kw) {
+            c_tx = 0;
+            ++c_ty;
+          }
+        }
+      }
+      if (BMODE != SDMI_B_KN_CONV) {
+        const int bsh = BMODE == SDMI_B_NK ? k0 * 2 : k0 * g.ldb * 2;
+#pragma unroll
+        for (int j = 0; j < B_PW; ++j) dma16(rsB, sb + (wave * B_PW + j) * 1024, b_v[j] + bsh);
+        return;
+      }
+    } else {
+      issue_general_a(k0, sa);
+    }
+    issue_general_b(k0, sb);
   };
 
   f32x4 acc[4][NJ];
@@ -975,26 +1067,28 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
       if (s < nt) issue(kt0 + s, s);
     for (int t = 0; t < nt; ++t) {
       // tile t landed for this thread: at most (tiles issued after t) x (A_PW + B_PW) DMA instructions outstanding
-      const int after = min(STAGES - 2, nt - 1 - t);
-      if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(A_PW + B_PW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (in the last STAGES-2 tiles fewer are in flight: wait for all)
+      if (STAGES > 2 && t + STAGES - 2 < nt)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"((STAGES > 2 ? STAGES - 2 : 0) * (A_PW + B_PW)) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMA for tile t done; every wave done with tile t-1
       if (t + STAGES - 1 < nt) issue(kt0 + t + STAGES - 1, (t + STAGES - 1) % STAGES);
       const char* ta = smem + (t % STAGES) * STAGE_BYTES;
       const char* tb = ta + A_BYTES;
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         s16x8 fa[4], fb[NJ];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int mb = wm + 16 * i;
-          fa[i] = A_MN ? frag_tr_asm(ta + (mb >> 7) * 16384, mb & 127, ks, lane) : frag_kc(ta, mb, ks, lane);
+          fa[i] = A_MN ? frag_tr_asm(ta + (mb >> 7) * SUB, mb & 127, ks, lane) : frag_kc_k<KBK>(ta, mb, ks, lane);
         }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int nb = wn + 16 * j;
-          fb[j] = B_MN ? frag_tr_asm(tb + (nb >> 7) * 16384, nb & 127, ks, lane) : frag_kc(tb, nb, ks, lane);
+          fb[j] = B_MN ? frag_tr_asm(tb + (nb >> 7) * SUB, nb & 127, ks, lane) : frag_kc_k<KBK>(tb, nb, ks, lane);
         }
         if constexpr (A_MN) lds_wait_frags(fa);
         if constexpr (B_MN) lds_wait_frags(fb);
@@ -1004,7 +1098,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
           for (int j = 0; j < NJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         if (RED != 0 && red_tile) {
-          const int kb = (kt0 + t) * BK + ks * 32 + (lane >> 4) * 8;
+          const int kb = (kt0 + t) * KBK + ks * 32 + (lane >> 4) * 8;
 #pragma unroll
           for (int rr = 0; rr < RPW; ++rr) {
             const int r = wave % NWN + rr * NWN;
@@ -1153,17 +1247,18 @@ int n_total(const sdmi_gemm_desc* d) {
 // slab row width with split-K: the produced columns, plus one 8-column chunk carrying the VALU row sums
 int slab_n(const sdmi_gemm_desc* d) { return n_total(d) + ((has_reductions(d) && !d->gsum_out) ? 8 : 0); }
 
-// Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged, 2 / 3 LDS-DMA ring with that many
-// stages (128-row tiles), 4 LDS-DMA 2-stage ring with the large 8-wave tiles (256 x {128, 192} for B_NK, 128 x
-// {256, 384} for col-major A with MN-contiguous B). -1 (default) per mode: the DMA ring where it measured faster on
-// the step's shapes (row-major and implicit-conv A), register staging for the col-major (weight-gradient) A; the
-// per-shape table sdmi/tuned_gemm.json overrides it through variant_hint.
+// Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged; LDS-DMA rings: 2 / 3 stages of
+// 64-deep 128-row tiles (4 waves), 4 = 128 x {256, 384} tiles on 8 waves with a 4-stage ring of 32-deep stages (3
+// tiles, 96 KiB, in flight per CU), 5 = 128 x {128, 192} tiles on 4 waves with a 3-stage ring of 32-deep stages (two
+// workgroups per CU). -1 (default) per mode: the DMA ring where it measured faster on the step's shapes (row-major
+// and implicit-conv A), register staging for the col-major (weight-gradient) A; the per-shape table
+// sdmi/tuned_gemm.json overrides it through variant_hint.
 int gemm_variant() {
   static int v = -2;
   if (v == -2) {
     const char* s = getenv("SDMI_GEMM_VARIANT");
     v = s ? atoi(s) : -1;
-    if (v != 0 && v != 2 && v != 3 && v != 4) v = -1;
+    if (v != 0 && v != 2 && v != 3 && v != 4 && v != 5) v = -1;
   }
   return v;
 }
@@ -1177,24 +1272,19 @@ bool dma_reductions_ok(const sdmi_gemm_desc* d) {
 
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 4) v = d->variant_hint == 1 ? 0 : d->variant_hint;
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 5) v = d->variant_hint == 1 ? 0 : d->variant_hint;
   if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
   if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
   if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
   // the DMA path needs a tile-uniform second source (k_split % BK == 0)
   if (d->a_mode == SDMI_A_CONV && d->a2 && d->k_split % BK) v = 0;
-  if (v == 4) {  // large tiles: B_NK with row-major / conv A, or col-major A with MN-contiguous B and N % 256 == 0
-    const bool ok = d->a_mode == SDMI_A_COLMAJOR ? (d->b_mode != SDMI_B_NK && d->n % 256 == 0)
-                                                 : (d->b_mode == SDMI_B_NK && d->n >= 128);
-    if (!ok) v = 2;
-  }
+  if (v == 4 && d->n % 256 && d->n % 384) v = 2;  // 128 x {256, 384} tiles: N % 384 == 0 or N % 256 == 0
+  if (v == 5 && d->a_mode == SDMI_A_CONV && d->a2 && d->k_split % 32) v = 0;
   if (v != 0 && d->a_mode == SDMI_A_COLMAJOR && d->b_mode == SDMI_B_NK) v = 0;  // no DMA instantiation
   return v;
 }
 
-int tile_m(const sdmi_gemm_desc* d, int variant) {
-  return variant == 4 && d->a_mode != SDMI_A_COLMAJOR ? 256 : BM;
-}
+int tile_m(const sdmi_gemm_desc*, int) { return BM; }
 
 // columns the grid covers: the DMA kernels compute the reduction columns outside the column tiles
 int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total(d) : d->n; }
@@ -1207,10 +1297,8 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
     const char* s = getenv("SDMI_GEMM_TBN");
     force = s ? atoi(s) : -1;
   }
-  if (variant == 4) {
-    if (d->a_mode == SDMI_A_COLMAJOR) return d->n % 384 == 0 ? 384 : 256;
-    return d->n % 192 == 0 ? 192 : BN;
-  }
+  if (variant == 4) return d->n % 384 == 0 ? 384 : 256;
+  if (variant == 5) return d->b_mode == SDMI_B_NK && d->n % 192 == 0 ? 192 : BN;
   if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR) return BN;
   // narrow outputs (N <= 64: the VQVAE's 64-channel convs at 256^2, 4-channel heads, DiT proj_out): a 128-column
   // tile would spend half (or more) of its MFMAs on zero-padded columns. SDMI_GEMM_TBN64 = the largest N given
@@ -1238,24 +1326,26 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
   return r192 * 192 <= r128 * 128 ? 192 : BN;
 }
 
-template <int AM, int BMODE, int STAGES, int TBN, int TBM, int NWN, int RED>
+template <int AM, int BMODE, int STAGES, int TBN, int TBM, int NWN, int RED, int KBK = BK>
 hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
-  constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * BK * 2, epi = (size_t)64 * (TBN + 4) * 4;
-  sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED>), grid, dim3(dma_threads<TBM, NWN>()),
-                  ring > epi ? ring : epi, s, a, e);
+  constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * KBK * 2, epi = (size_t)64 * (TBN + 4) * 4;
+  sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid,
+                  dim3(dma_threads<TBM, NWN>()), ring > epi ? ring : epi, s, a, e);
   return hipGetLastError();
 }
 
 template <int AM, int BMODE, int RED>
 hipError_t launch_dma_red(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
   if (v == 3 && RED == 0) return launch_dma<AM, BMODE, 3, BN, BM, 2, 0>(a, e, grid, s);
-  if (v == 4) {
-    if constexpr (AM == SDMI_A_COLMAJOR) {
-      if (tbn == 384) return launch_dma<AM, BMODE, 2, 384, BM, 4, RED>(a, e, grid, s);
-      if (tbn == 256) return launch_dma<AM, BMODE, 2, 256, BM, 4, RED>(a, e, grid, s);
-    } else if constexpr (BMODE == SDMI_B_NK && RED == 0) {
-      if (tbn == 192) return launch_dma<AM, BMODE, 2, 192, 256, 2, 0>(a, e, grid, s);
-      if (tbn == BN) return launch_dma<AM, BMODE, 2, BN, 256, 2, 0>(a, e, grid, s);
+  if (v == 4) {  // 128 x {256, 384} on 8 waves, 32-deep stages, 4-stage ring (3 tiles in flight)
+    if (tbn == 384) return launch_dma<AM, BMODE, 4, 384, BM, 4, RED, 32>(a, e, grid, s);
+    if (tbn == 256) return launch_dma<AM, BMODE, 4, 256, BM, 4, RED, 32>(a, e, grid, s);
+    return hipErrorInvalidValue;
+  }
+  if (v == 5) {  // 128 x {128, 192} on 4 waves, 32-deep stages, 3-stage ring, two workgroups per CU
+    if (tbn == BN) return launch_dma<AM, BMODE, 3, BN, BM, 2, RED, 32>(a, e, grid, s);
+    if constexpr (BMODE == SDMI_B_NK && RED == 0) {
+      if (tbn == 192) return launch_dma<AM, BMODE, 3, 192, BM, 2, 0, 32>(a, e, grid, s);
     }
     return hipErrorInvalidValue;
   }
@@ -1446,9 +1536,8 @@ int plan_splits_uncapped(const sdmi_gemm_desc* d, long long tiles, int nkt) {
 
 }  // namespace
 
-// which mainloop / column-tile width a launch of this descriptor uses (variant: 0 register-staged, 2 / 3 LDS-DMA
-// ring stages with 128-row tiles, 4 the large 8-wave tiles; tile_n: 64 .. 384) -- for profiling / roofline
-// attribution
+// which mainloop / column-tile width a launch of this descriptor uses (variant: 0 register-staged, 2 .. 5 the LDS-DMA
+// rings of gemm_variant(); tile_n: 64 .. 384) -- for profiling / roofline attribution
 extern "C" int sdmi_gemm_kernel_info(const sdmi_gemm_desc* d, int* variant, int* tile_n) {
   if (!d) return -1;
   const int v = pick_variant(d);
@@ -1493,7 +1582,7 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     run.split_stride = (long long)d->m * ns;
     // the in-launch combine reduces whole tiles only: the VALU row-sum chunk (outside every tile) needs the reducer
     // (and only the 128-row, 4-wave tiles carry it)
-    run.counters = (ns != nt || variant == 4 || (variant != 0 && has_reductions(d)))
+    run.counters = (ns != nt || variant >= 4 || (variant != 0 && has_reductions(d)))
                        ? nullptr : splitk_counters((long long)grid.x * grid.y, splits);
   }
   hipError_t err;

@@ -315,6 +315,9 @@ class UNetEngine:
         # data-gradient chain of the backward on the current stream
         use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
         self.side = side_stream(self.device) if use_side else None
+        # the cross-attention context branch runs ahead of the forward on a stream of its own (SDMI_CTX_STREAM=0: inline)
+        use_ctx = self.device.type == "cuda" and os.environ.get("SDMI_CTX_STREAM", "1") != "0"
+        self.ctx_stream = torch.cuda.Stream(device=self.device) if use_ctx else None
         self._keep = []
         # linear data gradients from transposed packed weights (B_NK: the forward GEMM's wider tiles). Off by
         # default here: the data-gradient GEMMs gain 0.2 ms in isolation but the overlapped step measures
@@ -566,6 +569,8 @@ class UNetEngine:
                                                          txt.shape[2], K._stream()), "cast")
             st["S"] = S
         st["ctx"] = ctx
+        if ctx is not None and self.ctx_stream is not None:
+            self._ctx_ahead(st, B)
 
         # ---- down blocks (blocks.py:111-146) ----
         cur, cur_name = skip0, "skip0"
@@ -649,6 +654,52 @@ class UNetEngine:
         return pred, dict(tape=tape, st=st, grads=grads) if need_backward else None
 
     # ------------------------------------------------------------------------------------------
+    def _cross_layers(self):
+        """(block prefix, layer, channels) of every cross-attention, in forward order."""
+        L = self.L
+        nd = len(L["down"]) - 1
+        out = []
+        for i in range(nd):
+            out += [(f"downs.{i}", l, L["down"][i + 1]) for l in range(L["n_down"])]
+        for i in range(len(L["mid"]) - 1):
+            out += [(f"mids.{i}", l, L["mid"][i + 1]) for l in range(L["n_mid"])]
+        for j, i in enumerate(reversed(range(nd))):
+            cout = L["down"][i - 1] if i != 0 else L["conv_out"]
+            out += [(f"ups.{j}", l, cout) for l in range(L["n_up"])]
+        return out
+
+    def _wait_chunk_on(self, stream, c):
+        ev = self._pending.get(c)  # (not popped: the current stream still waits for it where it reads the chunk)
+        if ev is not None:
+            plan.wait_event(stream, ev)
+
+    def _ctx_ahead(self, st, B):
+        """The context branch of every cross-attention -- context_proj, then the k|v rows of the attention's packed
+        in-projection (blocks.py:139-140 -> nn.MultiheadAttention) -- depends only on the text context: issue all of
+        it up front on a stream of its own, each layer waiting for the optimizer chunk that updates its weights, so
+        its ~30 small launches run beside the forward's main chain instead of on it. The buffers are allocated on
+        the current stream (which waits for each layer's event before its attention reads them)."""
+        P, S, ctx = self.P, st["S"], st["ctx"]
+        cs = self.ctx_stream
+        work = []
+        for (p, l, C) in self._cross_layers():
+            work.append((p, l, C, self._new(B * S, C), self._new(B * S, 2 * C)))
+        plan.wait_stream(cs, torch.cuda.current_stream(self.device))
+        pre = {}
+        with torch.cuda.stream(cs):
+            for (p, l, C, cp, kv) in work:
+                mk, ck = f"{p}.cross_attentions.{l}", f"{p}.context_proj.{l}"
+                for name in (ck + "#f", mk + ".in_proj_weight#f"):
+                    self._wait_chunk_on(cs, self.pack.view_chunk.get(name, 0))
+                for key in (ck + ".bias", mk + ".in_proj_bias"):
+                    self._wait_chunk_on(cs, self._key_chunk.get(key, 0))
+                K.linear(ctx, self.pack.view(ck + "#f"), cp, bias=P.raw(ck + ".bias"))
+                K.linear(cp, self.pack.view(mk + ".in_proj_weight#f")[C:], kv, bias=P.raw(mk + ".in_proj_bias")[C:])
+                ev = torch.cuda.Event()
+                plan.record_event(ev, cs)
+                pre[(p, l)] = (cp, kv, ev)
+        st["ctx_pre"] = pre
+
     def _temb_bias(self):
         """The t_emb_layers biases are one contiguous fp32 vector of the flat store (forward order)."""
         return contiguous_run(self.P, [f"{p}.t_emb_layers.{l}.1.bias" for (p, l, ci, co) in self.resnets],
@@ -752,10 +803,15 @@ class UNetEngine:
             ck = f"{p}.context_proj.{l}"
             q = self._new(B * N, C)
             K.linear(a, Win[:C], q, bias=bin_[:C])
-            cp = self._new(B * S, C)
-            K.linear(ctx, self.W(ck + "#f"), cp, bias=P[ck + ".bias"])
-            kv = self._new(B * S, 2 * C)
-            K.linear(cp, Win[C:], kv, bias=bin_[C:])
+            pre = st.get("ctx_pre")
+            if pre is not None:  # issued ahead on the context stream (_ctx_ahead)
+                cp, kv, ev = pre[(p, l)]
+                plan.wait_event(torch.cuda.current_stream(self.device), ev)
+            else:
+                cp = self._new(B * S, C)
+                K.linear(ctx, self.W(ck + "#f"), cp, bias=P[ck + ".bias"])
+                kv = self._new(B * S, 2 * C)
+                K.linear(cp, Win[C:], kv, bias=bin_[C:])
             c["lse"] = K.attn_fwd(q, kv[:, :C], kv[:, C:], o, B, Hh, N, S, d)
             c.update(q=q, cp=cp, kv=kv, S=S, ctx=ctx, ck=ck)
         y = out if out is not None else self._new(B * N, C)
@@ -794,15 +850,16 @@ class UNetEngine:
             dq = self._new(B * N, C)
             dkv = self._new(B * S, 2 * C)
             K.attn_bwd(c["q"], kv[:, :C], kv[:, C:], c["o"], do, c["lse"], dq, dkv[:, :C], dkv[:, C:], B, Hh, N, S, d)
-            with self._wg(dq, dkv):
+            # the context branch (kv in-projection -> context_proj) ends at the text input, which takes no gradient:
+            # its data gradient only feeds the context_proj weight gradient, so all of it runs on the side stream
+            dcp = self._new(B * S, C)
+            with self._wg(dq, dkv, dcp):
                 K.linear_wgrad(dq, c["a"], gW[:C], bias_grad=gb[:C])
                 K.linear_wgrad(dkv, c["cp"], gW[C:], bias_grad=gb[C:])
-            dcp = self._new(B * S, C)
-            if WinT is not None:
-                K.linear_dgrad_t(dkv, WinT[:, C:], dcp)
-            else:
-                K.linear_dgrad(dkv, Win[C:], dcp)
-            with self._wg(dcp):
+                if WinT is not None:
+                    K.linear_dgrad_t(dkv, WinT[:, C:], dcp)
+                else:
+                    K.linear_dgrad(dkv, Win[C:], dcp)
                 K.linear_wgrad(dcp, c["ctx"], self.g(c["ck"] + ".weight"), bias_grad=self.g(c["ck"] + ".bias"))
             if WinT is not None:
                 K.linear_dgrad_t(dq, WinT[:, :C], da)
