@@ -19,7 +19,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
-SPLITS = (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, 24, 32, 40, 48, 64, 96, 128)
+SPLITS = (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128)
 
 
 def time_launch(L, d, ws, stream, iters=10, rounds=3):
@@ -94,9 +94,9 @@ def main():
         d.variant_hint = 0
         t_def = time_launch(L, d, ws, stream)
         best, t_best = 0, t_def
-        # mainloops: register staging (1) and the LDS-DMA rings (2, 3 stages); the library ignores a request the
-        # mode cannot take (reduction columns are register-staged only), so those shapes time variant 1 only
-        variants = (1, 2, 3)
+        # mainloops: register staging (1) and the LDS-DMA rings (2, 3: 2 / 3 stages of 64-deep K; 4: 8-wave
+        # 128 x {256, 384} tiles; 5: 3 stages of 32-deep K); the library downgrades a request the mode cannot take
+        variants = tuple(int(v) for v in os.environ.get("SDMI_TUNE_VARIANTS", "1,2,3,4,5").split(","))
         for v in variants:
             for s in SPLITS:
                 if s > nkt or s * d.m * d.n * 4 >= min(ws.numel() * 4, 1 << 31):
