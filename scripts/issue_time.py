@@ -40,6 +40,20 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"eager: host issue {1e3 * (t1 - t0) / n:.2f} ms/step, wall {1e3 * (t2 - t0) / n:.2f} ms/step")
+    from sdmi.plan import StepPlan
+    noise = torch.randn_like(x0)
+    t = torch.randint(0, 1000, (B,), device=dev)
+    plan = StepPlan(lambda: tr.step(x0, noise, t, text, mask, mask_keep=keep), dev)
+    for _ in range(3):
+        plan.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        plan.replay()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"native plan: host issue {1e3 * (t1 - t0) / n:.2f} ms/step, wall {1e3 * (t2 - t0) / n:.2f} ms/step")
     os.environ["SDMI_WG_STREAM"] = "1"
     cap = CapturedTrainStep(tr, x0, text, empty, mask, B)
     for _ in range(3):

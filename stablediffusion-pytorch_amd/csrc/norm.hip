@@ -148,10 +148,27 @@ __device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, f
                                            bool dup = false) {
   __shared__ float acc[NT][2];
   const int t = threadIdx.x;
-  const int nbg = max(1, NT / cw);
+  const int nthr = min((int)blockDim.x, NT);  // the single-pass kernels run 64 .. 1024 threads
+  if (cw > nthr) {  // narrow workgroup, wide strip: one thread per channel, all batch rows in order
+    for (int ch = t; ch < cw; ch += blockDim.x) {
+      float x1 = 0.f, x2 = 0.f;
+      for (int b = 0; b < a.nb; ++b) {
+        const float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
+        x1 += ld_coherent(rp);
+        x2 += ld_coherent(rp + 1);
+      }
+      const int c = c0 + ch;
+      if (c < c_store) {
+        if (o1) o1[c] = x1;
+        if (o2) o2[c] = dup ? x1 : x2;
+      }
+    }
+    return;
+  }
+  const int nbg = max(1, nthr / cw);
   const int ch = t % cw, bg = t / cw;
   float x1 = 0.f, x2 = 0.f;
-  if (t < NT && bg < nbg && t < nbg * cw) {
+  if (t < nthr && bg < nbg && t < nbg * cw) {
     // issue 8 rows' coherent loads before summing them: the sum then waits once per batch of loads instead of
     // once per load (a dependent chain of cross-XCD round trips otherwise)
     for (int b0 = bg; b0 < a.nb; b0 += 8 * nbg) {
@@ -172,7 +189,7 @@ __device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, f
       }
     }
   }
-  if (t < NT) {
+  if (t < nthr) {
     acc[t][0] = x1;
     acc[t][1] = x2;
   }
@@ -408,13 +425,29 @@ __device__ __forceinline__ void small_reduce(const float* u, const float* v, int
   __syncthreads();
 }
 
-// grid (nchunks, B): y = act(GroupNorm(x)), and the forward table for the backward pass
-template <int NTH>
+// (strip, batch row) of a single-pass workgroup on an (nchunks, B) grid, XCD-aware: workgroups are dispatched
+// round-robin over the 8 XCDs (dispatch id d on XCD d % 8, one 4 MiB L2 each); the logical ids are re-numbered so
+// every XCD owns a contiguous band, strips fastest -- the narrow strips that share the 128-B lines of one batch row's
+// pixel rows then read them through ONE L2 instead of up to eight (bijective for any grid size)
+__device__ __forceinline__ void strip_block(int& strip, int& b) {
+  const int total = gridDim.x * gridDim.y;
+  const int d = blockIdx.y * gridDim.x + blockIdx.x;
+  const int xcd = d & 7, q = total >> 3, r = total & 7;
+  const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (d >> 3);
+  b = l / gridDim.x;
+  strip = l - b * gridDim.x;
+}
+
+// grid (nchunks, B): y = act(GroupNorm(x)), and the forward table for the backward pass. NTH threads, IT pixel rows
+// per thread (P <= IT * (NTH / (strip / 8)))
+template <int NTH, int IT>
 __global__ __launch_bounds__(NTH) void gn_fwd_pass_kernel(StripArgs a, bf16_t* y, int ldy) {
   __shared__ float red[NTH][17];
   __shared__ float s1[NT], s2[NT];
   __shared__ float2 grp[NT];
-  const int b = blockIdx.y, c0 = blockIdx.x * a.CW, cw = min(a.CW, a.C - c0);
+  int strip, b;
+  strip_block(strip, b);
+  const int c0 = strip * a.CW, cw = min(a.CW, a.C - c0);
   const int L = cw >> 3, R = NTH / L, t = threadIdx.x, lane = t % L, r = t / L;
   const int cc = c0 + lane * 8, Cg = a.C / a.G;
   const bool act = r < R;
@@ -424,7 +457,7 @@ __global__ __launch_bounds__(NTH) void gn_fwd_pass_kernel(StripArgs a, bf16_t* y
   const bf16_t* X = a.x + (long long)b * a.P * a.ldx + cc;
   // every row load issued first from a clamped (valid) row, masked afterwards: a guarded load per row would make
   // the compiler wait for each one before the next
-  constexpr int SMALL_IT = small_it(NTH);
+  constexpr int SMALL_IT = IT;
   uint4 rx[SMALL_IT];
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
@@ -442,13 +475,13 @@ __global__ __launch_bounds__(NTH) void gn_fwd_pass_kernel(StripArgs a, bf16_t* y
   }
   small_reduce<NTH>(u, v, cw, red, s1, s2);
   const int ng = cw / Cg;
-  if (t < ng) {
+  for (int gi = t; gi < ng; gi += NTH) {
     double m1 = 0, m2 = 0;
-    for (int c = t * Cg; c < (t + 1) * Cg; ++c) { m1 += s1[c]; m2 += s2[c]; }
+    for (int c = gi * Cg; c < (gi + 1) * Cg; ++c) { m1 += s1[c]; m2 += s2[c]; }
     const double n = (double)a.P * Cg, mu = m1 / n;
     double var = m2 / n - mu * mu;
     if (var < 0) var = 0;
-    grp[t] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)a.eps)));
+    grp[gi] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)a.eps)));
   }
   __syncthreads();
   for (int ch = t; ch < cw; ch += NTH) {
@@ -485,19 +518,22 @@ __global__ __launch_bounds__(NTH) void gn_fwd_pass_kernel(StripArgs a, bf16_t* y
 // grid (nchunks, B): GroupNorm (+SiLU) backward in one pass; dgamma/dbeta by the batch tail. x (and, for the
 // 256-thread form, dy) stay packed in registers; the 1024-thread form re-reads dy in the apply pass (an L2 hit:
 // the workgroup read it moments before) to stay within 128 VGPRs; dz = dy * SiLU'(...) is recomputed there.
-template <int NTH>
+template <int NTH, int IT>
 __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* dx, int lddx, const bf16_t* add,
                                                           int ldadd) {
   __shared__ float red[NTH][17];
   __shared__ float s1[NT], s2[NT];
   __shared__ float2 grp[NT];
   __shared__ float4 stb[NT];  // forward table of the strip
-  const int b = blockIdx.y, c0 = blockIdx.x * a.CW, cw = min(a.CW, a.C - c0);
+  int strip, b;
+  strip_block(strip, b);
+  const int c0 = strip * a.CW, cw = min(a.CW, a.C - c0);
   const int L = cw >> 3, R = NTH / L, t = threadIdx.x, lane = t % L, r = t / L;
   const int cc = c0 + lane * 8, Cg = a.C / a.G;
   const bool act = r < R;
   const long long rb = (long long)b * a.P;
-  constexpr int SMALL_IT = small_it(NTH);
+  constexpr int SMALL_IT = IT;
+  constexpr bool KEEP_DY = IT <= 4 || NTH <= 256;  // else dy is re-read in the apply pass (VGPR budget)
   uint4 rx[SMALL_IT], rg[SMALL_IT];  // all row loads in flight first
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
@@ -529,15 +565,15 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
   small_reduce<NTH>(u, v, cw, red, s1, s2);
   const int ng = cw / Cg;
   const float inv_n = 1.0f / ((float)a.P * Cg);
-  if (t < ng) {
+  for (int gi = t; gi < ng; gi += NTH) {
     float A = 0.f, Bc = 0.f;
-    for (int ch = t * Cg; ch < (t + 1) * Cg; ++ch) {
+    for (int ch = gi * Cg; ch < (gi + 1) * Cg; ++ch) {
       A += a.gamma[c0 + ch] * s1[ch];
       Bc += a.gamma[c0 + ch] * s2[ch];
     }
-    const float4 tt = stb[t * Cg];
+    const float4 tt = stb[gi * Cg];
     const float rs = tt.w, mu = tt.z;
-    grp[t] = make_float2(-rs * rs * Bc * inv_n, rs * rs * mu * Bc * inv_n - rs * A * inv_n);
+    grp[gi] = make_float2(-rs * rs * Bc * inv_n, rs * rs * mu * Bc * inv_n - rs * A * inv_n);
   }
   if (a.sum1) {
     for (int ch = t; ch < cw; ch += NTH) {
@@ -554,7 +590,7 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
       if (p < a.P) {
         float xv[8], gv[8], av[8], ov[8];
         unpack8(rx[it], xv);
-        if (NTH == 256) unpack8(rg[it], gv);
+        if (KEEP_DY) unpack8(rg[it], gv);
         else unpack8(*(const uint4*)(a.dy + (rb + p) * a.ldy + cc), gv);
         if (add) {
           unpack8(*(const uint4*)(add + (rb + p) * ldadd + cc), av);
@@ -575,8 +611,96 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
     }
   }
   if (!a.sum1) return;
-  if (!arrive_last(a.ctr + BATCH_CTR + blockIdx.x, a.nb)) return;
+  if (!arrive_last(a.ctr + BATCH_CTR + strip, a.nb)) return;
   batch_tail(a, c0, cw, a.sum1, a.sum2, a.C);
+}
+
+int strip_width(int C, int unit);
+
+// Single-pass launch shape: strip width (whole groups, 8-channel lanes), threads per workgroup, pixel rows per thread.
+struct PassCfg {
+  int cw, nth, it;
+};
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+// Occupancy-first choice: the widest strip that still gives >= SDMI_GN_MIN_WG workgroups (default 1024 = 4 per CU;
+// narrow strips share 128-B lines with their neighbours, which strip_block() keeps on one XCD), else the narrowest
+// strip; per strip the fewest threads with <= 4 pixel rows each (loads in flight per thread), else <= 8.
+// SDMI_GN_LEGACY=1: the round-1 shape (>= 64-channel strips, 256 threads x 10 rows or 1024 x 8).
+bool pick_pass(int B, int P, int C, int G, PassCfg& pc) {
+  if (gn_small_mode() == 0) return false;
+  const int Cg = C / G;
+  static const int legacy = env_int("SDMI_GN_LEGACY", 0), target = env_int("SDMI_GN_MIN_WG", 1024);
+  if (legacy) {
+    pc.cw = strip_width(C, Cg);
+    pc.nth = gn_pass_threads_for(P, pc.cw, (C + pc.cw - 1) / pc.cw, B);
+    pc.it = pc.nth == 256 ? 10 : 8;
+    return pc.nth != 0;
+  }
+  int u = Cg;
+  while (u % 8) u += Cg;
+  static const int NTHS[] = {64, 256, 512, 1024};
+  PassCfg good = {0, 0, 0}, any = {0, 0, 0};
+  long long any_wg = 0;
+  for (int cw = u; cw <= NT && cw - u < C; cw += u) {
+    const int L = cw / 8;
+    PassCfg c = {0, 0, 0};
+    for (int lim : {4, 8}) {
+      for (int nth : NTHS) {
+        const int R = nth / L;
+        if (R == 0) continue;
+        const int it = (P + R - 1) / R;
+        if (it <= lim) {
+          c = {cw, nth, it <= 1 ? 1 : it <= 2 ? 2 : it <= 4 ? 4 : 8};
+          break;
+        }
+      }
+      if (c.nth) break;
+    }
+    if (!c.nth) continue;
+    const long long wg = (long long)((C + cw - 1) / cw) * B;
+    if (wg >= target) good = c;  // widest so far with enough workgroups (cw ascends)
+    if (wg > any_wg) {
+      any = c;
+      any_wg = wg;
+    }
+  }
+  const PassCfg best = good.nth ? good : any;
+  if (!best.nth || (C + best.cw - 1) / best.cw > BATCH_CTR) return false;
+  pc = best;
+  return true;
+}
+
+template <int NTH>
+void launch_pass_it(bool bwd, int it, dim3 grid, hipStream_t s, const StripArgs& a, bf16_t* out, int ldo,
+                    const bf16_t* add, int ldadd) {
+#define SDMI_GN_PASS(IT)                                                                                  \
+  if (bwd) sdmi_rt::launch(gn_bwd_pass_kernel<NTH, IT>, grid, dim3(NTH), 0, s, a, out, ldo, add, ldadd); \
+  else sdmi_rt::launch(gn_fwd_pass_kernel<NTH, IT>, grid, dim3(NTH), 0, s, a, out, ldo);                 \
+  return;
+  switch (it) {
+    case 1: SDMI_GN_PASS(1)
+    case 2: SDMI_GN_PASS(2)
+    case 4: SDMI_GN_PASS(4)
+    case 8: SDMI_GN_PASS(8)
+    default:
+      if constexpr (NTH == 256) { SDMI_GN_PASS(10) }
+  }
+#undef SDMI_GN_PASS
+}
+
+void launch_pass(bool bwd, const PassCfg& pc, dim3 grid, hipStream_t s, const StripArgs& a, bf16_t* out, int ldo,
+                 const bf16_t* add = nullptr, int ldadd = 0) {
+  switch (pc.nth) {
+    case 64: launch_pass_it<64>(bwd, pc.it, grid, s, a, out, ldo, add, ldadd); break;
+    case 256: launch_pass_it<256>(bwd, pc.it, grid, s, a, out, ldo, add, ldadd); break;
+    case 512: launch_pass_it<512>(bwd, pc.it, grid, s, a, out, ldo, add, ldadd); break;
+    default: launch_pass_it<1024>(bwd, pc.it, grid, s, a, out, ldo, add, ldadd); break;
+  }
 }
 
 struct ApplyArgs {
@@ -738,17 +862,12 @@ extern "C" int sdmi_gn_stats(const void* x, int ldx, int B, int P, int C, int G,
 extern "C" int sdmi_gn_fwd(const void* x, int ldx, void* y, int ldy, int B, int P, int C, int G, float eps,
                            const float* gamma, const float* beta, int silu, float* ws, float* table, sdmi_stream_t stream) {
   if (C % 8 || G <= 0 || C % G) return -1;
-  const int cw = strip_width(C, C / G);
-  const int nth = gn_pass_threads_for(P, cw, (C + cw - 1) / cw, B);
-  if (nth) {
+  PassCfg pc;
+  if (pick_pass(B, P, C, G, pc)) {
     StripArgs a = {};
     a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.eps = eps; a.silu = silu;
-    a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table; a.CW = cw;
-    const dim3 grid((C + cw - 1) / cw, B);
-    if (nth == 256)
-      sdmi_rt::launch(gn_fwd_pass_kernel<256>, grid, dim3(256), 0, (hipStream_t)stream, a, (bf16_t*)y, ldy);
-    else
-      sdmi_rt::launch(gn_fwd_pass_kernel<1024>, grid, dim3(1024), 0, (hipStream_t)stream, a, (bf16_t*)y, ldy);
+    a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table; a.CW = pc.cw;
+    launch_pass(false, pc, dim3((C + pc.cw - 1) / pc.cw, B), (hipStream_t)stream, a, (bf16_t*)y, ldy);
     SDMI_CHECK_LAUNCH();
     return 0;
   }
@@ -778,21 +897,18 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   StripArgs r = {};
   r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy; r.tab = (const float4*)table;
   r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.gamma = gamma; r.out_tab = (float4*)table2_ws;
-  r.CW = strip_width(C, C / G);
-  const int nch = (C + r.CW - 1) / r.CW;
-  if (r.CW > NT || nch > BATCH_CTR) return -2;
   r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
-  if (const int nth = gn_pass_threads_for(P, r.CW, nch, B)) {  // single pass
+  PassCfg pc;
+  if (pick_pass(B, P, C, G, pc)) {  // single pass
+    r.CW = pc.cw;
     if (dgamma && !(r.ctr = counter_slot())) return -4;
-    if (nth == 256)
-      sdmi_rt::launch(gn_bwd_pass_kernel<256>, dim3(nch, B), dim3(256), 0, s, r, (bf16_t*)dx, lddx,
-                         (const bf16_t*)addend, ldadd);
-    else
-      sdmi_rt::launch(gn_bwd_pass_kernel<1024>, dim3(nch, B), dim3(1024), 0, s, r, (bf16_t*)dx, lddx,
-                         (const bf16_t*)addend, ldadd);
+    launch_pass(true, pc, dim3((C + pc.cw - 1) / pc.cw, B), s, r, (bf16_t*)dx, lddx, (const bf16_t*)addend, ldadd);
     SDMI_CHECK_LAUNCH();
     return 0;
   }
+  r.CW = strip_width(C, C / G);
+  const int nch = (C + r.CW - 1) / r.CW;
+  if (r.CW > NT || nch > BATCH_CTR) return -2;
   const int ps = pick_psplit(nch, B, P);
   r.part = part_base(ws, B, C);
   if ((dgamma || ps > 1) && !(r.ctr = counter_slot())) return -4;

@@ -24,7 +24,12 @@ def relerr(a, b):
 
 
 @pytest.mark.parametrize("B,H,C,G,silu", [(2, 8, 64, 32, True), (3, 16, 384, 32, True), (2, 4, 768, 32, False),
-                                          (1, 32, 96, 32, True)])
+                                          (1, 32, 96, 32, True),
+                                          # single-pass shapes of the B=32 step: 1024-thread 24-channel strips (C=384 at
+                                          # 32^2), 8-channel strips (C=256), 64-thread workgroups (4^2), ragged P
+                                          (32, 32, 384, 32, True), (32, 32, 256, 32, False), (32, 4, 768, 32, True),
+                                          (4, 30, 384, 32, True), (32, 16, 512, 32, True),
+                                          (1024, 2, 512, 32, True)])  # 256-channel strips on 64 threads
 def test_groupnorm_fwd_bwd(B, H, C, G, silu):
     k = K()
     torch.manual_seed(0)
@@ -33,35 +38,38 @@ def test_groupnorm_fwd_bwd(B, H, C, G, silu):
     gamma = torch.randn(C, device="cuda") * 0.1 + 1
     beta = torch.randn(C, device="cuda") * 0.1
     dy = bf(torch.randn(B, P, C, device="cuda"))
-    xr = x.float().permute(0, 2, 1).clone().requires_grad_(True)  # (B, C, P)
-    gr = gamma.clone().requires_grad_(True)
-    br = beta.clone().requires_grad_(True)
+    # reference on the CPU in float64: aten's ROCm group_norm backward returns wrong weight / bias gradients for
+    # batches >= 256 on this image (measured: half the per-channel sums; the CPU kernels agree with ours)
+    xr = x.double().cpu().permute(0, 2, 1).clone().requires_grad_(True)  # (B, C, P)
+    gr = gamma.double().cpu().requires_grad_(True)
+    br = beta.double().cpu().requires_grad_(True)
     yr = F.group_norm(xr, G, gr, br, eps=1e-5)
     if silu:
         yr = F.silu(yr)
-    yr.backward(dy.float().permute(0, 2, 1))
+    yr.backward(dy.double().cpu().permute(0, 2, 1))
+    xg, gg, bg_, yref = xr.grad.float().cuda(), gr.grad.float().cuda(), br.grad.float().cuda(), yr.detach().float().cuda()
     x2 = x.view(B * P, C)
     tab = k.gn_stats(x2, B, P, C, G, gamma, beta)
     y = torch.empty_like(x2)
     k.gn_apply(x2, tab, B, P, C, silu, y)
-    assert relerr(y.view(B, P, C).permute(0, 2, 1), yr.detach()) < 1e-2
+    assert relerr(y.view(B, P, C).permute(0, 2, 1), yref) < 1e-2
     dx = torch.empty_like(x2)
     dg = torch.empty(C, device="cuda")
     db = torch.empty(C, device="cuda")
     k.gn_bwd(x2, dy.view(B * P, C), dx, tab, gamma, B, P, C, G, silu, dg, db)
-    assert relerr(dx.view(B, P, C).permute(0, 2, 1), xr.grad) < 2e-2
-    assert relerr(dg, gr.grad) < 1e-2
-    assert relerr(db, br.grad) < 1e-2
+    assert relerr(dx.view(B, P, C).permute(0, 2, 1), xg) < 2e-2
+    assert relerr(dg, gg) < 1e-2
+    assert relerr(db, bg_) < 1e-2
     # gn_fwd (single pass for P <= 256, stats + apply beyond): same output and table
     y2 = torch.empty_like(x2)
     tab2 = k.gn_fwd(x2, B, P, C, G, gamma, beta, silu, y2)
-    assert relerr(y2.view(B, P, C).permute(0, 2, 1), yr.detach()) < 1e-2
+    assert relerr(y2.view(B, P, C).permute(0, 2, 1), yref) < 1e-2
     assert relerr(tab2, tab) < 1e-4
     # in-place backward (dx aliases dy) with an addend, as the resnet blocks call it
     add = bf(torch.randn(B * P, C, device="cuda"))
     buf = dy.view(B * P, C).clone()
     k.gn_bwd(x2, buf, buf, tab2, gamma, B, P, C, G, silu, None, None, addend=add)
-    assert relerr(buf.view(B, P, C).permute(0, 2, 1), xr.grad + add.float().view(B, P, C).permute(0, 2, 1)) < 2e-2
+    assert relerr(buf.view(B, P, C).permute(0, 2, 1), xg + add.float().view(B, P, C).permute(0, 2, 1)) < 2e-2
 
 
 @pytest.mark.parametrize("B,Hh,N,S,d", [(2, 16, 64, 64, 8), (2, 16, 256, 256, 24), (1, 16, 16, 77, 32),
