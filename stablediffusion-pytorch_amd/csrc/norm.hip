@@ -404,20 +404,42 @@ int gn_pass_threads_for(int P, int cw, int nch, int B) {
   return (nth == 1024 && (long long)nch * B < gn_pass_min_wg()) ? 0 : nth;
 }
 
-// per-channel sums of u (and v) over the workgroup's rows -> s1/s2[cw] in LDS (red: [NTH][17] scratch)
+// per-channel sums of u (and v) over the workgroup's rows -> s1/s2[cw] in LDS (red: [NTH][17] scratch), in two
+// fixed-order stages so no thread sums more than ~8 + NTH / cw partials: (1) thread j sums a contiguous segment of
+// ~8 rows of channel j % cw (segment j / cw), (2) one thread per channel sums the segments
 template <int NTH>
 __device__ __forceinline__ void small_reduce(const float* u, const float* v, int cw, float (*red)[17], float* s1,
                                              float* s2) {
+  __shared__ float seg[NTH][2];
   const int t = threadIdx.x, L = cw >> 3, R = NTH / L;
 #pragma unroll
   for (int e = 0; e < 8; ++e) { red[t][e] = u[e]; red[t][8 + e] = v[e]; }
   __syncthreads();
-  for (int ch = t; ch < cw; ch += NTH) {
-    const int l = ch >> 3, e = ch & 7;
+  const int S = max(1, min(R, NTH / cw));  // segments per channel
+  const int RS = (R + S - 1) / S;          // rows per segment
+  for (int j = t; j < S * cw; j += NTH) {  // S * cw <= NTH unless the strip is wider than the workgroup (S = 1)
+    const int ch = j % cw, sg = j / cw, l = ch >> 3, e = ch & 7;
+    const int r1 = min(R, (sg + 1) * RS);
     float x1 = 0.f, x2 = 0.f;
-    for (int rr = 0; rr < R; ++rr) {
+    for (int rr = sg * RS; rr < r1; ++rr) {
       x1 += red[rr * L + l][e];
       x2 += red[rr * L + l][8 + e];
+    }
+    if (S > 1) {
+      seg[j][0] = x1;
+      seg[j][1] = x2;
+    } else {
+      s1[ch] = x1;
+      s2[ch] = x2;
+    }
+  }
+  __syncthreads();
+  if (S == 1) return;
+  for (int ch = t; ch < cw; ch += NTH) {
+    float x1 = 0.f, x2 = 0.f;
+    for (int sg = 0; sg < S; ++sg) {
+      x1 += seg[sg * cw + ch][0];
+      x2 += seg[sg * cw + ch][1];
     }
     s1[ch] = x1;
     s2[ch] = x2;
@@ -627,14 +649,14 @@ int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 
-// Occupancy-first choice: the widest strip that still gives >= SDMI_GN_MIN_WG workgroups (default 1024 = 4 per CU;
+// Occupancy-first choice: the widest strip that still gives >= SDMI_GN_MIN_WG workgroups (default 512 = 2 per CU, measured best of 512 / 1024 / 2048;
 // narrow strips share 128-B lines with their neighbours, which strip_block() keeps on one XCD), else the narrowest
 // strip; per strip the fewest threads with <= 4 pixel rows each (loads in flight per thread), else <= 8.
 // SDMI_GN_LEGACY=1: the round-1 shape (>= 64-channel strips, 256 threads x 10 rows or 1024 x 8).
 bool pick_pass(int B, int P, int C, int G, PassCfg& pc) {
   if (gn_small_mode() == 0) return false;
   const int Cg = C / G;
-  static const int legacy = env_int("SDMI_GN_LEGACY", 0), target = env_int("SDMI_GN_MIN_WG", 1024);
+  static const int legacy = env_int("SDMI_GN_LEGACY", 0), target = env_int("SDMI_GN_MIN_WG", 512);
   if (legacy) {
     pc.cw = strip_width(C, Cg);
     pc.nth = gn_pass_threads_for(P, pc.cw, (C + pc.cw - 1) / pc.cw, B);

@@ -76,7 +76,7 @@ class DDPMTrainer:
         self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes) if self.world > 1 or force_reducer
                         else None)
         if self.reducer is not None and getattr(self.engine, "side", None) is not None:
-            self.reducer.producers.append(self.engine.side)
+            self.reducer.producers.extend(getattr(self.engine, "sides", None) or [self.engine.side])
         self._progress = None
         self.main_stream = None
         if self.device.type == "cuda" and os.environ.get("SDMI_MAIN_PRIORITY", "0") == "1":
