@@ -24,11 +24,16 @@ def timeit(fn, iters=20):
 def main():
     dev = "cuda"
     bf = torch.bfloat16
-    for (B, H, N, S, d) in ((32, 16, 1024, 1024, 24), (32, 16, 1024, 1024, 8), (32, 16, 1024, 77, 24),
-                            (32, 16, 256, 256, 32), (32, 16, 64, 64, 48), (32, 9, 256, 256, 32)):
+    shapes = ((32, 16, 1024, 1024, 16), (32, 16, 1024, 1024, 24), (32, 16, 1024, 77, 16), (32, 16, 1024, 77, 24),
+              (32, 16, 256, 256, 24), (32, 16, 256, 256, 32), (32, 16, 64, 64, 32), (32, 16, 64, 64, 48),
+              (32, 16, 16, 16, 48), (32, 9, 256, 256, 32))
+    if len(sys.argv) > 1:  # one shape index (for per-kernel rocprof runs)
+        shapes = (shapes[int(sys.argv[1])],)
+    for (B, H, N, S, d) in shapes:
         C = H * d
-        q = torch.randn(B * N, C, device=dev).to(bf)
-        k = torch.randn(B * S, C, device=dev).to(bf)
+        amp = float(os.environ.get("ATTN_AMP", "1"))  # input scale (score magnitude)
+        q = (torch.randn(B * N, C, device=dev) * amp).to(bf)
+        k = (torch.randn(B * S, C, device=dev) * amp).to(bf)
         v = torch.randn(B * S, C, device=dev).to(bf)
         o = torch.empty(B * N, C, device=dev, dtype=bf)
         lse = [None]
