@@ -54,6 +54,18 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     print(f"native plan: host issue {1e3 * (t1 - t0) / n:.2f} ms/step, wall {1e3 * (t2 - t0) / n:.2f} ms/step")
+    # the loops above saturate the HIP queue (the host blocks once ~1 step is in flight): the host cost of ONE step is
+    # its enqueue time from an idle GPU (median of 5), well inside the step's device time
+    def one(fn):
+        ts = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - a)
+            torch.cuda.synchronize()
+        return 1e3 * sorted(ts)[2]
+    print(f"single step from idle: eager enqueue {one(step):.2f} ms, native plan enqueue {one(plan.replay):.2f} ms")
     os.environ["SDMI_WG_STREAM"] = "1"
     cap = CapturedTrainStep(tr, x0, text, empty, mask, B)
     for _ in range(3):
