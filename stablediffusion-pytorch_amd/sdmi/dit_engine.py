@@ -21,7 +21,7 @@ import torch
 from . import _lib
 from . import kernels as K
 from . import plan
-from .unet_engine import PackPlan, contiguous_run
+from .unet_engine import PackPlan, UNetEngine, _WaitingParams, contiguous_run
 
 
 def dit_layout(cfg, im_channels=4):
@@ -97,7 +97,11 @@ class DiTEngine:
             raise ValueError("attention head_dim must be a multiple of 8 and <= 64")
         if L["text"] and (L["D"] // L["heads"]) % 8:
             raise ValueError("cross-attention head dim (hidden_size / num_heads) must be a multiple of 8")
-        self.P = params
+        # optimizer / pack pipeline (trainer): chunk -> event the current stream still has to wait for before it reads
+        # the chunk's parameters or packed weights (same protocol as the UNet engine)
+        self._pending = {}
+        self._key_chunk = {}
+        self.P = _WaitingParams(params, self)
         self.Gd = grads
         self.im_channels = im_channels
         self.device = next(iter(params.values())).device
@@ -175,7 +179,14 @@ class DiTEngine:
         return contiguous_run(self.P, [q + "k_proj.bias", q + "v_proj.bias"], (2 * self.L["D"],))
 
     def W(self, name):
+        if self._pending:
+            self._need(self.pack.view_chunk.get(name, 0))
         return self.pack.view(name)
+
+    # forward-ordered optimizer chunks (sdmi.trainer): the UNet engine's protocol
+    set_chunks = UNetEngine.set_chunks
+    _need = UNetEngine._need
+    _need_all = UNetEngine._need_all
 
     def refresh_weights(self):
         if self.pack.stale():
@@ -400,6 +411,7 @@ class DiTEngine:
         if grads is not None:
             self.Gd = grads
         assert self.Gd is not None, "engine built without gradient buffers"
+        self._need_all()  # the optimizer chunks read the gradient buffers the backward is about to overwrite
         self._wg_next = 0
         L, P = self.L, self.P
         st = ctx["st"]

@@ -86,9 +86,11 @@ class DDPMTrainer:
         # forward-ordered chunks; after the (global) clip, Adam + EMA + packing run chunk by chunk on the engine's
         # side stream, each chunk ending in an event that the engine waits for only where the forward first reads
         # one of that chunk's parameters or packed weights (UNet engine; SDMI_OPT_CHUNKS=1 disables it).
-        nchunks = int(os.environ.get("SDMI_OPT_CHUNKS", "6"))
+        # DiT: the forward's first GEMM (every layer's adaLN table) needs the largest chunk at once, so pipelining
+        # measured no gain there (4.00 ms/step unchunked vs 4.04-4.07 at 6 chunks): SDMI_DIT_OPT_CHUNKS, default 1
+        nchunks = int(os.environ.get("SDMI_DIT_OPT_CHUNKS", "1") if base == "dit" else os.environ.get("SDMI_OPT_CHUNKS", "6"))
         self.opt_ranges = None
-        if nchunks > 1 and base != "dit" and getattr(self.engine, "side", None) is not None:
+        if nchunks > 1 and getattr(self.engine, "side", None) is not None:
             self.opt_ranges, key_chunk = self.store.forward_chunks(nchunks)
             self.engine.set_chunks(key_chunk)
             self.opt_events = [torch.cuda.Event() for _ in self.opt_ranges]
