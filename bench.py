@@ -58,8 +58,15 @@ def kernel_name(tag, info):
     if v == 0:
         return f"gemm_kernel<{a}, {b}>"
     return f"gemm_dma_kernel<{a}, {b}, {v}, {tn if v == 2 else 128}>"
-PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
-ROOF_FILE = os.path.join(REPO, "profiles", "r01_roofline_evidence.json")
+def _latest(pattern):
+    """newest round's committed evidence file (profiles/rNN_*)"""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
+    return files[-1] if files else os.path.join(REPO, "profiles", pattern.replace("r*", "r01"))
+
+
+PMC_FILE = _latest("r*_pmc_traffic.json")
+ROOF_FILE = _latest("r*_roofline_evidence.json")
 
 
 def pmc_traffic(kernel, unsplit):
@@ -75,10 +82,13 @@ def pmc_traffic(kernel, unsplit):
     except (OSError, KeyError, TypeError, ValueError):
         pass
     try:
-        d = json.load(open(PMC_FILE))[kernel]
+        table = json.load(open(PMC_FILE))
+        # bench-style "gemm_dma_kernel<1, 0, 2, 128>" also names the full instantiation "...<1, 0, 2, 128, 128, ...>"
+        key = kernel if kernel in table else next(k for k in table if k.startswith(kernel[:-1] + ","))
+        d = table[key]
         return (d["read_bytes_per_launch"] + d["write_bytes_per_launch"],
                 "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, all launches of the kernel)")
-    except (OSError, KeyError, TypeError, ValueError):
+    except (OSError, KeyError, TypeError, ValueError, StopIteration):
         return None, None
 
 

@@ -24,11 +24,16 @@ def _grid_z(d):
     return {r["Dispatch_Id"]: int(r["Grid_Size_Z"]) for r in csv.DictReader(open(_trace_csv(d)))}
 
 
+def _match(kernel, name):
+    """bench-style "gemm_dma_kernel<1, 0, 2, 128>" also matches the full instantiation "...<1, 0, 2, 128, 128, ...>""""
+    return kernel in name or (kernel.endswith(">") and kernel[:-1] + "," in name)
+
+
 def main():
     trace, fdir, wdir, kernel = sys.argv[1:5]
     durs = []
     for r in csv.DictReader(open(_trace_csv(trace))):
-        if kernel not in r["Kernel_Name"]:
+        if not _match(kernel, r["Kernel_Name"]):
             continue
         if int(r["Grid_Size_Z"]) == 1:
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
@@ -39,7 +44,7 @@ def main():
         gz = _grid_z(d)
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if r["Counter_Name"] == cname and kernel in r["Kernel_Name"] and gz.get(r["Dispatch_Id"]) == 1:
+                if r["Counter_Name"] == cname and _match(kernel, r["Kernel_Name"]) and gz.get(r["Dispatch_Id"]) == 1:
                     vals.append(float(r["Counter_Value"]) * 1024 * mul)
         out[cname.lower() + "_bytes_per_launch"] = sum(vals) / len(vals) if vals else None
         out[cname.lower() + "_launches"] = len(vals)
