@@ -49,6 +49,8 @@ class VQVAETrainEngine(UNetEngine):
         self.temb_total = 0
         use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
         self.side = side_stream(self.device) if use_side else None
+        self.sides = [self.side] if self.side is not None else []  # the UNet engine's _wg / _join round-robin
+        self._wg_next = 0
         self._keep = []
         self.dgrad_t = False
         self._build_pack()
