@@ -25,7 +25,7 @@ def _grid_z(d):
 
 
 def _match(kernel, name):
-    """bench-style "gemm_dma_kernel<1, 0, 2, 128>" also matches the full instantiation "...<1, 0, 2, 128, 128, ...>""""
+    """bench-style name gemm_dma_kernel<1, 0, 2, 128> also matches the full instantiation <1, 0, 2, 128, 128, ...>"""
     return kernel in name or (kernel.endswith(">") and kernel[:-1] + "," in name)
 
 
