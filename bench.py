@@ -548,7 +548,10 @@ def main():
         tot_fl = sum(v[0] for v in by.values())
         tot_ms = sum(v[1] for v in by.values())
         dname, d = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
-        use1 = d["n1"] > 0
+        # the unsplit launches (events bracket the kernel alone) represent the kernel when they carry most of its work;
+        # otherwise (e.g. DiT weight gradients, whose few unsplit launches are the tiny t-emb GEMMs) all launches count,
+        # each event then including its split-K reducer (a lower bound on the kernel's own rate)
+        use1 = d["n1"] > 0 and d["fl1"] >= 0.5 * d["fl"]
         dfl, dms, dn = (d["fl1"], d["ms1"], d["n1"]) if use1 else (d["fl"], d["ms"], d["n"])
         traffic, traffic_unit = pmc_traffic(dname, use1)
         roof = {"bound": "mfma", "kernel": f"sdmi {dname} ({d['mode']}: implicit-GEMM conv fwd/dgrad)"
