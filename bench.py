@@ -486,8 +486,8 @@ def main():
         issue = "plan"
     if issue != "eager":
         from sdmi.graph import CapturedTrainStep
-        if issue == "graph" and not is_dit:
-            trainer.engine.side = None  # single-stream capture
+        if issue == "graph":
+            trainer.engine.side = None  # single-stream capture (weight gradients inline)
         cap = CapturedTrainStep(trainer, x0, None if (is_dit or is_uncond) else text, empty, None if is_uncond else mask,
                                 B, generator=gen, drop_p=drop_p,
                                 mode=issue)

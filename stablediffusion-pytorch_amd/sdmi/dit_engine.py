@@ -391,7 +391,7 @@ class DiTEngine:
         """Weight-gradient work on the next side stream, after everything issued so far on the current stream;
         `keep` pins its operands until the backward's final join (the allocator must not hand their memory to the
         current stream while a side stream still reads it)."""
-        if not self.sides:
+        if self.side is None or not self.sides:  # inline (SDMI_WG_STREAM=0, or single-stream graph capture)
             yield
             return
         self._keep.extend(keep)
@@ -403,6 +403,8 @@ class DiTEngine:
 
     def _join(self):
         """The current stream waits for all weight-gradient work issued so far."""
+        if self.side is None:
+            return
         for side in self.sides:
             plan.wait_stream(torch.cuda.current_stream(self.device), side)
 

@@ -1042,6 +1042,8 @@ class UNetEngine:
 
     def _join(self):
         """The current stream waits for all weight-gradient work issued so far."""
+        if self.side is None:  # inline weight gradients (SDMI_WG_STREAM=0, or single-stream graph capture)
+            return
         for side in self.sides:
             plan.wait_stream(torch.cuda.current_stream(self.device), side)
 
