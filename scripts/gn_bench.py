@@ -33,6 +33,7 @@ for (H, C) in [(32, 256), (32, 384), (32, 768), (32, 128), (16, 512), (16, 384),
     tab = k.gn_fwd(x, B, P, C, G, gamma, beta, True, y)
     tf = timeit(lambda: k.gn_fwd(x, B, P, C, G, gamma, beta, True, y))
     tb = timeit(lambda: k.gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, True, dg, db))
+    tn = timeit(lambda: k.gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, True, None, None))  # no dgamma / dbeta tail
     n = B * P * C
-    print(f"{H:3d}^2 C={C:5d}: fwd {tf:7.1f} us {4 * n / tf / 1e6:6.2f} TB/s | bwd {tb:7.1f} us {6 * n / tb / 1e6:6.2f} TB/s",
-          flush=True)
+    print(f"{H:3d}^2 C={C:5d}: fwd {tf:7.1f} us {4 * n / tf / 1e6:6.2f} TB/s | bwd {tb:7.1f} us {6 * n / tb / 1e6:6.2f} TB/s"
+          f" | bwd w/o param grads {tn:7.1f} us", flush=True)
