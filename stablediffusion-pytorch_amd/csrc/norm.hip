@@ -556,6 +556,10 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
   const long long rb = (long long)b * a.P;
   constexpr int SMALL_IT = IT;
   constexpr bool KEEP_DY = IT <= 4 || NTH <= 256;  // else dy is re-read in the apply pass (VGPR budget)
+  // IT <= 4: dz = dy * SiLU'(x a + s) of the reduction pass is kept (fp32) for the apply pass instead of being
+  // recomputed there (the SiLU derivative is an exp + a reciprocal per element: ~1/3 of the kernel's VALU work)
+  constexpr bool KEEP_DZ = KEEP_DY && IT <= 4;
+  float dzk[KEEP_DZ ? SMALL_IT * 8 : 1];
   uint4 rx[SMALL_IT], rg[SMALL_IT];  // all row loads in flight first
 #pragma unroll
   for (int it = 0; it < SMALL_IT; ++it) {
@@ -579,6 +583,7 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
         const float4 tb = stb[lane * 8 + e];
         float dz = gv[e];
         if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb.x, tb.y));
+        if constexpr (KEEP_DZ) dzk[it * 8 + e] = dz;
         u[e] += dz;
         v[e] = fmaf(dz, (xv[e] - tb.z) * tb.w, v[e]);
       }
@@ -612,8 +617,14 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
       if (p < a.P) {
         float xv[8], gv[8], av[8], ov[8];
         unpack8(rx[it], xv);
-        if (KEEP_DY) unpack8(rg[it], gv);
-        else unpack8(*(const uint4*)(a.dy + (rb + p) * a.ldy + cc), gv);
+        if constexpr (KEEP_DZ) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) gv[e] = dzk[it * 8 + e];
+        } else if (KEEP_DY) {
+          unpack8(rg[it], gv);
+        } else {
+          unpack8(*(const uint4*)(a.dy + (rb + p) * a.ldy + cc), gv);
+        }
         if (add) {
           unpack8(*(const uint4*)(add + (rb + p) * ldadd + cc), av);
         } else {
@@ -625,7 +636,7 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
           const float4 tb = stb[lane * 8 + e];
           const float2 qo = grp[(lane * 8 + e) / Cg];
           float dz = gv[e];
-          if (a.silu) dz *= silu_grad_f(fmaf(xv[e], tb.x, tb.y));
+          if (!KEEP_DZ && a.silu) dz *= silu_grad_f(fmaf(xv[e], tb.x, tb.y));
           ov[e] = av[e] + fmaf(tb.x, dz, fmaf(qo.x, xv[e], qo.y));
         }
         *(uint4*)(dx + (rb + p) * lddx + cc) = pack8(ov);
