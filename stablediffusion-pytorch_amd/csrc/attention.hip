@@ -336,7 +336,11 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
     f32x4 p[2][4], ds[2][4];
 #pragma unroll
     for (int qb = 0; qb < 4; ++qb) {
-      p[0][qb] = p[1][qb] = ds[0][qb] = ds[1][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      const int qi = qb * 16 + (lane >> 4) * 4;
+      const f32x4 nL = *(const f32x4*)&sLD[cur][0][qi], nD = *(const f32x4*)&sLD[cur][1][qi];
+      // dP accumulates on top of -delta: the MFMA yields dP - delta directly (no per-element subtraction)
+      p[0][qb] = p[1][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      ds[0][qb] = ds[1][qb] = nD;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         s16x8 qa = frag_rows<DP>(sQ, qb * 16, ks * 32, lane);
@@ -346,15 +350,13 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
         ds[0][qb] = mfma(oa, vf[0][ks], ds[0][qb]);
         ds[1][qb] = mfma(oa, vf[1][ks], ds[1][qb]);
       }
-      const int qi = qb * 16 + (lane >> 4) * 4;
-      const f32x4 nL = *(const f32x4*)&sLD[cur][0][qi], nD = *(const f32x4*)&sLD[cur][1][qi];
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
         f32x2_t p0 = __builtin_elementwise_fma(lo2(p[g][qb]), cc, lo2(nL));
         f32x2_t p1 = __builtin_elementwise_fma(hi2(p[g][qb]), cc, hi2(nL));
         p0 = (f32x2_t){fast_exp2(p0[0]), fast_exp2(p0[1])};
         p1 = (f32x2_t){fast_exp2(p1[0]), fast_exp2(p1[1])};
-        const f32x2_t d0 = p0 * (lo2(ds[g][qb]) + lo2(nD)), d1 = p1 * (hi2(ds[g][qb]) + hi2(nD));
+        const f32x2_t d0 = p0 * lo2(ds[g][qb]), d1 = p1 * hi2(ds[g][qb]);
         p[g][qb] = (f32x4){p0[0], p0[1], p1[0], p1[1]};
         ds[g][qb] = (f32x4){d0[0], d0[1], d1[0], d1[1]};
       }
@@ -460,7 +462,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       f32x4 sc[2], dp[2];
-      sc[0] = sc[1] = dp[0] = dp[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      sc[0] = sc[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      // dP accumulates on top of -delta (per query = per lane): the MFMA yields dP - delta directly
+      dp[0] = (f32x4){ndlt[0][0], ndlt[0][0], ndlt[0][0], ndlt[0][0]};
+      dp[1] = (f32x4){ndlt[1][0], ndlt[1][0], ndlt[1][0], ndlt[1][0]};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         s16x8 ka = frag_rows<DP>(sK, kb * 16, ks * 32, lane);
@@ -483,7 +488,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
           if (2 >= lim) p1[0] = 0.f;
           if (3 >= lim) p1[1] = 0.f;
         }
-        const f32x2_t d0 = p0 * (lo2(dp[g]) + ndlt[g]), d1 = p1 * (hi2(dp[g]) + ndlt[g]);
+        const f32x2_t d0 = p0 * lo2(dp[g]), d1 = p1 * hi2(dp[g]);
         ds[g][kb] = (f32x4){d0[0], d0[1], d1[0], d1[1]};
       }
     }
