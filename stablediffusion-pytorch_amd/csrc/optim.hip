@@ -3,6 +3,7 @@
 // (train_ddpm_cond_celebhq_multi_gpu.py:362-378; torch.optim.Adam defaults, EMA decay 0.9999).
 // All control state (step, loss scale, growth tracker, found-inf) lives on the device so a whole
 // training step can be replayed as one hipGraph without host synchronisation.
+#include <cstdint>
 #include <cstdlib>
 
 #include "common.h"
@@ -71,6 +72,24 @@ __global__ void norm_finalize_kernel(const float* partial, int n, float max_norm
   }
 }
 
+// one element of Adam + EMA (torch.optim.Adam, non-fused, non-amsgrad; ema as below)
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, float& e, bool ema, float gs, float b1,
+                                         float b2, float eps, float step_size, float bc2s, float ema_decay,
+                                         float ema_alpha) {
+  const float gi = g * gs;
+  const float mi = m + (1.f - b1) * (gi - m);  // lerp(m, g, 1 - b1)
+  const float vi = v * b2 + (1.f - b2) * gi * gi;
+  m = mi;
+  v = vi;
+  const float denom = sqrtf(vi) / bc2s + eps;
+  p = p - step_size * (mi / denom);
+  // ema.mul_(decay).add_(p, alpha=1 - decay) (:376-378): a rounded product, then add_'s fused alpha * p + self;
+  // alpha is the reference's own fp32 value of (1 - decay) computed in double (1e-4f, not 1 - 0.9999f)
+  if (ema) e = __builtin_fmaf(ema_alpha, p, mul_ieee(e, ema_decay));
+}
+
+// VEC = 4: 16-B loads / stores of all five streams (host checks the alignment), scalar tail in block 0
+template <int VEC>
 __global__ void adam_ema_kernel(float* p, const float* g, float* m, float* v, float* ema, long long n, const float* state,
                                 float lr, float b1, float b2, float eps, float ema_decay, float ema_alpha) {
   if (state[5] != 0.f) return;  // skipped step
@@ -79,19 +98,33 @@ __global__ void adam_ema_kernel(float* p, const float* g, float* m, float* v, fl
   const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
   const float step_size = (float)(lr / bc1);
   const float bc2s = (float)sqrt(bc2);
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
-    float gi = g[i] * gs;
-    float mi = m[i] + (1.f - b1) * (gi - m[i]);  // lerp(m, g, 1 - b1)
-    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    float denom = sqrtf(vi) / bc2s + eps;
-    float pi = p[i] - step_size * (mi / denom);
-    p[i] = pi;
-    // ema.mul_(decay).add_(p, alpha=1 - decay) (:376-378): a rounded product, then add_'s fused alpha * p + self;
-    // alpha is the reference's own fp32 value of (1 - decay) computed in double (1e-4f, not 1 - 0.9999f)
-    if (ema) ema[i] = __builtin_fmaf(ema_alpha, pi, mul_ieee(ema[i], ema_decay));
+  const long long nv = n / VEC;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < nv; i += (long long)gridDim.x * NT) {
+    if constexpr (VEC == 4) {
+      float4 pi = ((const float4*)p)[i], mi = ((const float4*)m)[i], vi = ((const float4*)v)[i];
+      const float4 gi = ((const float4*)g)[i];
+      float4 ei = ema ? ((const float4*)ema)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool he = ema != nullptr;
+      adam_one(pi.x, gi.x, mi.x, vi.x, ei.x, he, gs, b1, b2, eps, step_size, bc2s, ema_decay, ema_alpha);
+      adam_one(pi.y, gi.y, mi.y, vi.y, ei.y, he, gs, b1, b2, eps, step_size, bc2s, ema_decay, ema_alpha);
+      adam_one(pi.z, gi.z, mi.z, vi.z, ei.z, he, gs, b1, b2, eps, step_size, bc2s, ema_decay, ema_alpha);
+      adam_one(pi.w, gi.w, mi.w, vi.w, ei.w, he, gs, b1, b2, eps, step_size, bc2s, ema_decay, ema_alpha);
+      ((float4*)p)[i] = pi;
+      ((float4*)m)[i] = mi;
+      ((float4*)v)[i] = vi;
+      if (ema) ((float4*)ema)[i] = ei;
+    } else {
+      float e = ema ? ema[i] : 0.f;
+      adam_one(p[i], g[i], m[i], v[i], e, ema != nullptr, gs, b1, b2, eps, step_size, bc2s, ema_decay, ema_alpha);
+      if (ema) ema[i] = e;
+    }
   }
+  if (VEC > 1 && blockIdx.x == 0)
+    for (long long i = nv * VEC + threadIdx.x; i < n; i += NT) {
+      float e = ema ? ema[i] : 0.f;
+      adam_one(p[i], g[i], m[i], v[i], e, ema != nullptr, gs, b1, b2, eps, step_size, bc2s, ema_decay, ema_alpha);
+      if (ema) ema[i] = e;
+    }
 }
 }  // namespace
 
@@ -118,10 +151,21 @@ extern "C" int sdmi_adam_ema(float* params, const float* grads, float* m, float*
     max_blocks = e ? atoll(e) : 8192;
     if (max_blocks < 1) max_blocks = 8192;
   }
-  long long blocks = (n + NT - 1) / NT;
+  static int allow_vec = -1;  // SDMI_ADAM_VEC=0: scalar streams (A/B runs)
+  if (allow_vec < 0) {
+    const char* e = getenv("SDMI_ADAM_VEC");
+    allow_vec = e ? atoi(e) != 0 : 1;
+  }
+  const bool vec = allow_vec && ((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)m | (uintptr_t)v | (uintptr_t)ema) & 15) == 0);
+  long long blocks = (n / (vec ? 4 : 1) + NT - 1) / NT;
   if (blocks > max_blocks) blocks = max_blocks;
-  sdmi_rt::launch(adam_ema_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v, ema,
-                     n, state, lr, b1, b2, eps, ema_decay, ema_alpha);
+  if (blocks < 1) blocks = 1;
+  if (vec)
+    sdmi_rt::launch(adam_ema_kernel<4>, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v,
+                    ema, n, state, lr, b1, b2, eps, ema_decay, ema_alpha);
+  else
+    sdmi_rt::launch(adam_ema_kernel<1>, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v,
+                    ema, n, state, lr, b1, b2, eps, ema_decay, ema_alpha);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
