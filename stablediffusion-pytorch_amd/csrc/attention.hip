@@ -23,6 +23,7 @@
 //            with P recomputed from the forward's log-sum-exp and delta = rowsum(dO * O).
 #include "common.h"
 #include "../../include/sdmi.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -155,7 +156,10 @@ using Ragged = std::true_type;
 // =============================================================================================
 // forward
 // =============================================================================================
-template <int DT>
+// ONES (d % 16 == 8: the last output tile has free padded columns): column d of every valid V row is 1, so the
+// PV MFMA accumulates the softmax row sum into o[g][DT-1] (tile row 8: lane group 2, element 0) -- no per-score
+// VALU row-sum adds in the loop; the sum is of the bf16 P the MFMA consumes, i.e. exactly what O accumulated
+template <int DT, bool ONES>
 __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
@@ -181,8 +185,20 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   }
 
   uint4 rk[Tile<DP>::CPT], rv[Tile<DP>::CPT];
+  // ONES: the 8-column chunk of V starting at column d (all padding) becomes {1, 0, ..., 0} on valid key rows
+  auto fetch_v = [&](int row0) __attribute__((always_inline)) {
+    tile_fetch<DP>(rv, V, a.ldv, row0, a.S, h * a.d, a.d);
+    if constexpr (ONES) {
+      constexpr int CPR = DP / 8;
+#pragma unroll
+      for (int j = 0; j < Tile<DP>::CPT; ++j) {
+        const int c = threadIdx.x + j * NT, rr = c / CPR, ch = c - rr * CPR;
+        if (ch * 8 == a.d && row0 + rr < a.S) rv[j].x = 0x3F80u;  // bf16 1.0 in the chunk's first element
+      }
+    }
+  };
   tile_fetch<DP>(rk, K, a.ldk, 0, a.S, h * a.d, a.d);
-  tile_fetch<DP>(rv, V, a.ldv, 0, a.S, h * a.d, a.d);
+  fetch_v(0);
   tile_store<DP>(smem, rk);
   tile_store<DP>(smem + Tile<DP>::ELEMS, rv);
   __syncthreads();
@@ -191,7 +207,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
     const bool more = k0 + TILE < a.S;
     if (more) {
       tile_fetch<DP>(rk, K, a.ldk, k0 + TILE, a.S, h * a.d, a.d);
-      tile_fetch<DP>(rv, V, a.ldv, k0 + TILE, a.S, h * a.d, a.d);
+      fetch_v(k0 + TILE);
     }
     const bf16_t* sK = smem + cur * 2 * Tile<DP>::ELEMS;
     const bf16_t* sV = sK + Tile<DP>::ELEMS;
@@ -233,11 +249,13 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
         f32x2_t x1 = __builtin_elementwise_fma(hi2(s[g][kb]), cc, nm);
         x0 = (f32x2_t){fast_exp2(x0[0]), fast_exp2(x0[1])};
         x1 = (f32x2_t){fast_exp2(x1[0]), fast_exp2(x1[1])};
-        ls += x0;
-        ls += x1;
+        if constexpr (!ONES) {
+          ls += x0;
+          ls += x1;
+        }
         s[g][kb] = (f32x4){x0[0], x0[1], x1[0], x1[1]};
       }
-      l[g] = fmaf(l[g], alpha, ls[0] + ls[1]);
+      if constexpr (!ONES) l[g] = fmaf(l[g], alpha, ls[0] + ls[1]);
 #pragma unroll
       for (int t = 0; t < DT; ++t) o[g][t] *= alpha;
       pf[g][0] = pack_acc(s[g][0], s[g][1]);
@@ -264,7 +282,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   if (k0 < a.S) step(k0, Ragged{});
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    const float lt = xsum4(l[g]);
+    // ONES: the row sum sits in lane group 2 of the last output tile; every lane of the query column takes it
+    const float lt = ONES ? __shfl(o[g][DT - 1][0], 32 + (lane & 15)) : xsum4(l[g]);
     if (myq[g] < a.N) {
       const float inv = 1.f / lt;
       bf16_t* O = a.out + ((long long)b * a.N + myq[g]) * a.ldo + h * a.d;
@@ -543,12 +562,22 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
   if (rc) return rc;
   dim3 grid((N + ROWS - 1) / ROWS, B * H);
   hipStream_t s = (hipStream_t)stream;
-  switch ((d + 15) / 16) {
-    case 1: sdmi_rt::launch(attn_fwd_kernel<1>, grid, dim3(NT), 0, s, a); break;
-    case 2: sdmi_rt::launch(attn_fwd_kernel<2>, grid, dim3(NT), 0, s, a); break;
-    case 3: sdmi_rt::launch(attn_fwd_kernel<3>, grid, dim3(NT), 0, s, a); break;
-    default: sdmi_rt::launch(attn_fwd_kernel<4>, grid, dim3(NT), 0, s, a); break;
+  static int ones_ok = -1;  // SDMI_ATTN_ONES=0: VALU row sums for every head dim (A/B runs)
+  if (ones_ok < 0) {
+    const char* e = getenv("SDMI_ATTN_ONES");
+    ones_ok = e ? atoi(e) != 0 : 1;
   }
+  const bool ones = ones_ok && d % 16 == 8;
+#define SDMI_ATTN_FWD(DT)                                                          \
+  if (ones) sdmi_rt::launch(attn_fwd_kernel<DT, true>, grid, dim3(NT), 0, s, a);  \
+  else sdmi_rt::launch(attn_fwd_kernel<DT, false>, grid, dim3(NT), 0, s, a);
+  switch ((d + 15) / 16) {
+    case 1: SDMI_ATTN_FWD(1) break;
+    case 2: SDMI_ATTN_FWD(2) break;
+    case 3: SDMI_ATTN_FWD(3) break;
+    default: SDMI_ATTN_FWD(4) break;
+  }
+#undef SDMI_ATTN_FWD
   SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -72,8 +72,10 @@ def test_groupnorm_fwd_bwd(B, H, C, G, silu):
     assert relerr(buf.view(B, P, C).permute(0, 2, 1), xg + add.float().view(B, P, C).permute(0, 2, 1)) < 2e-2
 
 
+# d = 8, 24, 40 take the forward's ones-column row sum (d % 16 == 8), incl. ragged N and S = 77
 @pytest.mark.parametrize("B,Hh,N,S,d", [(2, 16, 64, 64, 8), (2, 16, 256, 256, 24), (1, 16, 16, 77, 32),
-                                        (2, 4, 1024, 1024, 16), (2, 16, 64, 77, 48), (1, 8, 100, 100, 64)])
+                                        (2, 4, 1024, 1024, 16), (2, 16, 64, 77, 48), (1, 8, 100, 100, 64),
+                                        (1, 16, 40, 77, 24), (1, 4, 33, 70, 40)])
 def test_attention_fwd_bwd(B, Hh, N, S, d):
     k = K()
     torch.manual_seed(1)
@@ -94,6 +96,9 @@ def test_attention_fwd_bwd(B, Hh, N, S, d):
     o = torch.empty(B * N, C, device="cuda", dtype=torch.bfloat16)
     lse = k.attn_fwd(q, kk, v, o, B, Hh, N, S, d)
     assert relerr(heads(o, N), orf.detach()) < 2e-2
+    # base-2 log-sum-exp of the scaled scores, [B*H][N]
+    lse_ref = (qr.detach() @ kr.detach().transpose(-1, -2) / math.sqrt(d)).logsumexp(-1) * math.log2(math.e)
+    assert (lse.view(-1)[:B * Hh * N] - lse_ref.reshape(-1)).abs().max().item() < 2e-2
     dq = torch.empty_like(q)
     dk = torch.empty_like(kk)
     dv = torch.empty_like(v)
