@@ -3,14 +3,15 @@
 Every parameter (and its gradient) is a view into one flat fp32 buffer, ordered so that
   * the backward pass produces gradients roughly front-to-back (buckets can be all-reduced while
     the rest of the backward runs),
-  * all t_emb_layers weights / biases form single contiguous runs (one GEMM covers them),
+  * all t_emb_layers weights / biases form single contiguous runs (one GEMM covers them), and so do all
+    context_proj weights / biases (one forward GEMM of the text context, one weight-gradient GEMM),
   * the optimizer is one elementwise pass over three flat buffers.
 Keys are the reference's state-dict keys (models/unet_cond_base.py, models/blocks.py)."""
 import re
 
 import torch
 
-from .unet_engine import layout, resnet_list
+from .unet_engine import cross_list, layout, resnet_list
 
 
 def param_label(key):
@@ -18,6 +19,8 @@ def param_label(key):
     m = re.match(r"(downs|mids|ups)\.(\d+)\.", key)
     if ".t_emb_layers." in key and key.endswith(".weight"):
         return "time"  # one GEMM for all t_emb_layers weights, after every block
+    if ".context_proj." in key:
+        return "time"  # one GEMM for all context_proj weights and biases, after every block
     if m:
         return f"{m.group(1)}.{m.group(2)}"
     if key.startswith("norm_out") or key.startswith("conv_out"):
@@ -34,7 +37,10 @@ def flat_order(cfg, keys):
     res = resnet_list(L)
     tw = [f"{p}.t_emb_layers.{l}.1.weight" for (p, l, ci, co) in res]
     tb = [f"{p}.t_emb_layers.{l}.1.bias" for (p, l, ci, co) in res]
-    special = set(tw) | set(tb)
+    cross = cross_list(L) if L["text"] else []
+    cw = [f"{p}.context_proj.{l}.weight" for (p, l, c) in cross]
+    cb = [f"{p}.context_proj.{l}.bias" for (p, l, c) in cross]
+    special = set(tw) | set(tb) | set(cw) | set(cb)
 
     def rank(k):
         m = re.match(r"(downs|mids|ups)\.(\d+)\.", k)
@@ -52,7 +58,7 @@ def flat_order(cfg, keys):
     rest = sorted([k for k in keys if k not in special], key=lambda k: (rank(k), keys.index(k)))
     tail = [k for k in rest if rank(k) == 10_000]
     body = [k for k in rest if rank(k) != 10_000]
-    return body + tw + tb + tail
+    return body + tw + tb + cw + cb + tail
 
 
 class FlatStore:

@@ -66,6 +66,20 @@ def resnet_list(L):
     return out
 
 
+def cross_list(L):
+    """(block prefix, layer, channels) of every cross-attention, in forward order."""
+    nd = len(L["down"]) - 1
+    out = []
+    for i in range(nd):
+        out += [(f"downs.{i}", l, L["down"][i + 1]) for l in range(L["n_down"])]
+    for i in range(len(L["mid"]) - 1):
+        out += [(f"mids.{i}", l, L["mid"][i + 1]) for l in range(L["n_mid"])]
+    for j, i in enumerate(reversed(range(nd))):
+        cout = L["down"][i - 1] if i != 0 else L["conv_out"]
+        out += [(f"ups.{j}", l, cout) for l in range(L["n_up"])]
+    return out
+
+
 class PackPlan:
     """bf16 GEMM-layout copies of the fp32 weights, refreshed by one batched pack launch."""
 
@@ -311,6 +325,14 @@ class UNetEngine:
             self.temb_off[(p, l)] = off
             off += cout
         self.temb_total = off
+        # every cross-attention's context_proj (blocks.py context_proj: Linear(text_embed_dim, C)) reads the same
+        # text context: their weights are one packed [sum C][ctx_dim] matrix (contiguous fp32 runs in the flat
+        # store), so the forward is ONE GEMM into a [B*S][sum C] buffer and the weight gradient one GEMM at the end
+        self.ctx_off, off = {}, 0
+        for (p, l, c) in (cross_list(L) if L["text"] else []):
+            self.ctx_off[(p, l)] = off
+            off += c
+        self.ctx_total = off
         # weight-gradient work (wgrad GEMMs, bias sums) runs on a side stream, overlapped with the
         # data-gradient chain of the backward on the current stream
         use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
@@ -352,6 +374,12 @@ class UNetEngine:
         for (p, l, cin, cout) in self.resnets:
             w = P[f"{p}.t_emb_layers.{l}.1.weight"]
             pk.add(None, w, cout, L["T"], L["T"], 1, 1, L["T"], 1, 0, 0, into="temb_all", row0=self.temb_off[(p, l)])
+        if self.ctx_total:  # concatenated context_proj weight [sum C][ctx_dim]
+            D = L["ctx_dim"]
+            pk.reserve("ctxp_all", self.ctx_total, D)
+            for (p, l, c) in self._cross_layers():
+                w = P[f"{p}.context_proj.{l}.weight"]
+                pk.add(None, w, c, D, D, 1, 1, D, 1, 0, 0, into="ctxp_all", row0=self.ctx_off[(p, l)])
         for (p, l, cin, cout) in self.resnets:
             self._pk_resnet(pk, p, l, cin, cout)
         nd = len(L["down"]) - 1
@@ -364,7 +392,6 @@ class UNetEngine:
                 if L["text"]:
                     lin(pk, f"{p}.cross_attentions.{l}.in_proj_weight")
                     lin(pk, f"{p}.cross_attentions.{l}.out_proj")
-                    lin(pk, f"{p}.context_proj.{l}")
             if L["down_sample"][i]:
                 self._pk_down(pk, f"{p}.down_sample_conv")
         for i in range(len(L["mid"]) - 1):
@@ -375,7 +402,6 @@ class UNetEngine:
                 if L["text"]:
                     lin(pk, f"{p}.cross_attentions.{l}.in_proj_weight")
                     lin(pk, f"{p}.cross_attentions.{l}.out_proj")
-                    lin(pk, f"{p}.context_proj.{l}")
         for j, i in enumerate(reversed(range(nd))):
             p = f"ups.{j}"
             for l in range(L["n_up"]):
@@ -384,7 +410,6 @@ class UNetEngine:
                 if L["text"]:
                     lin(pk, f"{p}.cross_attentions.{l}.in_proj_weight")
                     lin(pk, f"{p}.cross_attentions.{l}.out_proj")
-                    lin(pk, f"{p}.context_proj.{l}")
             if L["down_sample"][i]:
                 self._pk_up(pk, f"{p}.up_sample_conv")
         conv(pk, "conv_out", opad=8)
@@ -563,7 +588,8 @@ class UNetEngine:
         bias_all = self._temb_bias()
         K.linear(stemb, self.W("temb_all"), temb_all, bias=bias_all)
         self.dtemb_all = None
-        tape.append((self._bwd_time, dict(e=e, h1=h1, s1=s1, temb=temb, stemb=stemb, B=B, cls=cls)))
+        time_c = dict(e=e, h1=h1, s1=s1, temb=temb, stemb=stemb, B=B, cls=cls)
+        tape.append((self._bwd_time, time_c))
         st["temb_all"] = temb_all
 
         ctx = None
@@ -575,8 +601,12 @@ class UNetEngine:
                                                          txt.shape[2], K._stream()), "cast")
             st["S"] = S
         st["ctx"] = ctx
+        time_c["ctx"] = ctx
         if ctx is not None and self.ctx_stream is not None:
             self._ctx_ahead(st, B)
+        elif ctx is not None:  # every context_proj in one GEMM (inline context branch)
+            st["cp_all"] = self._new(B * st["S"], self.ctx_total)
+            K.linear(ctx, self.W("ctxp_all"), st["cp_all"], bias=self._ctx_bias(self.P))
 
         # ---- down blocks (blocks.py:111-146) ----
         cur, cur_name = skip0, "skip0"
@@ -662,17 +692,7 @@ class UNetEngine:
     # ------------------------------------------------------------------------------------------
     def _cross_layers(self):
         """(block prefix, layer, channels) of every cross-attention, in forward order."""
-        L = self.L
-        nd = len(L["down"]) - 1
-        out = []
-        for i in range(nd):
-            out += [(f"downs.{i}", l, L["down"][i + 1]) for l in range(L["n_down"])]
-        for i in range(len(L["mid"]) - 1):
-            out += [(f"mids.{i}", l, L["mid"][i + 1]) for l in range(L["n_mid"])]
-        for j, i in enumerate(reversed(range(nd))):
-            cout = L["down"][i - 1] if i != 0 else L["conv_out"]
-            out += [(f"ups.{j}", l, cout) for l in range(L["n_up"])]
-        return out
+        return cross_list(self.L)
 
     def _wait_chunk_on(self, stream, c):
         ev = self._pending.get(c)  # (not popped: the current stream still waits for it where it reads the chunk)
@@ -680,31 +700,45 @@ class UNetEngine:
             plan.wait_event(stream, ev)
 
     def _ctx_ahead(self, st, B):
-        """The context branch of every cross-attention -- context_proj, then the k|v rows of the attention's packed
+        """The context branch of every cross-attention -- context_proj (all layers in ONE GEMM of the text context
+        against the concatenated [sum C][ctx_dim] weight), then the k|v rows of each attention's packed
         in-projection (blocks.py:139-140 -> nn.MultiheadAttention) -- depends only on the text context: issue all of
-        it up front on a stream of its own, each layer waiting for the optimizer chunk that updates its weights, so
-        its ~30 small launches run beside the forward's main chain instead of on it. The buffers are allocated on
-        the current stream (which waits for each layer's event before its attention reads them)."""
+        it up front on a stream of its own, each GEMM waiting for the optimizer chunks that update its weights, so
+        its launches run beside the forward's main chain instead of on it. The buffers are allocated on the current
+        stream (which waits for each layer's event before its attention reads them)."""
         P, S, ctx = self.P, st["S"], st["ctx"]
         cs = self.ctx_stream
+        cp_all = self._new(B * S, self.ctx_total)
         work = []
         for (p, l, C) in self._cross_layers():
-            work.append((p, l, C, self._new(B * S, C), self._new(B * S, 2 * C)))
+            work.append((p, l, C, self._new(B * S, 2 * C)))
         plan.wait_stream(cs, torch.cuda.current_stream(self.device))
         pre = {}
         with torch.cuda.stream(cs):
-            for (p, l, C, cp, kv) in work:
-                mk, ck = f"{p}.cross_attentions.{l}", f"{p}.context_proj.{l}"
-                for name in (ck + "#f", mk + ".in_proj_weight#f"):
-                    self._wait_chunk_on(cs, self.pack.view_chunk.get(name, 0))
-                for key in (ck + ".bias", mk + ".in_proj_bias"):
-                    self._wait_chunk_on(cs, self._key_chunk.get(key, 0))
-                K.linear(ctx, self.pack.view(ck + "#f"), cp, bias=P.raw(ck + ".bias"))
+            self._wait_chunk_on(cs, self.pack.view_chunk.get("ctxp_all", 0))
+            for c in sorted({self._key_chunk.get(k, 0) for k in self._ctx_bias_keys()}):
+                self._wait_chunk_on(cs, c)
+            # raw parameter reads: the waits above are on the context stream; the main stream keeps its own
+            K.linear(ctx, self.pack.view("ctxp_all"), cp_all, bias=self._ctx_bias({k: P.raw(k) for k in self._ctx_bias_keys()}))
+            for (p, l, C, kv) in work:
+                mk = f"{p}.cross_attentions.{l}"
+                self._wait_chunk_on(cs, self.pack.view_chunk.get(mk + ".in_proj_weight#f", 0))
+                self._wait_chunk_on(cs, self._key_chunk.get(mk + ".in_proj_bias", 0))
+                off = self.ctx_off[(p, l)]
+                cp = cp_all[:, off:off + C]
                 K.linear(cp, self.pack.view(mk + ".in_proj_weight#f")[C:], kv, bias=P.raw(mk + ".in_proj_bias")[C:])
                 ev = torch.cuda.Event()
                 plan.record_event(ev, cs)
                 pre[(p, l)] = (cp, kv, ev)
+        st["cp_all"] = cp_all
         st["ctx_pre"] = pre
+
+    def _ctx_bias_keys(self):
+        return [f"{p}.context_proj.{l}.bias" for (p, l, c) in self._cross_layers()]
+
+    def _ctx_bias(self, params):
+        """The context_proj biases are one contiguous fp32 vector of the flat store (layer order)."""
+        return contiguous_run(params, self._ctx_bias_keys(), (self.ctx_total,))
 
     def _temb_bias(self):
         """The t_emb_layers biases are one contiguous fp32 vector of the flat store (forward order)."""
@@ -814,8 +848,8 @@ class UNetEngine:
                 cp, kv, ev = pre[(p, l)]
                 plan.wait_event(torch.cuda.current_stream(self.device), ev)
             else:
-                cp = self._new(B * S, C)
-                K.linear(ctx, self.W(ck + "#f"), cp, bias=P[ck + ".bias"])
+                off = self.ctx_off[(p, l)]
+                cp = st["cp_all"][:, off:off + C]
                 kv = self._new(B * S, 2 * C)
                 K.linear(cp, Win[C:], kv, bias=bin_[C:])
             c["lse"] = K.attn_fwd(q, kv[:, :C], kv[:, C:], o, B, Hh, N, S, d)
@@ -858,15 +892,17 @@ class UNetEngine:
             K.attn_bwd(c["q"], kv[:, :C], kv[:, C:], c["o"], do, c["lse"], dq, dkv[:, :C], dkv[:, C:], B, Hh, N, S, d)
             # the context branch (kv in-projection -> context_proj) ends at the text input, which takes no gradient:
             # its data gradient only feeds the context_proj weight gradient, so all of it runs on the side stream
-            dcp = self._new(B * S, C)
-            with self._wg(dq, dkv, dcp):
+            # this layer's columns of the shared context_proj output gradient (one weight-gradient GEMM for every
+            # layer at the end of the backward, _bwd_time)
+            off = self.ctx_off[(c["p"], c["l"])]
+            dcp = self.dcp_all[:, off:off + C]
+            with self._wg(dq, dkv):
                 K.linear_wgrad(dq, c["a"], gW[:C], bias_grad=gb[:C])
                 K.linear_wgrad(dkv, c["cp"], gW[C:], bias_grad=gb[C:])
                 if WinT is not None:
                     K.linear_dgrad_t(dkv, WinT[:, C:], dcp)
                 else:
                     K.linear_dgrad(dkv, Win[C:], dcp)
-                K.linear_wgrad(dcp, c["ctx"], self.g(c["ck"] + ".weight"), bias_grad=self.g(c["ck"] + ".bias"))
             if WinT is not None:
                 K.linear_dgrad_t(dq, WinT[:, :C], da)
             else:
@@ -973,6 +1009,10 @@ class UNetEngine:
         P, L = self.P, self.L
         B, T = c["B"], L["T"]
         self._join()  # dtemb_all is filled by the resnets' side-stream bias sums
+        if c.get("ctx") is not None:  # every context_proj weight / bias gradient in one GEMM (contiguous runs)
+            with self._wg(self.dcp_all):
+                K.linear_wgrad(self.dcp_all, c["ctx"], self._ctx_grad_view(),
+                               bias_grad=self._ctx_bias(self.Gd))
         d_all = self.dtemb_all
         # t_emb_layers weights are contiguous in the gradient store: one GEMM for all of them
         K.linear_wgrad(d_all, c["stemb"], self.temb_grad_all)
@@ -1059,6 +1099,9 @@ class UNetEngine:
         self.dpred = dpred
         self.dtemb_all = self._new(B, self.temb_total)
         self.temb_grad_all = self._temb_grad_view()
+        self.dcp_all = self._new(B * st["S"], self.ctx_total) if st.get("ctx") is not None else None
+        if self.dcp_all is not None:
+            self._keep.append(self.dcp_all)  # written by side-stream dgrads, read by the final GEMM
         grads = ctx["grads"]
         tape = ctx["tape"]
         self._need_all()  # the optimizer chunks read the gradient buffers the backward is about to overwrite
@@ -1073,6 +1116,11 @@ class UNetEngine:
         self._keep = []
         self.dpred = None
         K.PHASE = ""
+
+    def _ctx_grad_view(self):
+        """The context_proj weight gradients are one contiguous [sum C][ctx_dim] region of the flat store."""
+        return contiguous_run(self.Gd, [f"{p}.context_proj.{l}.weight" for (p, l, c) in self._cross_layers()],
+                              (self.ctx_total, self.L["ctx_dim"]))
 
     def _temb_grad_view(self):
         """The t_emb_layers weight gradients are one contiguous [sum C][T] region of the flat store."""
