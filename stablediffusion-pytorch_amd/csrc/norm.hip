@@ -667,7 +667,11 @@ int env_int(const char* name, int dflt) {
 bool pick_pass(int B, int P, int C, int G, PassCfg& pc) {
   if (gn_small_mode() == 0) return false;
   const int Cg = C / G;
-  static const int legacy = env_int("SDMI_GN_LEGACY", 0), target = env_int("SDMI_GN_MIN_WG", 512);
+  // 32x32 and larger images (P >= 1024): 256 workgroups of wider strips measured better in isolation (32^2 C=384
+  // fwd 19.7 -> 15.2 us, bwd 35.1 -> 33.7 us; C=128 bwd 18.2 -> 16.6 us; others equal), smaller images keep 512
+  static const int legacy = env_int("SDMI_GN_LEGACY", 0), target_small = env_int("SDMI_GN_MIN_WG", 512),
+                   target_big = env_int("SDMI_GN_MIN_WG_32", 256);
+  const int target = P >= 1024 ? target_big : target_small;
   if (legacy) {
     pc.cw = strip_width(C, Cg);
     pc.nth = gn_pass_threads_for(P, pc.cw, (C + pc.cw - 1) / pc.cw, B);
