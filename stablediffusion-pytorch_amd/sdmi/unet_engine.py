@@ -719,7 +719,8 @@ class UNetEngine:
             for c in sorted({self._key_chunk.get(k, 0) for k in self._ctx_bias_keys()}):
                 self._wait_chunk_on(cs, c)
             # raw parameter reads: the waits above are on the context stream; the main stream keeps its own
-            K.linear(ctx, self.pack.view("ctxp_all"), cp_all, bias=self._ctx_bias({k: P.raw(k) for k in self._ctx_bias_keys()}))
+            raw = {k: P.raw(k) for k in self._ctx_bias_keys()}
+            K.linear(ctx, self.pack.view("ctxp_all"), cp_all, bias=self._ctx_bias(raw))
             for (p, l, C, kv) in work:
                 mk = f"{p}.cross_attentions.{l}"
                 self._wait_chunk_on(cs, self.pack.view_chunk.get(mk + ".in_proj_weight#f", 0))
