@@ -58,6 +58,15 @@ def test_flat_store_order_and_contiguous_runs():
     tw = [f"{p}.t_emb_layers.{l}.1.weight" for (p, l, ci, co) in res]
     v = contiguous_run(st.g, tw, (sum(co for (_, _, _, co) in res), 512))
     assert v.shape[0] == sum(co for (_, _, _, co) in res)
+    # every context_proj weight / bias: one contiguous run each (one forward GEMM, one weight-gradient GEMM), in
+    # cross-attention order, labelled "time" (final only after the whole backward)
+    from sdmi.unet_engine import cross_list
+    cr = cross_list(layout(cfg))
+    tot = sum(c for (_, _, c) in cr)
+    w = contiguous_run(st.g, [f"{p}.context_proj.{l}.weight" for (p, l, c) in cr], (tot, 512))
+    b = contiguous_run(st.g, [f"{p}.context_proj.{l}.bias" for (p, l, c) in cr], (tot,))
+    assert w.shape == (tot, 512) and b.shape == (tot,) and len(cr) == 14
+    assert all(param_label(f"{p}.context_proj.{l}.weight") == "time" for (p, l, c) in cr)
     # head parameters first, then up blocks (backward order)
     assert param_label(st.order[0]) == "head"
     assert st.order.index("ups.2.attentions.0.in_proj_weight") < st.order.index("downs.0.attentions.0.in_proj_weight")
