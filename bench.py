@@ -131,6 +131,37 @@ def cpu_model():
     return f"{name}, {os.cpu_count()} logical CPUs visible"
 
 
+def cpu_threads():
+    """Threads for the CPU baseline: the physical cores of this process's CPU affinity set (sibling hyperthreads
+    counted once, from /sys/devices/system/cpu/cpu*/topology), capped by the CPU share the host grants this job -- a
+    cgroup CPU quota (/sys/fs/cgroup/cpu.max) and the per-GPU thread share the GPU pool exports as OMP_NUM_THREADS
+    (16 per GPU: a 1-GPU job must not spread onto the other GPUs' cores). Returns (threads, facts)."""
+    aff = sorted(os.sched_getaffinity(0))
+    cores = set()
+    for c in aff:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            cores.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            cores.add(("cpu", c))
+    phys = len(cores)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    share = os.environ.get("OMP_NUM_THREADS")
+    share = int(share) if share and share.isdigit() and int(share) > 0 else None
+    threads = phys
+    for cap in (quota, share):
+        if cap is not None:
+            threads = min(threads, max(1, int(cap)))
+    return threads, {"affinity_logical_cpus": len(aff), "affinity_physical_cores": phys, "cgroup_cpu_quota": quota,
+                     "omp_num_threads_share": share}
+
+
 def timed_cpu(fn, warmup=1, timed=3):
     """Median wall time of `timed` calls of fn after `warmup` calls (1 warm-up + 3 timed)."""
     for _ in range(warmup):
@@ -144,7 +175,7 @@ def timed_cpu(fn, warmup=1, timed=3):
 
 
 def _cpu_result(per, ts, threads, what):
-    return dict(value=1.0 / per, unit="steps/s", cores=threads, kind="port", cpu=cpu_model(),
+    return dict(value=1.0 / per, unit="steps/s", cores=threads, kind="port", cpu=cpu_model(), host=cpu_threads()[1],
                 sample=f"{what}; median of {len(ts)} timed steps {per:.2f} s/step (all: "
                        f"{', '.join(f'{t:.2f}' for t in ts)}), torch CPU {torch.__version__} with {threads} threads")
 
@@ -152,7 +183,7 @@ def _cpu_result(per, ts, threads, what):
 def cpu_baseline_dit(cfg, B=32):
     """The DiT oracle's fp32 training step (Model_DiT_12L_train.py:300-375) on the host cores."""
     from oracle import sd_oracle as O, dit_oracle as DO
-    threads = min(16, os.cpu_count() or 1)
+    threads, _ = cpu_threads()
     torch.set_num_threads(threads)
     sd = O.deterministic_state(DO.dit_param_shapes(cfg), seed=0)
     opt = O.AdamState(sd)
@@ -178,7 +209,7 @@ def vqvae_config():
 def cpu_baseline_vqvae(cfg, B=8):
     """The VQVAE oracle's fp32 encode + decode on the host cores."""
     from oracle import sd_oracle as O, vqvae_oracle as VO
-    threads = min(16, os.cpu_count() or 1)
+    threads, _ = cpu_threads()
     torch.set_num_threads(threads)
     sd = O.deterministic_state(VO.vqvae_param_shapes(cfg), seed=0)
     x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1111)) * 2 - 1
@@ -195,7 +226,7 @@ def cpu_baseline(cfg, B=32, uncond=False, small_batch=4):
     """The oracle (CPU fp32 restatement of the reference step) on the host cores: B=32 (the bench workload) and
     B=small_batch, each 1 warm-up + 3 timed, median."""
     from oracle import sd_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads, _ = cpu_threads()
     torch.set_num_threads(threads)
     res = None
     for b in (B, small_batch):
@@ -286,7 +317,7 @@ def cpu_baseline_vqvae_train(cfg, B=8):
     """The VQVAE oracle's fp32 generator step (train_grads: forward, losses, autograd backward) on the host cores;
     3 timed steps, no warm-up (~11 s each)."""
     from oracle import sd_oracle as O, vqvae_oracle as VO
-    threads = min(16, os.cpu_count() or 1)
+    threads, _ = cpu_threads()
     torch.set_num_threads(threads)
     sd = O.deterministic_state(VO.vqvae_param_shapes(cfg), seed=0)
     x = torch.rand(B, 3, 256, 256, generator=torch.Generator().manual_seed(1111)) * 2 - 1
@@ -394,6 +425,24 @@ def main_sample(args, wl, world, rank, device):
         dist.destroy_process_group()
 
 
+def collective_facts(world, device):
+    """N > 1: what the process group itself reports -- backend, its world size, an all-reduce of ones through it (the
+    sum proves every rank took part in a collective on this group), and each rank's device (ordinal, PCI bus, uuid),
+    so a scaling run shows that RCCL saw N ranks on N distinct GPUs."""
+    if world <= 1:
+        return None
+    one = torch.ones(1, device=device)
+    dist.all_reduce(one)
+    props = torch.cuda.get_device_properties(device)
+    mine = {"rank": dist.get_rank(), "device": device.index, "pci_bus_id": getattr(props, "pci_bus_id", None),
+            "pci_domain_id": getattr(props, "pci_domain_id", None), "uuid": str(getattr(props, "uuid", ""))}
+    devs = [None] * world
+    dist.all_gather_object(devs, mine)
+    distinct = len({(d["pci_domain_id"], d["pci_bus_id"], d["uuid"]) for d in devs})
+    return {"backend": dist.get_backend(), "rccl_ranks": dist.get_world_size(),
+            "allreduce_of_ones": one.item(), "devices": devs, "distinct_devices": distinct}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -406,6 +455,9 @@ def main():
                     help="cond-unet (the headline metric, default), uncond-unet (celebhq.yaml), dit (DiT-12L training "
                          "step), vqvae (encode + decode), vqvae-train (VQVAE generator step) or sample (captured DDPM sampling loop)")
     ap.add_argument("--profile-gemm", action="store_true", default=True)
+    ap.add_argument("--grad-wire", default=None, choices=("fp32", "bf16"),
+                    help="N > 1: gradient all-reduce wire format (default fp32 as the reference's DDP; bf16 halves "
+                         "the bytes)")
     ap.add_argument("--issue", default="plan", choices=("plan", "eager", "graph"),
                     help="plan (default): the step recorded once and its native calls replayed (sdmi.plan); eager: "
                          "per-step Python issue; graph: single-stream hipGraph (N == 1)")
@@ -428,6 +480,7 @@ def main():
             dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    collectives = collective_facts(world, device)
 
     from sdmi.trainer import DDPMTrainer, S_LOSS, S_NORM, S_SKIP
     from sdmi import kernels as K
@@ -451,15 +504,16 @@ def main():
         for k, v in init.items():  # the reference zero-initialises adaLN / proj_out: give them random values so
             if v.abs().max() == 0:  # the timed step runs on non-trivial data (zeros clock higher, MI355X DVFS)
                 v.normal_(0.0, 0.02)
-        trainer = DDPMTrainer(cfg, init, device, base="dit", lr=1e-4, ema_decay=None, group=group)
+        trainer = DDPMTrainer(cfg, init, device, base="dit", lr=1e-4, ema_decay=None, group=group,
+                              grad_wire=args.grad_wire)
     elif is_uncond:  # tools/train_ddpm_vqvae.py:76-104: Adam(ldm_lr 5e-6, celebhq.yaml:54), no clip, no EMA
         import models.unet_base as mu
         init = mu.Unet(4, cfg).state_dict()
         trainer = DDPMTrainer(cfg, init, device, base="uncond", lr=5e-6, ema_decay=None, max_grad_norm=float("inf"),
-                              sched=(1000, 0.0015, 0.0195), group=group)
+                              sched=(1000, 0.0015, 0.0195), group=group, grad_wire=args.grad_wire)
     else:
         init = mc.Unet(4, cfg).state_dict()
-        trainer = DDPMTrainer(cfg, init, device, group=group)
+        trainer = DDPMTrainer(cfg, init, device, group=group, grad_wire=args.grad_wire)
     B = args.batch
     x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
     gen = torch.Generator(device=device).manual_seed(1111 + rank)
@@ -522,8 +576,15 @@ def main():
     if args.profile_gemm:
         PROF_STEPS = 3
         K.PROFILE = []
+        tails = []
+        if trainer.reducer is not None:
+            trainer.measure_exchange_tail()
         for _ in range(PROF_STEPS):
             eager_step()
+            if trainer.reducer is not None:
+                torch.cuda.synchronize()
+                tails.append(trainer.exchange_tail_ms())
+        trainer.measure_exchange_tail(False)
         torch.cuda.synchronize()
         prof, K.PROFILE = K.PROFILE, None
         by, per_kernel = {}, {}
@@ -592,6 +653,15 @@ def main():
         "issue": issue,
         "roofline": roof,
     }
+    if world > 1:
+        result["collectives"] = collectives
+        result["grad_wire"] = trainer.grad_wire
+        if args.profile_gemm and tails:
+            # exposed gradient exchange: compute-stream time from the end of the backward (all gradients final) to the
+            # last bucket's all-reduce waited for, eager profiled steps (HIP events), max over ranks
+            tail = torch.tensor([sum(tails) / len(tails)], device=device, dtype=torch.float64)
+            dist.all_reduce(tail, op=dist.ReduceOp.MAX)
+            result["exchange_tail_ms"] = tail.item()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_dit(cfg) if is_dit else cpu_baseline(cfg, uncond=is_uncond)
     if rank == 0:

@@ -123,7 +123,7 @@ int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t workspace_bytes, 
  * Replaces the core of torch nn.MultiheadAttention as called at models/blocks.py:128 (self) and
  * :140 (cross, kv = context_proj(context)): softmax((q / sqrt(d)) k^T) v per head, head h in columns
  * [h*d, h*d+d) of row-major [batch*len][ld] buffers; d % 8 == 0, d <= 64; S (keys) may differ from N.
- * lse: fp32 [B*H][N] (saved for the backward).  Backward: dq, dk, dv (no atomics); delta_ws fp32 [B*H*N].
+ * lse: fp32 [B*H][N], base 2: log2 sum_j 2^(s_ij log2 e) (saved for the backward).  Backward: dq, dk, dv (no atomics); delta_ws fp32 [B*H*N].
  * ------------------------------------------------------------------------------------------- */
 int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* out, int ldo,
                   float* lse, int B, int H, int N, int S, int d, sdmi_stream_t stream);
@@ -267,6 +267,9 @@ int sdmi_pointwise_in(const float* z, int B, int C, int HW, const float* w, cons
  *                   (t_dev), z unused at t == 0, x0 (clamped prediction) optional; decrement_t: t_dev -= 1 after
  *                   the step (capturable sampling loop, no host round trip per step).
  *  sdmi_ddim_prev : DDIMSampler.sample_one_step (:164-182) for alpha_t = abar[t], alpha_prev = abar[t_prev].
+ *  sdmi_ddim_prev_dev: the same DDIM step with the pair read on the device: i = *idx, alpha_t = abar[ts[i]],
+ *                   alpha_prev = abar[tp[i]] (DDIMSampler.forward's time_steps / time_steps_prev, :231-242); advance:
+ *                   afterwards *idx -= 1 and *t_dev = ts[*idx] (the model's timestep) -- a capturable DDIM loop.
  *  sdmi_affine_step: DDPMSampler.sample_one_step (:111-124): out = (c1 x - c2 eps) + sqrt(var) z (z NULL: + 0).
  * ------------------------------------------------------------------------------------------- */
 int sdmi_ddpm_prev(const float* xt, const float* eps, const float* z, long long n, long long* t_dev, const float* betas,
@@ -274,6 +277,9 @@ int sdmi_ddpm_prev(const float* xt, const float* eps, const float* z, long long 
                    sdmi_stream_t stream);
 int sdmi_ddim_prev(const float* xt, const float* eps, const float* noise, long long n, float alpha_t, float alpha_prev,
                    float eta, float* out, sdmi_stream_t stream);
+int sdmi_ddim_prev_dev(const float* xt, const float* eps, const float* noise, long long n, const long long* ts,
+                       const long long* tp, long long* idx, long long* t_dev, const float* abar, float eta, float* out,
+                       int advance, sdmi_stream_t stream);
 int sdmi_affine_step(const float* x, const float* eps, const float* z, long long n, float c1, float c2, float var,
                      float* out, sdmi_stream_t stream);
 
@@ -315,13 +321,19 @@ int sdmi_pack_transpose(const sdmi_tpack_desc* descs_dev, const void* bmap_dev, 
 /* ---------------------------------------------------------------------------------------------
  * Optimizer step over flat fp32 buffers (train_ddpm_cond_celebhq_multi_gpu.py:362-378):
  * GradScaler.unscale_ + clip_grad_norm_(max_norm) + non-finite skip + scaler.update (state on device:
- * float[8] = {norm, coef, scale, growth, step, skip, loss, -}), then Adam (torch defaults) + EMA.
+ * float[8] = {norm, coef, scale, growth, step, skip, loss, dp_loss_flag}), then Adam (torch defaults) + EMA.
  * grad_div = data-parallel world size (gradients arrive summed). growth_interval <= 0: no loss scaler (the
  * plain fp32 VQVAE trainer, train_vqvae_celebhq.py:466): the scale in state[2] is left as is (keep it 1).
+ * skip_if_loss_nonfinite: 0 ignore the loss; 1 a non-finite state[6] skips the step WITHOUT scaler.update()
+ * (:348-352); 2 the same decided by state[7] != 0 (data parallel: the all-reduced sum of every rank's flag, so every
+ * replica skips together). A non-finite gradient norm skips the step and backs the scale off (:366-371).
+ * sdmi_loss_flag: mode 0 *dst = !isfinite(*src) (a rank's flag, e.g. into the all-reduced gradient tail);
+ * mode 1 *dst = (*src != 0) (the summed flag into state[7]).
  * ------------------------------------------------------------------------------------------- */
 size_t sdmi_optim_workspace(void);
 int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws, int growth_interval,
                       int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
+int sdmi_loss_flag(const float* src, float* dst, int mode, sdmi_stream_t stream);
 /* ema_alpha: the fp32 value of (1 - ema_decay) as the caller computes it (the reference passes alpha = 1 - 0.9999
  * from Python doubles, :376-378) */
 int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n, const float* state,

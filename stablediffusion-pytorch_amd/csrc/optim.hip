@@ -31,6 +31,7 @@ __global__ void sumsq_kernel(const float* g, long long n, float* partial) {
 
 // state layout (fp32 unless noted): [0] grad norm (unscaled)  [1] clip coefficient * inv_scale
 // [2] loss scale  [3] growth tracker  [4] step (as float)  [5] found_inf/skip flag  [6] last loss
+// [7] data-parallel non-finite-loss flag (sum over ranks of each rank's flag; skip_if_loss_nonfinite == 2)
 __global__ void norm_finalize_kernel(const float* partial, int n, float max_norm, float* state, int growth_interval,
                                      int skip_if_loss_nonfinite, float grad_div) {
   __shared__ double red[NT];
@@ -47,7 +48,8 @@ __global__ void norm_finalize_kernel(const float* partial, int n, float max_norm
     float inv = 1.0f / (scale * grad_div);  // unscale and average over data-parallel ranks
     float norm = (float)sqrt(red[0]) * inv;  // ||g/scale|| = ||g|| / scale (power-of-two scale: exact)
     state[0] = norm;
-    bool loss_bad = skip_if_loss_nonfinite && !isfinite(state[6]);
+    bool loss_bad = skip_if_loss_nonfinite == 1 ? !isfinite(state[6])
+                    : skip_if_loss_nonfinite == 2 ? state[7] != 0.f : false;
     bool bad = !isfinite(norm) || loss_bad;
     state[5] = bad ? 1.f : 0.f;
     float coef = max_norm / (norm + 1e-6f);
@@ -69,6 +71,14 @@ __global__ void norm_finalize_kernel(const float* partial, int n, float max_norm
         state[4] = state[4] + 1.f;
       }
     }
+  }
+}
+
+// mode 0: *dst = isfinite(*src) ? 0 : 1 (a rank's non-finite-loss flag); mode 1: *dst = (*src != 0) (the summed flag)
+__global__ void loss_flag_kernel(const float* src, float* dst, int mode) {
+  if (threadIdx.x == 0) {
+    const float v = *src;
+    *dst = mode == 0 ? (isfinite(v) ? 0.f : 1.f) : (v != 0.f ? 1.f : 0.f);
   }
 }
 
@@ -138,6 +148,13 @@ extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm
   SDMI_CHECK_LAUNCH();
   sdmi_rt::launch(norm_finalize_kernel, dim3(1), dim3(NT), 0, s, ws, NORM_BLOCKS, max_norm, state, growth_interval,
                      skip_if_loss_nonfinite, grad_div);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_loss_flag(const float* src, float* dst, int mode, sdmi_stream_t stream) {
+  if (!src || !dst || mode < 0 || mode > 1) return -1;
+  sdmi_rt::launch(loss_flag_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, src, dst, mode);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

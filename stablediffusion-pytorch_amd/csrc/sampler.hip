@@ -9,6 +9,8 @@
 //              device-side timestep counter (no host sync per step; the reference syncs on `t == 0`).
 //  ddim_prev : DDIMSampler.sample_one_step (:164-182): x_{t-1} = sqrt(a_prev/a_t) x_t + (sqrt(1 - a_prev -
 //              sigma^2) - sqrt(a_prev (1 - a_t) / a_t)) eps + sigma noise, sigma = eta sqrt(...).
+//  ddim_prev_dev : the same step with (t, t_prev) read from device tables through a device step index, which a
+//              follow-up launch decrements (and the model's timestep scalar with it): a captured DDIM loop.
 //  affine    : DDPMSampler.sample_one_step (:111-124): (c1 x - c2 eps) + sqrt(var) z with host table scalars.
 #include "common.h"
 #include "../../include/sdmi.h"
@@ -68,6 +70,36 @@ __global__ void ddim_prev_kernel(const float* xt, const float* eps, const float*
   }
 }
 
+// DDIM step with its timestep pair read from DEVICE tables (a captured DDIMSampler.forward loop, reference :209-256):
+// step index i = *idx, a_t = abar[ts[i]], a_prev = abar[tp[i]]; the same arithmetic as ddim_prev_kernel, so a replayed
+// step is bit-identical to the eager one given the same noise
+__global__ void ddim_prev_dev_kernel(const float* xt, const float* eps, const float* noise, long long n,
+                                     const long long* ts, const long long* tp, const long long* idx, const float* abar,
+                                     float eta, float* out) {
+#pragma clang fp contract(off)
+  const long long i = *idx;
+  const float at = abar[ts[i]], ap = abar[tp[i]];
+  const float sigma = mul_ieee(eta, sqrt_ieee(mul_ieee(div_ieee(sub_ieee(1.0f, ap), sub_ieee(1.0f, at)),
+                                                     sub_ieee(1.0f, div_ieee(at, ap)))));
+  const float c1 = sqrt_ieee(div_ieee(ap, at));
+  const float c2 = sub_ieee(sqrt_ieee(sub_ieee(sub_ieee(1.0f, ap), mul_ieee(sigma, sigma))),
+                             sqrt_ieee(div_ieee(mul_ieee(ap, sub_ieee(1.0f, at)), at)));
+  for (long long j = (long long)blockIdx.x * NT + threadIdx.x; j < n; j += (long long)gridDim.x * NT) {
+    float v = add_ieee(mul_ieee(c1, xt[j]), mul_ieee(c2, eps[j]));
+    out[j] = add_ieee(v, mul_ieee(sigma, noise ? noise[j] : 0.0f));
+  }
+}
+
+// after a DDIM step: the step index moves down and the model's timestep scalar follows it (ts[i - 1]); a separate
+// single-thread launch ordered after the step on the same stream (every block of the step has read the index)
+__global__ void ddim_advance_kernel(const long long* ts, long long* idx, long long* t_dev) {
+  if (threadIdx.x == 0 && *idx > 0) {
+    const long long i = *idx - 1;
+    *idx = i;
+    if (t_dev) *t_dev = ts[i];
+  }
+}
+
 __global__ void affine_kernel(const float* x, const float* eps, const float* z, long long n, float c1, float c2,
                               float var, float* out) {
 #pragma clang fp contract(off)
@@ -102,6 +134,20 @@ extern "C" int sdmi_ddim_prev(const float* xt, const float* eps, const float* no
   sdmi_rt::launch(ddim_prev_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, xt, eps, noise, n, alpha_t,
                      alpha_prev, eta, out);
   SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_ddim_prev_dev(const float* xt, const float* eps, const float* noise, long long n,
+                                  const long long* ts, const long long* tp, long long* idx, long long* t_dev,
+                                  const float* abar, float eta, float* out, int advance, sdmi_stream_t stream) {
+  if (!xt || !eps || !out || !ts || !tp || !idx || !abar || n <= 0) return -1;
+  sdmi_rt::launch(ddim_prev_dev_kernel, dim3(grid_for(n)), dim3(NT), 0, (hipStream_t)stream, xt, eps, noise, n, ts, tp,
+                  (const long long*)idx, abar, eta, out);
+  SDMI_CHECK_LAUNCH();
+  if (advance) {
+    sdmi_rt::launch(ddim_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ts, idx, t_dev);
+    SDMI_CHECK_LAUNCH();
+  }
   return 0;
 }
 

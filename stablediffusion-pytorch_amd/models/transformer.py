@@ -15,7 +15,7 @@ from models.transformer_layer import TransformerLayer
 from utils.config_utils import (get_config_value, validate_class_config, validate_class_conditional_input,
                                 validate_image_config, validate_image_conditional_input, validate_text_config)
 from sdmi import leaf as LF
-from sdmi.module_glue import EngineHolder, run_denoiser
+from sdmi.module_glue import EngineHolder, invalidate_module, run_denoiser
 
 
 def get_time_embedding(time_steps, temb_dim):
@@ -103,12 +103,18 @@ class DIT(nn.Module):
             assert "text" in cond_input, \
                 "Model initialized with text conditioning but cond_input has no text information"
             text = cond_input["text"]
-        from models.attention import Attention
-        from models.multihead_attention import CustomMultiheadAttention
-        if getattr(self, "sdmi_leaf_path", False) or not LF.engine_ok(
-                self, (DIT, PatchEmbedding, TransformerLayer, Attention, CustomMultiheadAttention)):
+        if getattr(self, "sdmi_leaf_path", False) or not self._sdmi_engine_ok():
             return self._leaf_forward(x, t, text, mask, klass)
         return run_denoiser(self, self._sdmi, x, t, text, mask, klass)
+
+    def _sdmi_engine_ok(self):
+        from models.attention import Attention
+        from models.multihead_attention import CustomMultiheadAttention
+        return LF.engine_ok(self, (DIT, PatchEmbedding, TransformerLayer, Attention, CustomMultiheadAttention))
+
+    def sdmi_invalidate(self):
+        """Repack the bf16 weights at the next forward (after writing parameters through `.data`)."""
+        invalidate_module(self)
 
     def _leaf_forward(self, x, t, text, mask, klass):
         patch_source = x

@@ -6,7 +6,7 @@ import torch.nn as nn
 
 from models.blocks import DownBlock, MidBlock, UpBlockUnet, get_time_embedding  # noqa: F401
 from sdmi import leaf as LF
-from sdmi.module_glue import EngineHolder, run_unet
+from sdmi.module_glue import EngineHolder, invalidate_module, run_unet
 
 
 class Unet(nn.Module):
@@ -49,10 +49,17 @@ class Unet(nn.Module):
         self._sdmi = EngineHolder(self, cfg, "uncond")
 
     def forward(self, x, t):
-        if getattr(self, "sdmi_leaf_path", False) or not LF.engine_ok(self, (Unet, DownBlock, MidBlock, UpBlockUnet)):
+        if getattr(self, "sdmi_leaf_path", False) or not self._sdmi_engine_ok():
             # a swapped leaf: unet_base.py:68-100 leaf by leaf
             from models.unet_cond_base import _leaf_body
             out = LF.call(self.conv_in, x)
             t_emb = LF.call(self.t_proj, LF.time_embedding(t, x.shape[0], self.t_emb_dim, x.device))
             return _leaf_body(self, out, t_emb, None)
         return run_unet(self, self._sdmi, x, t)
+
+    def _sdmi_engine_ok(self):
+        return LF.engine_ok(self, (Unet, DownBlock, MidBlock, UpBlockUnet))
+
+    def sdmi_invalidate(self):
+        """Repack the bf16 weights at the next forward (after writing parameters through `.data`)."""
+        invalidate_module(self)

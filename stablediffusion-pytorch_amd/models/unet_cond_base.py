@@ -15,7 +15,7 @@ from models.blocks import DownBlock, MidBlock, UpBlockUnet, get_time_embedding  
 from utils.config_utils import (get_config_value, validate_class_config, validate_text_config,
                                 validate_image_conditional_input, validate_class_conditional_input)
 from sdmi import leaf as LF
-from sdmi.module_glue import EngineHolder, run_unet
+from sdmi.module_glue import EngineHolder, invalidate_module, run_unet
 
 
 class Unet(nn.Module):
@@ -100,9 +100,16 @@ class Unet(nn.Module):
             assert "text" in cond_input, \
                 "Model initialized with text conditioning but cond_input has no text information"
             text = cond_input["text"]
-        if getattr(self, "sdmi_leaf_path", False) or not LF.engine_ok(self, (Unet, DownBlock, MidBlock, UpBlockUnet)):
+        if getattr(self, "sdmi_leaf_path", False) or not self._sdmi_engine_ok():
             return self._leaf_forward(x, t, text, mask, klass)
         return run_unet(self, self._sdmi, x, t, text, mask, klass)
+
+    def _sdmi_engine_ok(self):
+        return LF.engine_ok(self, (Unet, DownBlock, MidBlock, UpBlockUnet))
+
+    def sdmi_invalidate(self):
+        """Repack the bf16 weights at the next forward (after writing parameters through `.data`)."""
+        invalidate_module(self)
 
     def _leaf_forward(self, x, t, text, mask, klass):
         """unet_cond_base.py:131-183, leaf by leaf (sdmi.leaf.call)."""

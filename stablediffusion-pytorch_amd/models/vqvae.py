@@ -129,7 +129,8 @@ class VQVAE(nn.Module):
             self._tptrs = ptrs
             self._tsig = None
         sig = tuple(p._version for p in params.values())
-        if sig != self._tsig:  # repack only after an update (optimizer.step / load_state_dict bump the versions)
+        # grad-enabled (training) calls repack every time: `.data` writes keep the version counter
+        if torch.is_grad_enabled() or sig != self._tsig:
             self._tengine.refresh_weights()
             self._tsig = sig
         return self._tengine

@@ -176,9 +176,26 @@ class DDIMSampler(nn.Module):
 
     @torch.no_grad()
     def forward(self, x_t, cond_input, uncond_input, steps=1, method="linear", eta=0.0, only_return_x_0=True,
-                interval=1):
+                interval=1, captured=True, seed=0):
+        """captured (default): a drop-in denoiser on the fused engine samples through sdmi.sampling.DDIMSampleLoop --
+        the loop recorded once and replayed with device timestep tables and device noise (Philox, `seed`) -- when only
+        x_0 is returned; otherwise (intermediates, foreign models) every step is issued eagerly with torch.randn_like
+        noise as the reference does (:200)."""
         self.cond_input = cond_input
         self.uncond_input = uncond_input
+        if captured and only_return_x_0 and hasattr(self.model, "_sdmi"):
+            from sdmi.module_glue import engine_path_ok
+            from sdmi.sampling import DDIMSampleLoop
+            if engine_path_ok(self.model):
+                cond_key = tuple(sorted((k, v.data_ptr(), tuple(v.shape)) for k, v in (cond_input or {}).items()
+                                        if isinstance(v, torch.Tensor)))
+                key = (tuple(x_t.shape), steps, method, float(eta), int(seed), cond_key)
+                loop = getattr(self, "_loop", None)
+                if loop is None or self._loop_key != key:
+                    loop = DDIMSampleLoop(self.model, self.alpha_t_bar, tuple(x_t.shape), cond_input, steps=steps,
+                                          method=method, eta=eta, seed=seed)
+                    self._loop, self._loop_key = loop, key
+                return loop.run(x_t.float()).clone()
         ts, tp = self.time_steps(self.T, steps, method)
         x = [x_t]
         for i in reversed(range(0, steps)):

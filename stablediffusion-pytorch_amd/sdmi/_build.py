@@ -82,5 +82,23 @@ def build(force=False, verbose=False):
     return LIB
 
 
+CABI_SRC = os.path.join(REPO, "tests", "cabi", "cabi_check.c")
+CABI_BIN = os.path.join(REPO, "tests", "cabi", "cabi_check")
+
+
+def build_cabi_check():
+    """The plain-C caller of include/sdmi.h (tests/cabi/cabi_check.c), compiled by gcc as C against libsdmi.so and the
+    HIP runtime: proves the boundary is callable without PyTorch or C++ (tests/test_cabi_gpu.py runs it)."""
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    tmp = CABI_BIN + f".tmp{os.getpid()}"
+    subprocess.check_call(["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                           "-I", os.path.join(rocm, "include"), "-I", os.path.join(REPO, "include"), CABI_SRC,
+                           "-o", tmp, "-L", HERE, "-lsdmi", "-L", os.path.join(rocm, "lib"), "-lamdhip64",
+                           "-Wl,-rpath,$ORIGIN/../../stablediffusion-pytorch_amd/sdmi",
+                           "-Wl,-rpath," + os.path.join(rocm, "lib")])
+    os.replace(tmp, CABI_BIN)
+    return CABI_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))

@@ -101,6 +101,7 @@ SIGNATURES = {
     "sdmi_pack_transpose": ([_P, _P, _I, _P], _I),
     "sdmi_optim_workspace": ([], _SZ),
     "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
+    "sdmi_loss_flag": ([_P, _P, _I, _P], _I),
     "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _F, _P], _I),
     "sdmi_ln_chunk_rows": ([_I], _I),
     "sdmi_ln_mod_fwd": ([_P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _I, _F, _I, _P], _I),
@@ -114,6 +115,7 @@ SIGNATURES = {
     "sdmi_pointwise_in": ([_P, _I, _I, _I, _P, _P, _I, _P, _I, _P], _I),
     "sdmi_ddpm_prev": ([_P, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _I, _P], _I),
     "sdmi_ddim_prev": ([_P, _P, _P, _L, _F, _F, _F, _P, _P], _I),
+    "sdmi_ddim_prev_dev": ([_P, _P, _P, _L, _P, _P, _P, _P, _P, _F, _P, _I, _P], _I),
     "sdmi_affine_step": ([_P, _P, _P, _L, _F, _F, _F, _P, _P], _I),
     "sdmi_mse_patch": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
     "sdmi_randn": ([_P, _L, ctypes.c_ulonglong, _P, _I, _P], _I),

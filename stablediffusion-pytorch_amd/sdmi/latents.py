@@ -133,12 +133,19 @@ def read_mask_shard(path):
     return _read(path, MAGIC_MSK)
 
 
-def generate_latents(encode, images, names, latent_dir, shard_size=1000, batch_size=32):
+def generate_latents(encode, images, names, latent_dir, shard_size=1000, batch_size=32, device=None):
     """gen_vqvae_latents.py:89-106 as a batched pipeline: encode every image with `encode` (a VQVAE module's
     `encode` -- models.vqvae.VQVAE on the HIP path -- or any callable (B, C, H, W) -> (z, ...) / z) batch_size images
     at a time, and write the quantised latents as `{part}.sdlat` shards of `shard_size` records in image order (the
     reference pickles `{image path: (1, C, h, w)}` every 1000 images as `{part}.pkl`). `images`: a (N, C, H, W)
-    tensor (host or device) or a sequence of (C, H, W) / (1, C, H, W) tensors. Returns the shard paths."""
+    tensor (host or device) or a sequence of (C, H, W) / (1, C, H, W) tensors; each batch is moved to `device` before
+    `encode` sees it (default: the device of the encoder's module when `encode` is a bound module method, else left
+    where it is), so host data-loader images feed the HIP VQVAE directly. Returns the shard paths."""
+    if device is None:
+        owner = getattr(encode, "__self__", None)
+        if isinstance(owner, torch.nn.Module):
+            p = next(owner.parameters(), None)
+            device = p.device if p is not None else None
     if len(images) != len(names):
         raise ValueError(f"{len(images)} images for {len(names)} names")
     os.makedirs(latent_dir, exist_ok=True)
@@ -156,6 +163,8 @@ def generate_latents(encode, images, names, latent_dir, shard_size=1000, batch_s
         chunk = images[s:s + batch_size]
         if not isinstance(chunk, torch.Tensor):
             chunk = torch.stack([c[0] if c.dim() == 4 else c for c in chunk])
+        if device is not None:
+            chunk = chunk.to(device, non_blocking=True)
         with torch.no_grad():
             z = encode(chunk)
         z = (z[0] if isinstance(z, (tuple, list)) else z).detach().to("cpu", torch.float32)

@@ -65,7 +65,9 @@ _PACKS = weakref.WeakKeyDictionary()
 
 
 def _packed(mod, w, build):
-    """PackPlan of `w` built by build(pk, w) once per (module, storage); repacked when w's version changes."""
+    """PackPlan of `w` built by build(pk, w) once per (module, storage). Repacked on every grad-enabled call (updates
+    through `.data` keep the version counter, see module_glue.EngineHolder.refresh) and, under torch.no_grad, when
+    w's version changed or invalidate_packs(mod) was called."""
     ent = _PACKS.get(mod)
     if ent is None or ent["ptr"] != w.data_ptr():
         pk = PackPlan(w.device)
@@ -73,10 +75,22 @@ def _packed(mod, w, build):
         pk.finalize()
         ent = {"ptr": w.data_ptr(), "ver": None, "pk": pk}
         _PACKS[mod] = ent
-    if ent["ver"] != w._version:
+    if torch.is_grad_enabled() or ent["ver"] != w._version:
         ent["pk"].run()
         ent["ver"] = w._version
     return ent["pk"]
+
+
+def invalidate_packs(mod=None):
+    """Drop the cached pack state of `mod`'s leaves (every leaf when mod is None): the next forward repacks."""
+    if mod is None:
+        for ent in _PACKS.values():
+            ent["ver"] = None
+        return
+    for m in mod.modules():
+        ent = _PACKS.get(m)
+        if ent is not None:
+            ent["ver"] = None
 
 
 def _pack_conv(mod):
@@ -614,7 +628,18 @@ def engine_ok(model, containers=()):
     """True while every submodule is an exact engine leaf type or one of the model's own container classes
     (nn.MultiheadAttention's out_proj is torch's NonDynamicallyQuantizableLinear: part of the exact MHA)."""
     allowed = set(ENGINE_LEAVES) | set(containers) | {nn.modules.linear.NonDynamicallyQuantizableLinear}
-    return all(type(m) in allowed for m in model.modules())
+
+    def ok(m):
+        if type(m) not in allowed:
+            return False
+        # the engines apply no dropout: an active one (p > 0 in training mode; CustomMultiheadAttention builds
+        # nn.Dropout(dropout), multihead_attention.py) takes the leaf path, which runs it
+        if type(m) is nn.Dropout and m.training and m.p > 0:
+            return False
+        if type(m) is nn.MultiheadAttention and m.training and m.dropout > 0:
+            return False
+        return True
+    return all(ok(m) for m in model.modules())
 
 
 def time_embedding(t, B, dim, device):

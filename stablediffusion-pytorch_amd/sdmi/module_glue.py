@@ -48,13 +48,43 @@ class EngineHolder:
         return self.engine
 
     def refresh(self, params):
-        """Repack the bf16 GEMM-layout weights only when a parameter changed since the last pack: every in-place
-        update (optimizer.step, load_state_dict, .copy_) bumps the tensor's version counter. A sampling loop
-        (tools/sample_ddpm_*.py: 1000 forwards, no updates) packs once instead of once per call."""
+        """Repack the bf16 GEMM-layout weights (the cast autocast performs on every forward).
+        Grad-enabled calls (training) repack unconditionally: updates written through `.data` -- the reference's EMA
+        `.data.mul_().add_()` (train_ddpm_cond_celebhq_multi_gpu.py:376-378), PercentOptimizerFP / DDFP SGD
+        (cim_layers/IBA_optimizer.py:67) -- do not bump a tensor's version counter, and one batched pack launch is
+        cheap next to a training step. Under torch.no_grad (sampling loops, tools/sample_ddpm_*.py: 1000 forwards and
+        no updates) the pack is skipped while no parameter's version changed; call invalidate() after writing
+        weights through `.data` between no-grad forwards."""
         sig = tuple(p._version for p in params)
-        if sig != self._packed_sig:
+        if torch.is_grad_enabled() or sig != self._packed_sig:
             self.engine.refresh_weights()
             self._packed_sig = sig
+
+    def invalidate(self):
+        """Force a repack at the next forward (weights changed behind the version counter, e.g. via `.data`)."""
+        self._packed_sig = None
+
+
+def invalidate_module(module):
+    """Weights of `module` were written behind the version counter (`.data`): repack everything at the next forward
+    (the fused engine's packs, the leaf path's per-module packs, the VQVAE training engine's)."""
+    from . import leaf
+    for m in module.modules():
+        h = getattr(m, "_sdmi", None)
+        if isinstance(h, EngineHolder):
+            h.invalidate()
+        if hasattr(m, "_tsig"):
+            m._tsig = None
+    leaf.invalidate_packs(module)
+
+
+def engine_path_ok(model):
+    """True when `model` (a drop-in denoiser) runs on the fused whole-network engine: no sdmi_leaf_path override and
+    every leaf an exact engine type (sdmi.leaf.engine_ok with the model's own container classes)."""
+    if getattr(model, "sdmi_leaf_path", False):
+        return False
+    check = getattr(model, "_sdmi_engine_ok", None)
+    return bool(check()) if check is not None else False
 
 
 class DenoiserFunction(torch.autograd.Function):

@@ -5,7 +5,12 @@ buckets, allreduce-then-average) for the HIP trainer: the flat buffer is ordered
 pass finalises it front to back; as soon as a prefix of at least `bucket_bytes` is final it is
 all-reduced (SUM) on a dedicated stream while the backward continues. The averaging (1/world) is
 folded into the optimizer's unscale/clip coefficient, so no extra pass touches the gradients.
-On ROCm the "nccl" backend is RCCL over xGMI; the same class runs with gloo on CPU for tests."""
+On ROCm the "nccl" backend is RCCL over xGMI; the same class runs with gloo on CPU for tests.
+
+wire="bf16" (off by default; SDMI_GRAD_WIRE=bf16 in the trainer) sends each bucket as bf16: half the bytes on the
+xGMI links, at the cost of bf16 rounding of every rank's gradient and of the ring's partial sums (the reference's DDP
+averages fp32 gradients). The fp32 buffer is rounded into a bf16 staging copy on the reducer stream, all-reduced,
+and widened back once the collective has completed."""
 import torch
 import torch.distributed as dist
 
@@ -13,9 +18,12 @@ from . import plan
 
 
 class BucketReducer:
-    def __init__(self, flat, group=None, bucket_bytes=64 << 20):
+    def __init__(self, flat, group=None, bucket_bytes=64 << 20, wire="fp32"):
+        if wire not in ("fp32", "bf16"):
+            raise ValueError(f"gradient wire format {wire!r}: fp32 or bf16")
         self.flat = flat
         self.group = group
+        self.wire = wire
         self.bucket = max(1, bucket_bytes // flat.element_size())
         self.total = flat.numel()
         self.cuda = flat.is_cuda
@@ -31,9 +39,16 @@ class BucketReducer:
         """all-reduce on the reducer stream (also the unit a recorded StepPlan re-issues)."""
         if self.cuda:
             with torch.cuda.stream(self.stream):
-                self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+                self._issue_on(view)
         else:
-            self.works.append(dist.all_reduce(view, group=self.group, async_op=True))
+            self._issue_on(view)
+
+    def _issue_on(self, view):
+        if self.wire == "bf16":
+            wire = view.to(torch.bfloat16)
+            self.works.append((dist.all_reduce(wire, group=self.group, async_op=True), wire, view))
+        else:
+            self.works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
 
     def _launch(self, lo, hi):
         view = self.flat[lo:hi]
@@ -55,8 +70,10 @@ class BucketReducer:
             self.launched = self.total
 
     def _drain(self):
-        for w in self.works:
+        for w, wire, view in self.works:
             w.wait()  # NCCL/RCCL: makes the current stream wait for the collective (no host sync)
+            if wire is not None:
+                view.copy_(wire)  # widen the summed bf16 bucket back into the fp32 gradients (current stream)
         self.works = []
 
     def finish(self):

@@ -62,7 +62,9 @@ def flat_order(cfg, keys):
 
 
 class FlatStore:
-    def __init__(self, shapes, cfg, device, with_grads=True, order=None):
+    def __init__(self, shapes, cfg, device, with_grads=True, order=None, grad_tail=0):
+        """grad_tail: extra fp32 slots after the gradients (inside the all-reduced buffer, outside every parameter and
+        the gradient norm): the data-parallel trainer's non-finite-loss flag rides in the last bucket."""
         keys = list(shapes.keys())
         self.order = list(order) if order is not None else flat_order(cfg, keys)
         assert sorted(self.order) == sorted(keys), "flat order must cover every parameter exactly once"
@@ -77,7 +79,7 @@ class FlatStore:
             off += (n + 3) // 4 * 4  # 16-B aligned starts (vector epilogue loads of biases)
         self.numel = off
         self.params = torch.zeros(off, dtype=torch.float32, device=device)
-        self.grads = torch.zeros(off, dtype=torch.float32, device=device) if with_grads else None
+        self.grads = torch.zeros(off + grad_tail, dtype=torch.float32, device=device) if with_grads else None
         self.p = {k: self.view(self.params, k) for k in self.order}
         self.g = {k: self.view(self.grads, k) for k in self.order} if with_grads else None
 

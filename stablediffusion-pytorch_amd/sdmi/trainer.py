@@ -24,7 +24,7 @@ from .unet_engine import UNetEngine
 from .dit_engine import DiTEngine, dit_flat_order
 
 # state vector layout (see csrc/optim.hip)
-S_NORM, S_COEF, S_SCALE, S_GROWTH, S_STEP, S_SKIP, S_LOSS = range(7)
+S_NORM, S_COEF, S_SCALE, S_GROWTH, S_STEP, S_SKIP, S_LOSS, S_DPFLAG = range(8)
 
 
 def scheduler_tables(num_timesteps, beta_start, beta_end):
@@ -40,16 +40,18 @@ class DDPMTrainer:
 
     def __init__(self, cfg, state_dict, device, *, base="cond", lr=1e-5, betas=(0.9, 0.999), eps=1e-8,
                  max_grad_norm=1.0, ema_decay=0.9999, init_scale=65536.0, growth_interval=2000,
-                 sched=(1000, 0.00085, 0.012), group=None, bucket_bytes=64 << 20, force_reducer=False):
+                 sched=(1000, 0.00085, 0.012), group=None, bucket_bytes=64 << 20, force_reducer=False,
+                 grad_wire=None):
         self.cfg = cfg
         self.base = base
         self.device = torch.device(device)
         shapes = {k: tuple(v.shape) for k, v in state_dict.items()}
         order = dit_flat_order(cfg, list(shapes)) if base == "dit" else None
-        self.store = FlatStore(shapes, cfg, self.device, order=order)
-        self.store.load(state_dict)
         self.group = group
         self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
+        # N > 1: one fp32 slot after the gradients carries this rank's non-finite-loss flag through the all-reduce
+        self.store = FlatStore(shapes, cfg, self.device, order=order, grad_tail=4 if self.world > 1 else 0)
+        self.store.load(state_dict)
         if self.world > 1:
             # DistributedDataParallel broadcasts rank 0's parameters when it wraps the model
             # (train_ddpm_cond_celebhq_multi_gpu.py:257-263): every replica (and its EMA copy) starts from them
@@ -73,8 +75,11 @@ class DDPMTrainer:
         sa, s1a = scheduler_tables(*sched)
         self.sqrt_abar, self.sqrt_1m_abar = sa.to(self.device), s1a.to(self.device)
         # force_reducer: run the bucketed all-reduce even at world size 1 (exercises RCCL + plan replay on one GPU)
-        self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes) if self.world > 1 or force_reducer
-                        else None)
+        # gradient wire format of the all-reduce: fp32 (the reference's DDP) unless grad_wire / SDMI_GRAD_WIRE = bf16
+        self.grad_wire = grad_wire or os.environ.get("SDMI_GRAD_WIRE", "fp32")
+        self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes, wire=self.grad_wire)
+                        if self.world > 1 or force_reducer else None)
+        self.tail_events = None  # (after backward, after the all-reduce drain): set by measure_exchange_tail()
         if self.reducer is not None and getattr(self.engine, "side", None) is not None:
             self.reducer.producers.extend(getattr(self.engine, "sides", None) or [self.engine.side])
         self._progress = None
@@ -159,27 +164,37 @@ class DDPMTrainer:
         pred, ctx = eng.forward(xt, t, text, mask, mask_keep=mask_keep, klass=klass)
         dpred = eng.new_dpred(B, H, W)
         eng.loss(pred, noise, dpred, self.state[S_LOSS:S_LOSS + 1], gscale_dev=self.state[S_SCALE:S_SCALE + 1])
+        L = _lib.lib()
+        if self.world > 1:  # this rank's non-finite-loss flag into the gradient tail (all-reduced with the last bucket)
+            _lib.check(L.sdmi_loss_flag(self.state[S_LOSS:].data_ptr(), st.grads[st.numel:].data_ptr(), 0, K._stream()),
+                       "sdmi_loss_flag")
         if self.reducer is not None and self.base == "dit":
             self.reducer.reset()
             eng.backward(ctx, dpred, on_progress=self._on_progress_dit)
+            self._tail_mark(0)
             self.reducer.finish()
+            self._tail_mark(1)
         elif self.reducer is not None:
             self.reducer.reset()
             if self._progress is None:
                 self._progress = self._watermarks(ctx["tape"])
             eng.backward(ctx, dpred, on_progress=self._on_progress)
+            self._tail_mark(0)
             self.reducer.finish()
+            self._tail_mark(1)
         else:
             eng.backward(ctx, dpred)
-        L = _lib.lib()
         ws = torch.empty(L.sdmi_optim_workspace() // 4, dtype=torch.float32, device=self.device)
         hp = self.hp
-        # Non-finite loss: one process skips before scaler.update() (:348-352). With N > 1 only the rank-local loss
-        # is known here, so the skip / back-off decision is left to the all-reduced gradient norm (a non-finite loss
-        # makes that rank's gradients, hence the global sum, non-finite): every replica then skips and halves its
-        # loss scale identically instead of drifting apart.
+        # Non-finite loss: the reference skips before scaler.update() (:348-352), leaving the scale alone. N > 1: the
+        # all-reduced sum of every rank's flag decides, so all replicas skip together (and keep their scale) when any
+        # rank's loss is non-finite; a non-finite gradient norm (all-reduced gradients: identical on every rank) skips
+        # and backs the scale off everywhere (:366-371).
+        if self.world > 1:
+            _lib.check(L.sdmi_loss_flag(st.grads[st.numel:].data_ptr(), self.state[S_DPFLAG:].data_ptr(), 1,
+                                        K._stream()), "sdmi_loss_flag")
         _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(), ws.data_ptr(),
-                                       hp["growth"], 1 if self.world == 1 else 0, float(self.world), K._stream()),
+                                       hp["growth"], 1 if self.world == 1 else 2, float(self.world), K._stream()),
                    "sdmi_clip_unscale")
         ema_decay = hp["ema"] if hp["ema"] is not None else 0.0
         if self.opt_ranges is None:
@@ -207,6 +222,21 @@ class DDPMTrainer:
         if late is not None:
             eng._pending[late] = self.late_event
         return self.state
+
+    def measure_exchange_tail(self, on=True):
+        """Eager steps record two events on the compute stream: when the backward (every gradient kernel, side streams
+        joined) is done and when the last all-reduce bucket has been waited for; their distance is the gradient exchange
+        left exposed after the backward (exchange_tail_ms)."""
+        self.tail_events = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] if on else None
+
+    def _tail_mark(self, i):
+        if self.tail_events is not None:
+            self.tail_events[i].record()
+
+    def exchange_tail_ms(self):
+        if self.tail_events is None:
+            return None
+        return self.tail_events[0].elapsed_time(self.tail_events[1])
 
     def _on_progress_dit(self, i):
         """DiT backward finished layer i: proj_out and layers i..L-1 are final (the flat prefix up to layer i)."""

@@ -61,9 +61,12 @@ def _worker(rank, world, port, out, model="unet"):
                          bucket_bytes=1 << 20)
     for s in range(STEPS):
         x0, noise, t, text, mask = _batch(rank, SMALL_COND, s)
+        if model == "nan" and s == 1 and rank == 1:
+            noise[1, 2, 3, 4] = float("nan")  # only rank 1's loss is non-finite at step 1
         tr.step(x0, noise, t, text, mask)
     sd = tr.state_dict()
     torch.cuda.synchronize()
+    out[f"state{rank}"] = tr.state.cpu()
     out[f"params{rank}"] = torch.cat([v.flatten() for v in sd.values()]).cpu()
     if tr.ema is not None:
         out[f"ema{rank}"] = tr.ema.cpu()
@@ -96,13 +99,33 @@ def test_two_rank_dit_step_matches_grad_average():
     _compare(tr, out, world)
 
 
-def _reference_steps(tr, world, ema_decay):
+def test_two_rank_nonfinite_loss_on_one_rank_skips_everywhere():
+    """Only rank 1's loss is non-finite at step 1: every replica skips that step WITHOUT scaler.update() (the reference
+    rule, train_ddpm_cond_celebhq_multi_gpu.py:348-352, decided by the all-reduced loss flag), so both ranks end
+    bit-identical, at the update of steps 0 and 2 alone, with the loss scale untouched."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _port(), out, "nan"), nprocs=world, join=True)
+    from tests.golden.configs import SMALL_COND
+    from sdmi.trainer import DDPMTrainer, S_SCALE, S_STEP, S_GROWTH, S_SKIP
+    assert torch.equal(out["params0"], out["params1"]) and torch.equal(out["ema0"], out["ema1"])
+    for r in range(world):
+        st = out[f"state{r}"]
+        assert st[S_SCALE].item() == 65536.0 and int(st[S_STEP].item()) == STEPS - 1
+        assert int(st[S_GROWTH].item()) == STEPS - 1 and st[S_SKIP].item() == 0.0
+    tr = DDPMTrainer(SMALL_COND, _init_state(SMALL_COND), "cuda", lr=1e-3)
+    _reference_steps(tr, world, ema_decay=0.9999, steps=[s for s in range(STEPS) if s != 1])
+    _compare(tr, out, world)
+
+
+def _reference_steps(tr, world, ema_decay, steps=None):
     """One process: per step, sum the ranks' gradients by hand, then the same clip + Adam (+ EMA) kernels."""
     from tests.golden.configs import SMALL_COND
     from sdmi import _lib, kernels as K
     L = _lib.lib()
     ws = torch.empty(L.sdmi_optim_workspace() // 4, device="cuda")
-    for s in range(STEPS):
+    for s in (range(STEPS) if steps is None else steps):
         gsum = torch.zeros_like(tr.store.grads)
         for r in range(world):
             x0, noise, t, text, mask = _batch(r, SMALL_COND, s)

@@ -29,7 +29,8 @@ def test_images_to_shards_to_resident_set_to_train_step(tmp_path):
     N = 40
     ims = torch.rand(N, 3, 64, 64, generator=g) * 2 - 1
     names = [f"CelebAMask-HQ/CelebA-HQ-img/{i}.jpg" for i in range(N)]
-    paths = LT.generate_latents(vq.encode, ims.cuda(), names, str(tmp_path / "lat"), shard_size=16, batch_size=8)
+    # host images, as a data loader yields them: generate_latents moves each batch to the encoder's device
+    paths = LT.generate_latents(vq.encode, ims.cpu(), names, str(tmp_path / "lat"), shard_size=16, batch_size=8)
     assert [os.path.basename(p) for p in paths] == ["0.sdlat", "1.sdlat", "2.sdlat"]
     got = LT.load_latents(str(tmp_path / "lat"))
     assert list(got) == names

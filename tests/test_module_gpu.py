@@ -107,3 +107,33 @@ def test_inference_packs_once_and_keeps_no_tape():
     torch.cuda.synchronize()
     assert len(calls) == 1
     assert torch.allclose(o2, ref + 0.5, atol=1e-5) and torch.equal(o2, o3)
+
+
+def test_data_writes_between_forwards_are_seen():
+    """Updates written through `.data` keep the version counter (the reference's EMA `.data.mul_().add_()`,
+    PercentOptimizerFP's `p.data.copy_`): a grad-enabled forward always repacks, so its output follows the new
+    weights; under torch.no_grad, sdmi_invalidate() forces the repack."""
+    sd0 = O.deterministic_state(O.unet_param_shapes(SMALL_COND), seed=6)
+    model = _model(sd0)
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 4, 32, 32, generator=g).cuda()
+    cond = {"text": torch.randn(2, 77, 64, generator=g).cuda(),
+            "image": one_hot(torch.randint(0, 19, (2, 64, 64), generator=g)).cuda()}
+    t = torch.tensor([5, 900]).cuda()
+    a = model(x, t, cond).detach().clone()
+    w = model.downs[0].resnet_conv_first[0][2].weight
+    v0 = w._version
+    w.data.copy_(w.data * 1.5)
+    assert w._version == v0  # no version bump: the old gate would have kept the stale pack
+    b = model(x, t, cond).detach()
+    assert not torch.equal(a, b)
+    with torch.no_grad():
+        c = model(x, t, cond)
+        w.data.mul_(2.0)
+        stale = model(x, t, cond)
+        model.sdmi_invalidate()
+        d = model(x, t, cond)
+    torch.cuda.synchronize()
+    assert torch.equal(b, c) and torch.equal(stale, c) and not torch.equal(d, c)
+    ref = model(x, t, cond).detach()  # grad-enabled: repacks, same weights as d
+    assert torch.equal(ref, d)

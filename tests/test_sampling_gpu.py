@@ -95,3 +95,65 @@ def test_device_noise_is_standard_normal_and_fresh():
     _lib.check(L.sdmi_randn(z2.data_ptr(), n, ctypes.c_ulonglong(7), off.data_ptr(), 0, K._stream()), "randn")
     torch.cuda.synchronize()
     assert torch.equal(z1, z2) and off.item() == 0
+
+
+@pytest.mark.parametrize("method,eta", [("linear", 0.0), ("quadratic", 0.5)])
+def test_captured_ddim_matches_stepwise(method, eta):
+    """DDIMSampler.forward (reference scheduler/linear_noise_scheduler.py:209-256) as a recorded loop: device (t, t_prev)
+    tables + device step index + device noise, bit-identical to issuing every step eagerly; the drop-in
+    DDIMSampler.forward(captured=True) returns the same x_0; one step equals the module's eager sample_one_step
+    (host-table alphas) on the same noise."""
+    from sdmi.sampling import DDIMSampleLoop, ddim_time_steps
+    from scheduler.linear_noise_scheduler import DDIMSampler
+    model = _model(True)
+    g = torch.Generator().manual_seed(12)
+    B, steps = 2, 7
+    c = {"text": torch.randn(B, 77, 64, generator=g).cuda(),
+         "image": one_hot(torch.randint(0, 19, (B, 64, 64), generator=g)).cuda()}
+    xT = torch.randn(B, 4, 32, 32, generator=g).cuda()
+    sampler = DDIMSampler(model, (0.0001, 0.02), 1000)
+    cap = DDIMSampleLoop(model, sampler.alpha_t_bar, (B, 4, 32, 32), c, steps=steps, method=method, eta=eta, seed=5)
+    xa = cap.run(xT, captured=True).clone()
+    ts, _ = ddim_time_steps(1000, steps, method)
+    assert cap.idx.item() == 0 and cap.t.item() == int(ts[0])
+    eag = DDIMSampleLoop(model, sampler.alpha_t_bar, (B, 4, 32, 32), c, steps=steps, method=method, eta=eta, seed=5)
+    xb = eag.run(xT, captured=False)
+    torch.cuda.synchronize()
+    assert torch.isfinite(xa).all()
+    assert torch.equal(xa, xb)
+    assert torch.equal(cap.run(xT, captured=True), xa)  # replayed again from the same start
+    xs = sampler(xT, c, None, steps=steps, method=method, eta=eta, seed=5)
+    assert torch.equal(xs, xa)
+    # one step vs the eager module step (sampler.sample_one_step: model forward + sdmi_ddim_prev with host alphas)
+    one = DDIMSampleLoop(model, sampler.alpha_t_bar, (B, 4, 32, 32), c, steps=steps, method=method, eta=eta, seed=5)
+    one.reset(xT)
+    one._step()
+    ts, tp = ddim_time_steps(1000, steps, method)
+    ref = sampler.sample_one_step(xT, int(ts[steps - 1]), int(tp[steps - 1]), eta, noise=one.z)
+    torch.cuda.synchronize()
+    assert torch.equal(one.xt, ref)
+
+
+def test_loop_refreshes_weights_and_honours_leaf_path():
+    """A loop reused after a weight update written through `.data` (no version bump: the reference's EMA update)
+    samples with the new weights; a model forced onto the leaf path is sampled stepwise through its own forward."""
+    from sdmi.sampling import DDPMSampleLoop
+    from scheduler.linear_noise_scheduler import LinearNoiseScheduler
+    model = _model(False)
+    xT = torch.randn(2, 4, 32, 32, generator=torch.Generator().manual_seed(6)).cuda()
+    sched = LinearNoiseScheduler(1000, 0.0015, 0.0195)
+    loop = DDPMSampleLoop(model, sched, (2, 4, 32, 32), seed=3)
+    assert loop.fused
+    a = loop.run(xT, steps=3)[0].clone()
+    with torch.no_grad():
+        model.conv_out.weight.data.mul_(0.5)
+    b = loop.run(xT, steps=3)[0].clone()
+    assert not torch.equal(a, b)
+    fresh = DDPMSampleLoop(model, sched, (2, 4, 32, 32), seed=3)
+    assert torch.equal(fresh.run(xT, steps=3)[0], b)
+    model.sdmi_leaf_path = True
+    leaf = DDPMSampleLoop(model, sched, (2, 4, 32, 32), seed=3)
+    assert not leaf.fused
+    c = leaf.run(xT, steps=3)[0]
+    torch.cuda.synchronize()
+    assert (c - b).abs().max().item() < 5e-2 * b.abs().max().item()
