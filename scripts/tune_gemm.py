@@ -94,9 +94,10 @@ def main():
         d.variant_hint = 0
         t_def = time_launch(L, d, ws, stream)
         best, t_best = 0, t_def
-        # mainloops: register staging (1) and the LDS-DMA rings (2, 3: 2 / 3 stages of 64-deep K; 4: 8-wave
+        # mainloops: register staging (1) and the LDS-DMA rings (2, 3, 6: 2 / 3 / 4 stages of 64-deep K; 7, 8: 64-row
+        # tiles with 6 stages; 4: 8-wave
         # 128 x {256, 384} tiles; 5: 3 stages of 32-deep K); the library downgrades a request the mode cannot take
-        variants = tuple(int(v) for v in os.environ.get("SDMI_TUNE_VARIANTS", "1,2,3,4,5").split(","))
+        variants = tuple(int(v) for v in os.environ.get("SDMI_TUNE_VARIANTS", "1,2,3,4,5,6,7,8").split(","))
         for v in variants:
             for s in SPLITS:
                 if s > nkt or s * d.m * d.n * 4 >= min(ws.numel() * 4, 1 << 31):

@@ -772,6 +772,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, char* lds_wave_
 //     N = 384 outputs split into 2 (not 3) 192-column tiles, so a 32768 x 384 conv is exactly 512 tiles = one round
 //   256 x {128, 192}, 8 waves (4 x 2), B_NK: the large-M convolutions / linears -- 1.5x the MFMA work per byte staged
 //   128 x {256, 384}, 8 waves (2 x 4), MN-contiguous B: weight gradients, whose N = 9 * cin is a multiple of 384
+//   64 x {64, 128}, 4 waves (1 x 4), K-contiguous A and B: the latency-bound low-resolution GEMMs (M <= 8192, a grid
+//     of <= 256 tiles, K of 8-40 k-tiles) with a 6-stage ring -- five 64-deep k-tiles in flight per workgroup, so the
+//     DMA latency is paid about once per launch instead of once per k-tile
 // The MN-contiguous (ds_read_b64_tr_b16) LDS images are kept as 128-column sub-tiles [64 k][128] (256-B rows).
 // RED (col-major A only): reduction columns as extra MFMA tiles against synthesised B fragments (see reduce_frag).
 template <int TBM, int NWN>
@@ -1258,7 +1261,7 @@ int gemm_variant() {
   if (v == -2) {
     const char* s = getenv("SDMI_GEMM_VARIANT");
     v = s ? atoi(s) : -1;
-    if (v != 0 && v != 2 && v != 3 && v != 4 && v != 5) v = -1;
+    if (v != 0 && (v < 2 || v > 8)) v = -1;
   }
   return v;
 }
@@ -1272,7 +1275,7 @@ bool dma_reductions_ok(const sdmi_gemm_desc* d) {
 
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 5) v = d->variant_hint == 1 ? 0 : d->variant_hint;
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 8) v = d->variant_hint == 1 ? 0 : d->variant_hint;
   if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
   if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
   if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
@@ -1281,10 +1284,12 @@ int pick_variant(const sdmi_gemm_desc* d) {
   if (v == 4 && d->n % 256 && d->n % 384) v = 2;  // 128 x {256, 384} tiles: N % 384 == 0 or N % 256 == 0
   if (v == 5 && d->a_mode == SDMI_A_CONV && d->a2 && d->k_split % 32) v = 0;
   if (v != 0 && d->a_mode == SDMI_A_COLMAJOR && d->b_mode == SDMI_B_NK) v = 0;  // no DMA instantiation
+  // 64-row tiles: K-contiguous images only (row-major / implicit-conv A, [n][k] B), no reduction columns
+  if ((v == 7 || v == 8) && (d->a_mode == SDMI_A_COLMAJOR || d->b_mode != SDMI_B_NK || has_reductions(d))) v = 2;
   return v;
 }
 
-int tile_m(const sdmi_gemm_desc*, int) { return BM; }
+int tile_m(const sdmi_gemm_desc*, int variant) { return variant == 7 || variant == 8 ? 64 : BM; }
 
 // columns the grid covers: the DMA kernels compute the reduction columns outside the column tiles
 int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total(d) : d->n; }
@@ -1298,6 +1303,8 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
     force = s ? atoi(s) : -1;
   }
   if (variant == 4) return d->n % 384 == 0 ? 384 : 256;
+  if (variant == 7) return 64;
+  if (variant == 8 || variant == 6) return BN;
   if (variant == 5) return d->b_mode == SDMI_B_NK && d->n % 192 == 0 ? 192 : BN;
   if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR) return BN;
   // narrow outputs (N <= 64: the VQVAE's 64-channel convs at 256^2, 4-channel heads, DiT proj_out): a 128-column
@@ -1337,6 +1344,11 @@ hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s)
 template <int AM, int BMODE, int RED>
 hipError_t launch_dma_red(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
   if (v == 3 && RED == 0) return launch_dma<AM, BMODE, 3, BN, BM, 2, 0>(a, e, grid, s);
+  if (v == 6) return launch_dma<AM, BMODE, 4, BN, BM, 2, RED>(a, e, grid, s);  // 4-stage 128 x 128 (128 KiB ring)
+  if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR && RED == 0) {
+    if (v == 7) return launch_dma<AM, BMODE, 6, 64, 64, 4, 0>(a, e, grid, s);    // 64 x 64, 6 stages (96 KiB)
+    if (v == 8) return launch_dma<AM, BMODE, 6, 128, 64, 4, 0>(a, e, grid, s);   // 64 x 128, 6 stages (144 KiB)
+  }
   if (v == 4) {  // 128 x {256, 384} on 8 waves, 32-deep stages, 4-stage ring (3 tiles in flight)
     if (tbn == 384) return launch_dma<AM, BMODE, 4, 384, BM, 4, RED, 32>(a, e, grid, s);
     if (tbn == 256) return launch_dma<AM, BMODE, 4, 256, BM, 4, RED, 32>(a, e, grid, s);

@@ -47,6 +47,7 @@ def test_state_machine_matches_torch_gradscaler_adam():
             opt.zero_grad(set_to_none=True)
             t_skip = True
         else:
+            scaler.scale(torch.ones((), device="cuda"))  # the reference's scaler.scale(loss) (lazily creates the scale)
             gs = gr.cuda() * scaler.get_scale()
             if bad_grad:
                 gs[17] = float("nan") if ev == "nan_grad" else float("inf")
