@@ -280,8 +280,10 @@ constexpr int PACK_LDS_ELEMS = 16384;  // bf16 staging capacity (32 KiB, 4+ work
 template <int TAPS>
 __device__ __forceinline__ void pack_gather(const sdmi_pack_desc& d, const float* src, bf16_t* st, int ld, int taps) {
   const int T = TAPS > 0 ? TAPS : taps;
+  // channel-contiguous sources (GEMM-natural (co, kh, kw, ci) weights, linears): channel fastest, coalesced reads
+  const bool cfast = d.si == 1;
   for (int idx = threadIdx.x; idx < T * d.I; idx += NT) {
-    const int i = idx / T, t = idx - i * T;
+    const int i = cfast ? idx % d.I : idx / T, t = cfast ? idx / d.I : idx - i * T;
     const int a = t / d.KW, b = t - a * d.KW;
     const int kh = d.kh_off + d.kh_mul * a, kw = d.kw_off + d.kw_mul * b;
     st[t * ld + i] = f2bf(src[(long long)i * d.si + (long long)kh * d.skh + (long long)kw * d.skw]);

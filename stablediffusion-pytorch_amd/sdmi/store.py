@@ -61,11 +61,24 @@ def flat_order(cfg, keys):
     return body + tw + tb + cw + cb + tail
 
 
+def unet_gemm_natural(key, shape):
+    """UNet conv weights kept in the GEMM-natural (co, kh, kw, ci) order in the flat buffers (FlatStore natural=):
+    the resnet 3x3 convs and the stride-2 down-sampling convs, whose weight gradients the engine then writes with
+    16-byte row stores (a torch-layout (co, ci, kh, kw) gradient is a stride-(kh*kw) column scatter: the 4x4-level
+    3x3 weight gradient measured 38 -> 16 us, scripts/wg_anatomy.py) and whose forward packs become plain casts.
+    conv_in / conv_out (padded channels) and the transposed up-sampling convs ((ci, co, kh, kw)) keep torch order."""
+    return (len(shape) == 4 and shape[2] * shape[3] > 1 and key.endswith(".weight")
+            and (".resnet_conv_first." in key or ".resnet_conv_second." in key or key.endswith("down_sample_conv.weight")))
+
+
 class FlatStore:
-    def __init__(self, shapes, cfg, device, with_grads=True, order=None, grad_tail=0):
+    def __init__(self, shapes, cfg, device, with_grads=True, order=None, grad_tail=0, natural=None):
         """grad_tail: extra fp32 slots after the gradients (inside the all-reduced buffer, outside every parameter and
-        the gradient norm): the data-parallel trainer's non-finite-loss flag rides in the last bucket."""
+        the gradient norm): the data-parallel trainer's non-finite-loss flag rides in the last bucket.
+        natural: predicate (key, shape) -> True for 4-d conv weights stored in (co, kh, kw, ci) order; their views
+        (parameters, gradients, EMA, Adam moments) are torch-shaped (co, ci, kh, kw) permutations of that memory."""
         keys = list(shapes.keys())
+        self.natural = {k for k in keys if natural is not None and natural(k, tuple(shapes[k]))}
         self.order = list(order) if order is not None else flat_order(cfg, keys)
         assert sorted(self.order) == sorted(keys), "flat order must cover every parameter exactly once"
         self.shapes = dict(shapes)
@@ -103,6 +116,9 @@ class FlatStore:
 
     def view(self, flat, k):
         off, n = self.offsets[k]
+        if k in self.natural:
+            co, ci, kh, kw = self.shapes[k]
+            return flat[off:off + n].view(co, kh, kw, ci).permute(0, 3, 1, 2)
         return flat[off:off + n].view(self.shapes[k])
 
     def load(self, state_dict):

@@ -19,7 +19,7 @@ from . import _lib
 from . import kernels as K
 from . import plan
 from .reducer import BucketReducer
-from .store import FlatStore, param_label
+from .store import FlatStore, param_label, unet_gemm_natural
 from .unet_engine import UNetEngine
 from .dit_engine import DiTEngine, dit_flat_order
 
@@ -50,7 +50,10 @@ class DDPMTrainer:
         self.group = group
         self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
         # N > 1: one fp32 slot after the gradients carries this rank's non-finite-loss flag through the all-reduce
-        self.store = FlatStore(shapes, cfg, self.device, order=order, grad_tail=4 if self.world > 1 else 0)
+        # UNet: 3x3 / down-sampling conv weights in GEMM-natural (co, kh, kw, ci) order (store.unet_gemm_natural;
+        # SDMI_NATURAL=0 keeps torch order everywhere)
+        nat = unet_gemm_natural if base != "dit" and os.environ.get("SDMI_NATURAL", "1") != "0" else None
+        self.store = FlatStore(shapes, cfg, self.device, order=order, grad_tail=4 if self.world > 1 else 0, natural=nat)
         self.store.load(state_dict)
         if self.world > 1:
             # DistributedDataParallel broadcasts rank 0's parameters when it wraps the model

@@ -422,14 +422,14 @@ class UNetEngine:
         w = self.P[key + ".weight"]
         O, I, KH, KW = w.shape
         Ip = ipad or I
+        so, si, skh, skw = w.stride()  # torch (co, ci, kh, kw) or GEMM-natural (co, kh, kw, ci) memory order
         if fwd:
-            pk.add(key + "#f", w, O, I, Ip, KH, KW, I * KH * KW, KH * KW, KW, 1, rows=opad)
+            pk.add(key + "#f", w, O, I, Ip, KH, KW, so, si, skh, skw, rows=opad)
         if dgrad and fwd:  # stride-1 dgrad [I][KH][KW][O] with flipped taps = the forward layout transposed
             pk.add_transpose(key + "#d", key + "#f", O, I, KH * KW, [KH * KW - 1 - t for t in range(KH * KW)], Ip,
                              rows=ipad, opad=opad)
         elif dgrad:
-            pk.add(key + "#d", w, I, O, opad or O, KH, KW, KH * KW, I * KH * KW, KW, 1, KH - 1, -1, KW - 1, -1,
-                   rows=ipad)
+            pk.add(key + "#d", w, I, O, opad or O, KH, KW, si, so, skh, skw, KH - 1, -1, KW - 1, -1, rows=ipad)
 
     def _pk_lin(self, pk, key):
         w = self.P[key + ".weight"] if key + ".weight" in self.P else self.P[key]
@@ -446,7 +446,7 @@ class UNetEngine:
         wr = P[f"{p}.residual_input_conv.{l}.weight"]
         cat = f"{p}.res{l}#cat"
         pk.reserve(cat, cout, 9 * cout + cin)
-        pk.add(None, w2, cout, cout, cout, 3, 3, cout * 9, 9, 3, 1, into=cat)
+        pk.add(None, w2, cout, cout, cout, 3, 3, *w2.stride(), into=cat)
         pk.add(None, wr, cout, cin, cin, 1, 1, cin, 1, 0, 0, into=cat, col0=9 * cout)
         # its dgrad layout: the conv part of the concatenated forward weight, transposed per (flipped) tap
         pk.add_transpose(f"{p}.resnet_conv_second.{l}.2#d", cat, cout, cout, 9, [8 - t for t in range(9)], cout)
@@ -512,6 +512,12 @@ class UNetEngine:
 
     def g(self, key):
         return self.Gd[key] if self.Gd is not None else None
+
+    def wperm(self, key):
+        """conv_wgrad output layout of a conv weight gradient: torch (co, ci, kh, kw) order (column permute) for a
+        contiguous gradient view, the GEMM's own (co, kh, kw, ci) order (16-B row stores) for a natural-order one
+        (sdmi.store.unet_gemm_natural)."""
+        return self.g(key).is_contiguous()
 
     def forward(self, x, t, text=None, mask=None, need_backward=True, mask_keep=None, klass=None):
         """x: (B, C, H, W) fp32; t: int64 (B,), (1,) or 0-d; text: (B, S, ctx) ; mask: (B, cmi, MH, MW) fp32;
@@ -796,7 +802,8 @@ class UNetEngine:
         with self._wg(dy):
             # conv2 and residual-conv bias gradients (both = column sums of dy) come out of the same launch
             K.conv_wgrad(dy, ldy, c["h2"], B, h, w, cout, cout, cout, 3, 3, 1, 1, self.g(b + ".2.weight"), h, w,
-                         bias_grad=self.g(b + ".2.bias"), bias_grad2=self.g(rc + ".bias"))
+                         perm=self.wperm(b + ".2.weight"), bias_grad=self.g(b + ".2.bias"),
+                         bias_grad2=self.g(rc + ".bias"))
             K.linear_wgrad(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
         dh2 = self._new(B * Pn, cout)
         K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout)
@@ -812,7 +819,7 @@ class UNetEngine:
             # conv1 bias, t_emb_layers bias and the per-sample time-embedding gradient (blocks.py:117-118) are
             # reductions of dh2 computed by the weight-gradient launch itself
             K.conv_wgrad(dh2, cout, c["h0"], B, h, w, cin, cin, cout, 3, 3, 1, 1, self.g(a + ".2.weight"), h, w,
-                         bias_grad=self.g(a + ".2.bias"),
+                         perm=self.wperm(a + ".2.weight"), bias_grad=self.g(a + ".2.bias"),
                          bias_grad2=self.g(f"{p}.t_emb_layers.{l}.1.bias") if off is not None else None,
                          group_sums=self.dtemb_all[:, off:off + cout] if off is not None else None)
         dh0 = self._new(B * Pn, cin)
@@ -941,7 +948,7 @@ class UNetEngine:
         ldy = K.ld_of(dy)
         with self._wg(dy):
             K.conv_wgrad(dy, ldy, c["x"], B, h, w, C, K.ld_of(c["x"]), C, 4, 4, 2, 1, self.g(key + ".weight"),
-                         h // 2, w // 2, bias_grad=self.g(key + ".bias"))
+                         h // 2, w // 2, perm=self.wperm(key + ".weight"), bias_grad=self.g(key + ".bias"))
         dx, fresh = grads.get(c["xn"])
         wph = [self.W(f"{key}#d{ph}{pw}") for ph in range(2) for pw in range(2)]
         K.conv_dgrad_phases(dy, B, h, w, C, ldy, wph, C, dx, K.ld_of(dx), resid=None if fresh else dx,
