@@ -132,6 +132,14 @@ int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v,
 int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, const void* o, int ldo,
                   const void* dout, int lddo, const float* lse, float* delta_ws, void* dq, int lddq, void* dk,
                   int lddk, void* dv, int lddv, int B, int H, int N, int S, int d, sdmi_stream_t stream);
+/* The same backward as ONE pass over the keys (P and dS computed once per score; dQ from a transposed dS image in
+ * LDS): one key block (S <= 128) stores dQ directly, more key blocks sum fp32 dQ partials (ws, at least
+ * sdmi_attn_bwd_workspace bytes) in a fixed key-block order -- deterministic, no float atomics. delta_ws as above. */
+size_t sdmi_attn_bwd_workspace(int B, int H, int N, int S, int d);
+int sdmi_attn_bwd_fused(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, const void* o, int ldo,
+                        const void* dout, int lddo, const float* lse, float* delta_ws, void* ws, size_t ws_bytes,
+                        void* dq, int lddq, void* dk, int lddk, void* dv, int lddv, int B, int H, int N, int S, int d,
+                        sdmi_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * GroupNorm (+ fused SiLU) on NHWC bf16 x[b][p][c] = x[(b*P + p)*ld + c]; fp32 statistics.

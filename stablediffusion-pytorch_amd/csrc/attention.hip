@@ -39,6 +39,8 @@ struct AttnArgs {
   int ldq, ldk, ldv, ldo, lddo, lddq, lddk, lddv;
   int B, H, N, S, d;
   float scale;  // 1/sqrt(d)
+  float* dq_part;     // fused backward: per-key-block fp32 dQ partials [nkb][B*H][N][d] (nkb > 1)
+  unsigned* ctr;      // fused backward: per-(b*h, query tile) arrival counters (zero between launches)
 };
 
 template <int DP> struct Tile {
@@ -544,6 +546,256 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     }
 }
 
+// =============================================================================================
+// backward, fused: dK, dV AND dQ in one pass (keys on lanes, 128 keys per workgroup, query tiles streamed) --
+// P and dS are computed once per score instead of once in each of the two kernels above (the exp, the scale FMA,
+// the dS product and the dS conversion per score halve; two MFMA products of five are not recomputed).
+// dQ = dS K needs the contraction over keys, which sit on the lanes: every wave writes its dS tile transposed
+// (dS^T [key][query], bf16, the same values the dK product consumes) into LDS, and after one barrier wave w forms
+// dQ^T for queries 16w .. 16w+15 of the tile over all 128 keys of the workgroup from transposed reads of dS^T and
+// of the workgroup's key block (staged once). One key block (S <= 128: cross-attention over the 77 text tokens)
+// stores dQ directly; otherwise every key block writes an fp32 partial and the LAST of the gridDim.x key blocks to
+// finish a (b*h, query tile) -- device-scope arrival counter, no spinning -- sums the partials in key-block order
+// (deterministic) and stores dQ. Partials are written and read with sc1 (device-coherent) buffer operations: the
+// summing workgroup may run on another XCD. delta = rowsum(dO * O) comes from attn_delta_kernel.
+// =============================================================================================
+constexpr int LDQ = TILE + 8;  // dS^T image row: 64 queries + 16 B of padding
+
+template <int LD>
+__device__ __forceinline__ s16x8 frag_tr_ld(const bf16_t* t, int rbase, int cbase, int lane) {
+  int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16_t* a1 = t + (rbase + 4 * g + q) * LD + cbase + 4 * p;
+  const bf16_t* a2 = a1 + 16 * LD;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SDMI_LDS s16x4*)a1);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SDMI_LDS s16x4*)a2);
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+constexpr int ATTN_CPOL_SC1 = 16;  // buffer cache policy: device (agent) scope coherence
+
+template <int DT>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_fused_kernel(AttnArgs a) {
+  constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
+  constexpr int LDK = Tile<DP>::LD;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][Q|dO]
+  __shared__ __attribute__((aligned(16))) bf16_t sK[ROWS * LDK];             // this workgroup's key block
+  __shared__ __attribute__((aligned(16))) bf16_t sDS[ROWS * LDQ];            // dS^T of the current query tile
+  __shared__ __attribute__((aligned(16))) float sLD[2][2][64];               // [buf][-lse|-delta]
+  __shared__ int sflag;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  const int kb = blockIdx.x, nkb = gridDim.x;
+  const float c = a.scale * LOG2E;
+  const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
+  const bf16_t* dO = a.dout + (long long)b * a.N * a.lddo;
+  const bf16_t* Kb = a.k + (long long)b * a.S * a.ldk;
+
+  {  // the workgroup's 128 keys (rows >= S zero) for the dQ products
+    uint4 rk[Tile<DP>::CPT];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      tile_fetch<DP>(rk, Kb, a.ldk, kb * ROWS + half * TILE, a.S, h * a.d, a.d);
+      tile_store<DP>(sK + half * TILE * LDK, rk);
+    }
+  }
+  int mykey[2];
+  bool kok[2];
+  s16x8 kf[2][KS], vf[2][KS];
+  f32x4 dk[2][DT], dv[2][DT];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    mykey[g] = kb * ROWS + wave * 32 + g * 16 + (lane & 15);
+    kok[g] = mykey[g] < a.S;
+    row_frags<DP>(kf[g], Kb, a.ldk, mykey[g], a.S, h * a.d, a.d, lane);
+    row_frags<DP>(vf[g], a.v + (long long)b * a.S * a.ldv, a.ldv, mykey[g], a.S, h * a.d, a.d, lane);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) dk[g][t] = dv[g][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+
+  uint4 rq[Tile<DP>::CPT], ro[Tile<DP>::CPT];
+  float rl = 0.f, rd = 0.f;
+  auto fetch = [&](int q0) __attribute__((always_inline)) {
+    tile_fetch<DP>(rq, Q, a.ldq, q0, a.N, h * a.d, a.d);
+    tile_fetch<DP>(ro, dO, a.lddo, q0, a.N, h * a.d, a.d);
+    if (threadIdx.x < 64) {
+      int q = q0 + threadIdx.x;
+      rl = q < a.N ? -a.lse[(long long)bh * a.N + q] : -INFINITY;  // invalid rows: p = 0
+      rd = q < a.N ? -a.delta[(long long)bh * a.N + q] : 0.f;
+    }
+  };
+  auto put = [&](int buf) __attribute__((always_inline)) {
+    tile_store<DP>(smem + buf * 2 * Tile<DP>::ELEMS, rq);
+    tile_store<DP>(smem + buf * 2 * Tile<DP>::ELEMS + Tile<DP>::ELEMS, ro);
+    if (threadIdx.x < 64) {
+      sLD[buf][0][threadIdx.x] = rl;
+      sLD[buf][1][threadIdx.x] = rd;
+    }
+  };
+  const __amdgpu_buffer_rsrc_t rsP = __builtin_amdgcn_make_buffer_rsrc((void*)a.dq_part, (short)0, 0x7fffffff, 0x00020000);
+  const int ntq = (a.N + TILE - 1) / TILE;
+  fetch(0);
+  put(0);
+  __syncthreads();
+  int cur = 0;
+  const f32x2_t cc = {c, c};
+  for (int q0 = 0; q0 < a.N; q0 += TILE) {
+    const bool more = q0 + TILE < a.N;
+    if (more) fetch(q0 + TILE);
+    const bf16_t* sQ = smem + cur * 2 * Tile<DP>::ELEMS;
+    const bf16_t* sO = sQ + Tile<DP>::ELEMS;
+    f32x4 p[2][4], ds[2][4];
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb) {
+      const int qi = qb * 16 + (lane >> 4) * 4;
+      const f32x4 nL = *(const f32x4*)&sLD[cur][0][qi], nD = *(const f32x4*)&sLD[cur][1][qi];
+      p[0][qb] = p[1][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      ds[0][qb] = ds[1][qb] = nD;  // dP accumulates on top of -delta
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s16x8 qa = frag_rows<DP>(sQ, qb * 16, ks * 32, lane);
+        s16x8 oa = frag_rows<DP>(sO, qb * 16, ks * 32, lane);
+        p[0][qb] = mfma(qa, kf[0][ks], p[0][qb]);
+        p[1][qb] = mfma(qa, kf[1][ks], p[1][qb]);
+        ds[0][qb] = mfma(oa, vf[0][ks], ds[0][qb]);
+        ds[1][qb] = mfma(oa, vf[1][ks], ds[1][qb]);
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        f32x2_t p0 = __builtin_elementwise_fma(lo2(p[g][qb]), cc, lo2(nL));
+        f32x2_t p1 = __builtin_elementwise_fma(hi2(p[g][qb]), cc, hi2(nL));
+        p0 = (f32x2_t){fast_exp2(p0[0]), fast_exp2(p0[1])};
+        p1 = (f32x2_t){fast_exp2(p1[0]), fast_exp2(p1[1])};
+        if (!kok[g]) p0 = p1 = (f32x2_t){0.f, 0.f};  // keys >= S (zero K rows) must not reach dQ
+        const f32x2_t d0 = p0 * lo2(ds[g][qb]), d1 = p1 * hi2(ds[g][qb]);
+        p[g][qb] = (f32x4){p0[0], p0[1], p1[0], p1[1]};
+        ds[g][qb] = (f32x4){d0[0], d0[1], d1[0], d1[1]};
+        uint2 w;
+        w.x = pack2bf(d0[0], d0[1]);
+        w.y = pack2bf(d1[0], d1[1]);
+        *(uint2*)(sDS + (wave * 32 + g * 16 + (lane & 15)) * LDQ + qb * 16 + (lane >> 4) * 4) = w;
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      s16x8 pf0 = pack_acc(p[0][2 * s2], p[0][2 * s2 + 1]), pf1 = pack_acc(p[1][2 * s2], p[1][2 * s2 + 1]);
+      s16x8 df0 = pack_acc(ds[0][2 * s2], ds[0][2 * s2 + 1]), df1 = pack_acc(ds[1][2 * s2], ds[1][2 * s2 + 1]);
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        s16x8 ot = frag_tr<DP>(sO, 32 * s2, 16 * t, lane);
+        dv[0][t] = mfma(ot, pf0, dv[0][t]);
+        dv[1][t] = mfma(ot, pf1, dv[1][t]);
+        s16x8 qt = frag_tr<DP>(sQ, 32 * s2, 16 * t, lane);
+        dk[0][t] = mfma(qt, df0, dk[0][t]);
+        dk[1][t] = mfma(qt, df1, dk[1][t]);
+      }
+    }
+    __syncthreads();  // dS^T of every wave in LDS
+    // dQ^T[d][q] for the tile's queries 16*wave .. +15 over the workgroup's 128 keys: lane holds d = 16t + 4(lane>>4)
+    // .. +3 of query 16*wave + (lane & 15)
+    f32x4 dq[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) dq[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < ROWS / 32; ++ks) {
+      s16x8 sb = frag_tr_ld<LDQ>(sDS, ks * 32, wave * 16, lane);
+#pragma unroll
+      for (int t = 0; t < DT; ++t) dq[t] = mfma(frag_tr_ld<LDK>(sK, ks * 32, t * 16, lane), sb, dq[t]);
+    }
+    const int myq = q0 + wave * 16 + (lane & 15);
+    if (nkb == 1) {
+      if (myq < a.N) {
+        bf16_t* DQ = a.dq + ((long long)b * a.N + myq) * a.lddq + h * a.d;
+#pragma unroll
+        for (int t = 0; t < DT; ++t) {
+          const int d0 = 16 * t + (lane >> 4) * 4;
+          if (d0 < a.d) store4(DQ + d0, dq[t], a.scale);
+        }
+      }
+    } else {
+      if (myq < a.N) {
+#pragma unroll
+        for (int t = 0; t < DT; ++t) {
+          const int d0 = 16 * t + (lane >> 4) * 4;
+          if (d0 < a.d) {
+            const int off = ((((kb * a.B * a.H + bh) * a.N) + myq) * a.d + d0) * 4;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, dq[t]), rsP, off, 0, ATTN_CPOL_SC1);
+          }
+        }
+      }
+      // arrival: the partial stores (and the next tile's loads) complete, then one relaxed device-scope increment;
+      // the last key block of this (b*h, query tile) sums the partials
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned* ctr = a.ctr + (long long)bh * ntq + q0 / TILE;
+        const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == (unsigned)(nkb - 1);
+        if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sflag = last;
+      }
+      __syncthreads();
+      if (sflag) {
+        const int c4 = a.d / 4;
+        for (int i = threadIdx.x; i < TILE * c4; i += NT) {
+          const int r = i / c4, d0 = (i - r * c4) * 4, q = q0 + r;
+          if (q >= a.N) continue;
+          f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+          for (int z = 0; z < nkb; ++z) {
+            const int off = ((((z * a.B * a.H + bh) * a.N) + q) * a.d + d0) * 4;
+            acc += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, off, 0, ATTN_CPOL_SC1));
+          }
+          store4(a.dq + ((long long)b * a.N + q) * a.lddq + h * a.d + d0, acc, a.scale);
+        }
+      }
+    }
+    if (more) put(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+    if (kok[g]) {
+      bf16_t* DK = a.dk + ((long long)b * a.S + mykey[g]) * a.lddk + h * a.d;
+      bf16_t* DV = a.dv + ((long long)b * a.S + mykey[g]) * a.lddv + h * a.d;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        int d0 = 16 * t + (lane >> 4) * 4;
+        if (d0 < a.d) {
+          store4(DK + d0, dk[g][t], a.scale);
+          store4(DV + d0, dv[g][t], 1.f);
+        }
+      }
+    }
+}
+
+// delta[b*h][q] = rowsum(dO * O) over the head's d columns (fp32), one thread per (b, q, h)
+__global__ __launch_bounds__(NT) void attn_delta_kernel(AttnArgs a) {
+  const long long i = (long long)blockIdx.x * NT + threadIdx.x;
+  const long long total = (long long)a.B * a.N * a.H;
+  if (i >= total) return;
+  const int h = (int)(i % a.H);
+  const long long bq = i / a.H;
+  const int q = (int)(bq % a.N), b = (int)(bq / a.N);
+  const bf16_t* o = a.o + bq * a.ldo + h * a.d;
+  const bf16_t* g = a.dout + bq * a.lddo + h * a.d;
+  float D = 0.f;
+  for (int c0 = 0; c0 < a.d; c0 += 8) {
+    float x[8], y[8];
+    unpack8(*(const uint4*)(o + c0), x);
+    unpack8(*(const uint4*)(g + c0), y);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) D = fmaf(x[e], y[e], D);
+  }
+  ((float*)a.delta)[((long long)b * a.H + h) * a.N + q] = D;
+}
+
+constexpr int ATTN_CTR_SLOTS = 4, ATTN_CTR_SLOT = 1 << 16;
+__device__ unsigned g_attn_counters[ATTN_CTR_SLOTS * ATTN_CTR_SLOT];
+
 int check_args(const AttnArgs& a) {
   if (a.B <= 0 || a.H <= 0 || a.N <= 0 || a.S <= 0 || a.d <= 0) return -1;
   if (a.d % 8 || a.d > 64) return -2;
@@ -608,6 +860,54 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
     SDMI_ATTN_BWD(3)
     default: SDMI_ATTN_BWD(4)
 #undef SDMI_ATTN_BWD
+  }
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// fused backward (attn_bwd_fused_kernel): fp32 dQ partial workspace bytes (0 when the keys fit one key block)
+extern "C" size_t sdmi_attn_bwd_workspace(int B, int H, int N, int S, int d) {
+  const long long nkb = (S + ROWS - 1) / ROWS;
+  return nkb > 1 ? (size_t)(nkb * B * H * (long long)N * d * 4) : 0;
+}
+
+extern "C" int sdmi_attn_bwd_fused(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv,
+                                   const void* o, int ldo, const void* dout, int lddo, const float* lse,
+                                   float* delta_ws, void* ws, size_t ws_bytes, void* dq, int lddq, void* dk,
+                                   int lddk, void* dv, int lddv, int B, int H, int N, int S, int d,
+                                   sdmi_stream_t stream) {
+  AttnArgs a = {};
+  a.q = (const bf16_t*)q; a.k = (const bf16_t*)k; a.v = (const bf16_t*)v; a.o = (const bf16_t*)o;
+  a.dout = (const bf16_t*)dout; a.lse = (float*)lse; a.delta = delta_ws;
+  a.dq = (bf16_t*)dq; a.dk = (bf16_t*)dk; a.dv = (bf16_t*)dv;
+  a.ldq = ldq; a.ldk = ldk; a.ldv = ldv; a.ldo = ldo; a.lddo = lddo; a.lddq = lddq; a.lddk = lddk; a.lddv = lddv;
+  a.B = B; a.H = H; a.N = N; a.S = S; a.d = d; a.scale = 1.0f / sqrtf((float)d);
+  int rc = check_args(a);
+  if (rc) return rc;
+  const size_t need = sdmi_attn_bwd_workspace(B, H, N, S, d);
+  const long long ntq = (N + TILE - 1) / TILE;
+  // partial offsets are 32-bit buffer offsets; counters: one slot region per launch
+  if (need && (!ws || ws_bytes < need || need >= (1ull << 31) || (long long)B * H * ntq > ATTN_CTR_SLOT)) return -3;
+  static unsigned* ctr_base = nullptr;
+  static int next = 0;
+  if (need) {
+    if (!ctr_base) {
+      void* p = nullptr;
+      if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_attn_counters)) != hipSuccess) return -4;
+      ctr_base = (unsigned*)p;
+    }
+    a.ctr = ctr_base + (size_t)(next++ % ATTN_CTR_SLOTS) * ATTN_CTR_SLOT;
+    a.dq_part = (float*)ws;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const long long rows = (long long)B * N * H;
+  sdmi_rt::launch(attn_delta_kernel, dim3((unsigned)((rows + NT - 1) / NT)), dim3(NT), 0, s, a);
+  dim3 gk((S + ROWS - 1) / ROWS, B * H);
+  switch ((d + 15) / 16) {
+    case 1: sdmi_rt::launch(attn_bwd_fused_kernel<1>, gk, dim3(NT), 0, s, a); break;
+    case 2: sdmi_rt::launch(attn_bwd_fused_kernel<2>, gk, dim3(NT), 0, s, a); break;
+    case 3: sdmi_rt::launch(attn_bwd_fused_kernel<3>, gk, dim3(NT), 0, s, a); break;
+    default: sdmi_rt::launch(attn_bwd_fused_kernel<4>, gk, dim3(NT), 0, s, a); break;
   }
   SDMI_CHECK_LAUNCH();
   return 0;

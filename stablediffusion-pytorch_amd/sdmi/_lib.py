@@ -76,6 +76,9 @@ SIGNATURES = {
     "sdmi_attn_fwd": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _P], _I),
     "sdmi_attn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _I, _P, _I, _P, _I,
                        _I, _I, _I, _I, _I, _P], _I),
+    "sdmi_attn_bwd_workspace": ([_I, _I, _I, _I, _I], _SZ),
+    "sdmi_attn_bwd_fused": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _P, _SZ, _P, _I, _P, _I, _P, _I,
+                             _I, _I, _I, _I, _I, _P], _I),
     "sdmi_chan_reduce_workspace": ([_I, _I, _I], _SZ),
     "sdmi_gn_stats": ([_P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
     "sdmi_gn_apply": ([_P, _I, _P, _I, _P, _I, _I, _I, _I, _P], _I),

@@ -74,12 +74,19 @@ class _Prof:
             PROFILE.append((self.tag, self.flops, self.e0, self.e1, f"[{PHASE}] {self.info}" if PHASE else self.info))
 
 
+# SDMI_DIAG_SKIP (diagnostics only -- the step then trains wrongly): "wg" leaves out every weight-gradient GEMM,
+# "opt" the optimizer + weight packing, to attribute the overlapped step's time (scripts/gpu_diag.sh)
+DIAG_SKIP = set(filter(None, os.environ.get("SDMI_DIAG_SKIP", "").split(",")))
+
+
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
          rb_ld=0, rb_div=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0,
          a2=None, lda2=0, k_split=0, bias2=None, rb_mod=0, aux=None, ld_aux=0, sum_out=None, sum_out2=None,
          gsum=None, sum_group=0):
     """C[m][n] = epi(sum_k A[m][k] B[k][n]).  a/b/c/resid/rowbias are tensors (pointer = data_ptr,
     offsets already applied by slicing); see include/sdmi.h for the operand modes."""
+    if "wg" in DIAG_SKIP and PHASE == "wg":
+        return c
     L = _lib.lib()
     d = GemmDesc()
     d.m, d.n, d.k = m, n, k
@@ -320,12 +327,25 @@ def attn_fwd(q, k, v, out, B, H, N, S, d):
     return lse
 
 
-def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, B, H, N, S, d):
+# SDMI_ATTN_FUSED=1: the fused one-pass backward (attn_bwd_fused_kernel) instead of the dQ pass + dK/dV pass
+ATTN_FUSED = os.environ.get("SDMI_ATTN_FUSED", "0") != "0"
+
+
+def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, B, H, N, S, d, fused=None):
+    L = _lib.lib()
     delta = torch.empty(B * H * N, dtype=torch.float32, device=q.device)
+    fused = ATTN_FUSED if fused is None else fused
     with _Prof("attn_bwd", 10.0 * B * H * N * S * d, f"B={B} H={H} N={N} S={S} d={d}"):
-      check(_lib.lib().sdmi_attn_bwd(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(o), ld_of(o), _p(dout),
-                                   ld_of(dout), _p(lse), _p(delta), _p(dq), ld_of(dq), _p(dk), ld_of(dk), _p(dv),
-                                   ld_of(dv), B, H, N, S, d, _stream()), "sdmi_attn_bwd")
+        if fused:
+            nws = L.sdmi_attn_bwd_workspace(B, H, N, S, d)
+            ws = torch.empty(max(nws // 4, 1), dtype=torch.float32, device=q.device)
+            check(L.sdmi_attn_bwd_fused(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(o), ld_of(o), _p(dout),
+                                        ld_of(dout), _p(lse), _p(delta), _p(ws), nws, _p(dq), ld_of(dq), _p(dk),
+                                        ld_of(dk), _p(dv), ld_of(dv), B, H, N, S, d, _stream()), "sdmi_attn_bwd_fused")
+        else:
+            check(L.sdmi_attn_bwd(_p(q), ld_of(q), _p(k), ld_of(k), _p(v), ld_of(v), _p(o), ld_of(o), _p(dout),
+                                  ld_of(dout), _p(lse), _p(delta), _p(dq), ld_of(dq), _p(dk), ld_of(dk), _p(dv),
+                                  ld_of(dv), B, H, N, S, d, _stream()), "sdmi_attn_bwd")
 
 
 def conv_dgrad_phases(dy, B, H, W, cout, ldy, wph, cin, out, ldo, *, resid=None, ldr=0):

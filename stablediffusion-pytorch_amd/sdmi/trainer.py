@@ -209,7 +209,7 @@ class DDPMTrainer:
         side = eng.side
         plan.wait_stream(side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
-            for c, (lo, hi) in enumerate(self.opt_ranges):
+            for c, (lo, hi) in enumerate(self.opt_ranges if "opt" not in K.DIAG_SKIP else ()):
                 e = self.ema[lo:hi] if self.ema is not None else None
                 _lib.check(L.sdmi_adam_ema(st.params[lo:hi].data_ptr(), st.grads[lo:hi].data_ptr(),
                                            self.m[lo:hi].data_ptr(), self.v[lo:hi].data_ptr(), K._p(e), hi - lo,

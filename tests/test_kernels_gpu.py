@@ -75,8 +75,10 @@ def test_groupnorm_fwd_bwd(B, H, C, G, silu):
 # d = 8, 24, 40 take the forward's ones-column row sum (d % 16 == 8), incl. ragged N and S = 77
 @pytest.mark.parametrize("B,Hh,N,S,d", [(2, 16, 64, 64, 8), (2, 16, 256, 256, 24), (1, 16, 16, 77, 32),
                                         (2, 4, 1024, 1024, 16), (2, 16, 64, 77, 48), (1, 8, 100, 100, 64),
-                                        (1, 16, 40, 77, 24), (1, 4, 33, 70, 40)])
-def test_attention_fwd_bwd(B, Hh, N, S, d):
+                                        (1, 16, 40, 77, 24), (1, 4, 33, 70, 40), (1, 4, 300, 300, 24),
+                                        (2, 2, 130, 257, 32)])
+@pytest.mark.parametrize("fused", [True, False])
+def test_attention_fwd_bwd(B, Hh, N, S, d, fused):
     k = K()
     torch.manual_seed(1)
     C = Hh * d
@@ -102,10 +104,14 @@ def test_attention_fwd_bwd(B, Hh, N, S, d):
     dq = torch.empty_like(q)
     dk = torch.empty_like(kk)
     dv = torch.empty_like(v)
-    k.attn_bwd(q, kk, v, o, do, lse, dq, dk, dv, B, Hh, N, S, d)
+    k.attn_bwd(q, kk, v, o, do, lse, dq, dk, dv, B, Hh, N, S, d, fused=fused)
     assert relerr(heads(dq, N), qr.grad) < 3e-2
     assert relerr(heads(dk, S), kr.grad) < 3e-2
     assert relerr(heads(dv, S), vr.grad) < 3e-2
+    if fused:  # the cross-key-block dQ sum is in a fixed order: a second run is bitwise identical
+        dq2, dk2, dv2 = torch.empty_like(q), torch.empty_like(kk), torch.empty_like(v)
+        k.attn_bwd(q, kk, v, o, do, lse, dq2, dk2, dv2, B, Hh, N, S, d, fused=True)
+        assert torch.equal(dq, dq2) and torch.equal(dk, dk2) and torch.equal(dv, dv2)
 
 
 def test_chan_sum_and_mse():
