@@ -327,14 +327,19 @@ def attn_fwd(q, k, v, out, B, H, N, S, d):
     return lse
 
 
-# SDMI_ATTN_FUSED=1: the fused one-pass backward (attn_bwd_fused_kernel) instead of the dQ pass + dK/dV pass
-ATTN_FUSED = os.environ.get("SDMI_ATTN_FUSED", "0") != "0"
+# Attention backward: the fused one-pass kernel (attn_bwd_fused_kernel) where all keys fit one 128-key block and
+# there are >= 512 queries -- the 32x32 cross-attention over the 77 text tokens, dQ stored directly: 59.8 -> 50.6 us
+# at d = 16, 71.3 -> 68.7 us at d = 24 (B = 32, N = 1024). Otherwise the dQ pass + dK/dV pass: at S = 1024 the
+# fused kernel's cross-block dQ partials made it 1.5-4x slower (296 -> 490 us at d = 16, 322 -> 1347 us at d = 24),
+# and at N = S = 64 / 16 its single query tile per workgroup lost 1-2 us. SDMI_ATTN_FUSED=0 / 1 forces either path.
+ATTN_FUSED = os.environ.get("SDMI_ATTN_FUSED", "auto")
 
 
 def attn_bwd(q, k, v, o, dout, lse, dq, dk, dv, B, H, N, S, d, fused=None):
     L = _lib.lib()
     delta = torch.empty(B * H * N, dtype=torch.float32, device=q.device)
-    fused = ATTN_FUSED if fused is None else fused
+    if fused is None:
+        fused = (S <= 128 and N >= 512) if ATTN_FUSED == "auto" else ATTN_FUSED != "0"
     with _Prof("attn_bwd", 10.0 * B * H * N * S * d, f"B={B} H={H} N={N} S={S} d={d}"):
         if fused:
             nws = L.sdmi_attn_bwd_workspace(B, H, N, S, d)
