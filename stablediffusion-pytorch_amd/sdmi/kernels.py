@@ -74,6 +74,11 @@ class _Prof:
             PROFILE.append((self.tag, self.flops, self.e0, self.e1, f"[{PHASE}] {self.info}" if PHASE else self.info))
 
 
+# split-K cap for the weight-gradient GEMMs currently issued (set per backward block by the UNet engine, 0 = none):
+# weight gradients that overlap the rest of the backward need not fill the chip, and fewer slices write and re-read
+# fewer fp32 slabs; the last blocks' weight gradients (the step's tail) keep their measured split counts
+WG_CAP = 0
+
 # SDMI_DIAG_SKIP (diagnostics only -- the step then trains wrongly): "wg" leaves out every weight-gradient GEMM,
 # "opt" the optimizer + weight packing, to attribute the overlapped step's time (scripts/gpu_diag.sh)
 DIAG_SKIP = set(filter(None, os.environ.get("SDMI_DIAG_SKIP", "").split(",")))
@@ -137,6 +142,9 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
+    if WG_CAP and PHASE == "wg" and splits.value > WG_CAP:  # see WG_CAP
+        d.splits_hint = WG_CAP
+        check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
     ws = None
     if ws_bytes.value:
         ws = torch.empty(ws_bytes.value // 4, dtype=torch.float32, device=c.device)

@@ -917,7 +917,7 @@ class UNetEngine:
                 K.linear_dgrad(dq, Win[:C], da)
         # x receives dy (residual) + GroupNorm-branch gradient
         key, off, _ = grads.groups[c["xn"]]
-        if not grads.init.get(c["xn"], False) and dy.is_contiguous() and K.ld_of(dy) == C and \
+        if self._dy_alias and not grads.init.get(c["xn"], False) and dy.is_contiguous() and K.ld_of(dy) == C and \
                 grads.shapes.get(key, (0, 0))[1] == C:
             grads.alias(c["xn"], dy)
             dx, addend = dy, dy
@@ -1117,6 +1117,9 @@ class UNetEngine:
         K.PHASE = "bwd"
         for k in range(len(tape) - 1, -1, -1):
             fn, c = tape[k]
+            # SDMI_WG_CAP_EARLY = n: weight gradients of every block but the tail ones (the first down level, the
+            # input / time-embedding ends) split at most n ways (kernels.WG_CAP)
+            K.WG_CAP = 0 if c.get("label") in self._tail_labels else self._wg_cap_early
             fn(c, grads)
             if on_progress is not None:
                 on_progress(tape, k)
@@ -1124,6 +1127,13 @@ class UNetEngine:
         self._keep = []
         self.dpred = None
         K.PHASE = ""
+        K.WG_CAP = 0
+
+    # SDMI_DY_ALIAS=1: an attention block's input gradient reuses its output-gradient buffer (the GroupNorm backward
+    # then rewrites dy in place, so the main stream first waits for the side-stream weight gradient reading dy)
+    _dy_alias = os.environ.get("SDMI_DY_ALIAS", "1") != "0"
+    _wg_cap_early = int(os.environ.get("SDMI_WG_CAP_EARLY", "0"))
+    _tail_labels = set(os.environ.get("SDMI_WG_TAIL", "downs.0,input,time").split(","))
 
     def _ctx_grad_view(self):
         """The context_proj weight gradients are one contiguous [sum C][ctx_dim] region of the flat store."""
