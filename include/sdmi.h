@@ -348,6 +348,38 @@ int sdmi_loss_flag(const float* src, float* dst, int mode, sdmi_stream_t stream)
  * from Python doubles, :376-378) */
 int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n, const float* state,
                   float lr, float b1, float b2, float eps, float ema_decay, float ema_alpha, sdmi_stream_t stream);
+/* The same step also writing params_bf16[i] = bf16(params[i]) (round to nearest even; untouched on a skipped step):
+ * the autocast weight cast folded into the optimizer pass. The trainer keeps a bf16 image of the flat parameter
+ * buffer this way, and every weight whose GEMM layout is its flat layout is read from it directly (no repack). */
+int sdmi_adam_ema_bf16(float* params, const float* grads, float* m, float* v, float* ema, long long n,
+                       const float* state, float lr, float b1, float b2, float eps, float ema_decay, float ema_alpha,
+                       void* params_bf16, sdmi_stream_t stream);
+/* dst[i] = bf16(src[i]) over n elements (src 16-B, dst 8-B aligned): the initial bf16 parameter image */
+int sdmi_cast_bf16(const float* src, void* dst, long long n, sdmi_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Leaf-path glue (sdmi/leaf.py; fp32 torch layouts): what the reference computes with aten between its layers.
+ * sdmi_resize_nearest: F.interpolate(mode='nearest') of BC planes IHxIW -> OHxOW (unet_cond_base.py:132,
+ *   transformer.py:169): src = min(floor(dst * (float)in / out), in - 1).
+ * sdmi_chan_copy: NCHW channel slab dst[b][dst_c0 + c][p] = src[b][src_c0 + c][p] (torch.cat along dim 1 and the
+ *   split of its gradient, unet_cond_base.py:136, transformer.py:170).
+ * sdmi_modulate_fwd / _bwd: y = r + x * (alpha + s[b][c]) + t[b][c] over (B, N, C) rows (s, t row stride ls; r, t
+ *   optional): the DiT's adaLN modulation (alpha 1, transformer_layer.py:86-88, :97-99, transformer.py:205-207) and
+ *   gated residual (alpha 0, r = the stream, transformer_layer.py:89, :100); backward dx = dy * (alpha + s),
+ *   ds = sum_n dy * x, dt = sum_n dy (each output optional; dr = dy is the caller's).
+ * sdmi_attn_map: the attention weights an MHA returns for need_weights=True (multihead_attention.py:107-118):
+ *   softmax(q_h k_h^T * scaling) per head from fp32 rows q [B*N][ldq], k [B*S][ldk] (head h at columns h*d..),
+ *   averaged over heads into out (B, N, S), or per head into (B, H, N, S); S <= 4096.
+ * ------------------------------------------------------------------------------------------- */
+int sdmi_resize_nearest(const float* in, int BC, int IH, int IW, float* out, int OH, int OW, sdmi_stream_t stream);
+int sdmi_chan_copy(const float* src, int src_c, int src_c0, float* dst, int dst_c, int dst_c0, int B, int C,
+                   long long P, sdmi_stream_t stream);
+int sdmi_modulate_fwd(const float* x, const float* r, const float* s, const float* t, int ls, float alpha, float* y,
+                      int B, int N, int C, sdmi_stream_t stream);
+int sdmi_modulate_bwd(const float* x, const float* dy, const float* s, int ls, float alpha, float* dx, float* ds,
+                      float* dt, int B, int N, int C, sdmi_stream_t stream);
+int sdmi_attn_map(const float* q, int ldq, const float* k, int ldk, int B, int H, int N, int S, int d, float scaling,
+                  int average, float* out, sdmi_stream_t stream);
 
 /* Streams restricted to a share of the CUs (hipExtStreamCreateWithCUMask): keep_num of every keep_den CUs.
  * Used for the engine's weight-gradient side stream (SDMI_SIDE_CU=num/den), no reference counterpart. */

@@ -24,7 +24,7 @@ def timeit(fn, iters=20):
 def main():
     dev = "cuda"
     bf = torch.bfloat16
-    shapes = ((32, 16, 1024, 1024, 16), (32, 16, 1024, 1024, 24), (32, 16, 1024, 77, 16), (32, 16, 1024, 77, 24),
+    shapes = ((32, 16, 1024, 1024, 8), (32, 16, 1024, 1024, 16), (32, 16, 1024, 1024, 24), (32, 16, 1024, 77, 8), (32, 16, 1024, 77, 16), (32, 16, 1024, 77, 24),
               (32, 16, 256, 256, 24), (32, 16, 256, 256, 32), (32, 16, 64, 64, 32), (32, 16, 64, 64, 48),
               (32, 16, 16, 16, 48), (32, 9, 256, 256, 32))
     if len(sys.argv) > 1:  # one shape index (for per-kernel rocprof runs)

@@ -302,6 +302,22 @@ __global__ void pack_kernel(const sdmi_pack_desc* descs, const int2* bmap) {
   const int row = taps * d.Ipad;
   const int rows = max(1, PACK_CHUNK / row);
   const int o_end = min(d.O, bm.y + rows);
+  // identity layout (the packed rows are the source rows in the same order: linears, GEMM-natural conv weights, rows
+  // into a compact view): one contiguous cast, 8 elements per thread with 16-B loads and stores, no LDS staging
+  const bool ident = d.Ipad == d.I && d.si == 1 && d.dst_ld == 0 && d.kh_off == 0 && d.kh_mul == 1 && d.kw_off == 0 &&
+                     d.kw_mul == 1 && (d.KW == 1 || d.skw == d.I) && (d.KH == 1 || d.skh == (long long)d.KW * d.I) &&
+                     d.so == (long long)row && row % 8 == 0 && ((uintptr_t)d.src & 15) == 0 &&
+                     ((uintptr_t)d.dst & 15) == 0;
+  if (ident) {
+    const float* src = d.src + (long long)bm.y * row;
+    bf16_t* dst = (bf16_t*)d.dst + (long long)bm.y * row;
+    const int n8 = (o_end - bm.y) * row / 8;
+    for (int q = threadIdx.x; q < n8; q += NT) {
+      const float4 a = *(const float4*)(src + 8 * q), b = *(const float4*)(src + 8 * q + 4);
+      *(uint4*)(dst + 8 * q) = make_uint4(pack2bf(a.x, a.y), pack2bf(a.z, a.w), pack2bf(b.x, b.y), pack2bf(b.z, b.w));
+    }
+    return;
+  }
 #pragma unroll 1
   for (int o = bm.y; o < o_end; ++o) {
     const float* src = d.src + (long long)o * d.so;

@@ -98,10 +98,12 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
   if (ema) e = __builtin_fmaf(ema_alpha, p, mul_ieee(e, ema_decay));
 }
 
-// VEC = 4: 16-B loads / stores of all five streams (host checks the alignment), scalar tail in block 0
+// VEC = 4: 16-B loads / stores of all five streams (host checks the alignment), scalar tail in block 0.
+// pb (optional): bf16 image of the updated parameters at the same flat offsets -- the GEMM-ready copy of every weight
+// whose packed layout is its flat layout (linears, GEMM-natural conv weights), so no separate cast pass re-reads them
 template <int VEC>
 __global__ void adam_ema_kernel(float* p, const float* g, float* m, float* v, float* ema, long long n, const float* state,
-                                float lr, float b1, float b2, float eps, float ema_decay, float ema_alpha) {
+                                float lr, float b1, float b2, float eps, float ema_decay, float ema_alpha, bf16_t* pb) {
   if (state[5] != 0.f) return;  // skipped step
   const float gs = state[1];
   const int step = (int)state[4];
@@ -123,10 +125,12 @@ __global__ void adam_ema_kernel(float* p, const float* g, float* m, float* v, fl
       ((float4*)m)[i] = mi;
       ((float4*)v)[i] = vi;
       if (ema) ((float4*)ema)[i] = ei;
+      if (pb) *(uint2*)(pb + 4 * i) = make_uint2(pack2bf(pi.x, pi.y), pack2bf(pi.z, pi.w));
     } else {
       float e = ema ? ema[i] : 0.f;
       adam_one(p[i], g[i], m[i], v[i], e, ema != nullptr, gs, b1, b2, eps, step_size, bc2s, ema_decay, ema_alpha);
       if (ema) ema[i] = e;
+      if (pb) pb[i] = f2bf(p[i]);
     }
   }
   if (VEC > 1 && blockIdx.x == 0)
@@ -134,7 +138,19 @@ __global__ void adam_ema_kernel(float* p, const float* g, float* m, float* v, fl
       float e = ema ? ema[i] : 0.f;
       adam_one(p[i], g[i], m[i], v[i], e, ema != nullptr, gs, b1, b2, eps, step_size, bc2s, ema_decay, ema_alpha);
       if (ema) ema[i] = e;
+      if (pb) pb[i] = f2bf(p[i]);
     }
+}
+
+// pb[i] = bf16(p[i]) (round to nearest even): the initial image of the parameters (and after any host-side update)
+__global__ void cast_bf16_kernel(const float* p, bf16_t* pb, long long n) {
+  const long long n4 = n / 4;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
+    const float4 x = ((const float4*)p)[i];
+    *(uint2*)(pb + 4 * i) = make_uint2(pack2bf(x.x, x.y), pack2bf(x.z, x.w));
+  }
+  if (blockIdx.x == 0)
+    for (long long i = n4 * 4 + threadIdx.x; i < n; i += NT) pb[i] = f2bf(p[i]);
 }
 }  // namespace
 
@@ -162,6 +178,22 @@ extern "C" int sdmi_loss_flag(const float* src, float* dst, int mode, sdmi_strea
 extern "C" int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n,
                              const float* state, float lr, float b1, float b2, float eps, float ema_decay,
                              float ema_alpha, sdmi_stream_t stream) {
+  return sdmi_adam_ema_bf16(params, grads, m, v, ema, n, state, lr, b1, b2, eps, ema_decay, ema_alpha, nullptr, stream);
+}
+
+extern "C" int sdmi_cast_bf16(const float* src, void* dst, long long n, sdmi_stream_t stream) {
+  if (!src || !dst || n < 0 || ((uintptr_t)src & 15) || ((uintptr_t)dst & 7)) return -1;
+  if (n == 0) return 0;
+  long long blocks = (n / 4 + NT - 1) / NT;
+  blocks = blocks < 1 ? 1 : blocks > 8192 ? 8192 : blocks;
+  sdmi_rt::launch(cast_bf16_kernel, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, src, (bf16_t*)dst, n);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_adam_ema_bf16(float* params, const float* grads, float* m, float* v, float* ema, long long n,
+                                  const float* state, float lr, float b1, float b2, float eps, float ema_decay,
+                                  float ema_alpha, void* params_bf16, sdmi_stream_t stream) {
   static long long max_blocks = -1;  // grid cap (SDMI_ADAM_BLOCKS): a narrower grid leaves CUs to concurrent work
   if (max_blocks < 0) {
     const char* e = getenv("SDMI_ADAM_BLOCKS");
@@ -173,16 +205,17 @@ extern "C" int sdmi_adam_ema(float* params, const float* grads, float* m, float*
     const char* e = getenv("SDMI_ADAM_VEC");
     allow_vec = e ? atoi(e) != 0 : 1;
   }
-  const bool vec = allow_vec && ((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)m | (uintptr_t)v | (uintptr_t)ema) & 15) == 0);
+  const bool vec = allow_vec && ((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)m | (uintptr_t)v | (uintptr_t)ema) & 15) == 0) &&
+                   ((uintptr_t)params_bf16 & 7) == 0;
   long long blocks = (n / (vec ? 4 : 1) + NT - 1) / NT;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
   if (vec)
     sdmi_rt::launch(adam_ema_kernel<4>, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v,
-                    ema, n, state, lr, b1, b2, eps, ema_decay, ema_alpha);
+                    ema, n, state, lr, b1, b2, eps, ema_decay, ema_alpha, (bf16_t*)params_bf16);
   else
     sdmi_rt::launch(adam_ema_kernel<1>, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v,
-                    ema, n, state, lr, b1, b2, eps, ema_decay, ema_alpha);
+                    ema, n, state, lr, b1, b2, eps, ema_decay, ema_alpha, (bf16_t*)params_bf16);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

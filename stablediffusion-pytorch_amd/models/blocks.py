@@ -150,7 +150,7 @@ class UpBlock(_ParamBlock):
     def forward(self, x, out_down=None, t_emb=None):
         x = LF.call(self.up_sample_conv, x)
         if out_down is not None:
-            x = torch.cat([x, out_down], dim=1)
+            x = LF.cat_channels([x, out_down])
         out = x
         for i in range(self.num_layers):
             out = _resnet(self, i, out, t_emb)
@@ -179,7 +179,7 @@ class UpBlockUnet(_ParamBlock):
     def forward(self, x, out_down=None, t_emb=None, context=None):
         x = LF.call(self.up_sample_conv, x)
         if out_down is not None:
-            x = torch.cat([x, out_down], dim=1)
+            x = LF.cat_channels([x, out_down])
         out = x
         for i in range(self.num_layers):
             out = _resnet(self, i, out, t_emb)

@@ -42,10 +42,6 @@ class CustomMultiheadAttention(nn.Module):
         if not self.batch_first:
             out = out.transpose(0, 1)
         weights = None
-        if need_weights:  # the attention map itself (a diagnostic output; the flash kernel never materialises it)
-            B, N, S = q.shape[0], q.shape[1], k.shape[1]
-            qh = q.reshape(B, N, self.num_heads, self.head_dim).transpose(1, 2)
-            kh = k.reshape(B, S, self.num_heads, self.head_dim).transpose(1, 2)
-            weights = torch.softmax(qh @ kh.transpose(-2, -1) * self.scaling, dim=-1)
-            weights = weights.mean(dim=1) if average_attn_weights else weights
+        if need_weights:  # the attention map itself (a diagnostic output the flash kernel never materialises)
+            weights = LF.attention_map(q, k, self.num_heads, self.scaling, average_attn_weights)
         return out, weights

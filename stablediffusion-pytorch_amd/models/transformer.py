@@ -119,8 +119,8 @@ class DIT(nn.Module):
     def _leaf_forward(self, x, t, text, mask, klass):
         patch_source = x
         if self.image_cond:
-            im_cond = torch.nn.functional.interpolate(mask.to(device=x.device, dtype=x.dtype), size=x.shape[-2:])
-            patch_source = torch.cat([patch_source, LF.call(self.cond_conv_in, im_cond)], dim=1)
+            im_cond = LF.resize_nearest(mask.to(device=x.device, dtype=torch.float32), x.shape[-2:])
+            patch_source = LF.cat_channels([patch_source, LF.call(self.cond_conv_in, im_cond)])
         out = self.patch_embed_layer(patch_source)
         t_emb = LF.time_embedding(t, x.shape[0], self.timestep_emb_dim, x.device)
         if self.class_cond:
@@ -129,7 +129,7 @@ class DIT(nn.Module):
         for layer in self.transformer_layers:
             out = layer(out, t_emb, text)
         shift, scale = LF.call(self.adaptive_norm_layer, t_emb).chunk(2, dim=1)
-        out = LF.call(self.norm, out) * (1 + scale.unsqueeze(1)) + shift.unsqueeze(1)
+        out = LF.modulate(LF.call(self.norm, out), scale, shift)  # norm(out) * (1 + scale) + shift
         out = LF.call(self.proj_out, out)
         B, _, H, W = x.shape
         ph, pw = self.patch_height, self.patch_width

@@ -46,11 +46,12 @@ class TransformerLayer(nn.Module):
         (pre_attn_shift, pre_attn_scale, post_attn_scale, pre_mlp_shift, pre_mlp_scale,
          post_mlp_scale) = LF.call(self.adaptive_norm_layer, condition).chunk(6, dim=1)
         out = x
-        h = LF.call(self.att_norm, out) * (1 + pre_attn_scale.unsqueeze(1)) + pre_attn_shift.unsqueeze(1)
-        out = out + post_attn_scale.unsqueeze(1) * self.attn_block(h)
+        # adaLN modulation and gated residuals on the leaf-glue kernels (sdmi_modulate_fwd / _bwd)
+        h = LF.modulate(LF.call(self.att_norm, out), pre_attn_scale, pre_attn_shift)
+        out = LF.modulate(self.attn_block(h), post_attn_scale, r=out, alpha=0.0)
         if self.cross_attn and context is not None:
             ctx = LF.call(self.context_proj, context)
             o, _ = self.cross_attn_block(LF.call(self.cross_attn_norm, out), ctx, ctx, need_weights=False)
             out = out + o
-        h = LF.call(self.ff_norm, out) * (1 + pre_mlp_scale.unsqueeze(1)) + pre_mlp_shift.unsqueeze(1)
-        return out + post_mlp_scale.unsqueeze(1) * LF.call(self.mlp_block, h)
+        h = LF.modulate(LF.call(self.ff_norm, out), pre_mlp_scale, pre_mlp_shift)
+        return LF.modulate(LF.call(self.mlp_block, h), post_mlp_scale, r=out, alpha=0.0)

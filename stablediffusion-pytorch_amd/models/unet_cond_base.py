@@ -114,10 +114,10 @@ class Unet(nn.Module):
     def _leaf_forward(self, x, t, text, mask, klass):
         """unet_cond_base.py:131-183, leaf by leaf (sdmi.leaf.call)."""
         if self.image_cond:
-            im_cond = torch.nn.functional.interpolate(mask.float(), size=x.shape[-2:])
+            im_cond = LF.resize_nearest(mask.float(), x.shape[-2:])
             im_cond = LF.call(self.cond_conv_in, im_cond)
             assert im_cond.shape[-2:] == x.shape[-2:]
-            out = LF.call(self.conv_in_concat, torch.cat([x, im_cond], dim=1))
+            out = LF.call(self.conv_in_concat, LF.cat_channels([x, im_cond]))
         else:
             out = LF.call(self.conv_in, x)
         t_emb = LF.call(self.t_proj, LF.time_embedding(t, x.shape[0], self.t_emb_dim, x.device))

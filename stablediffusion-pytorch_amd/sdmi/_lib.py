@@ -106,6 +106,13 @@ SIGNATURES = {
     "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
     "sdmi_loss_flag": ([_P, _P, _I, _P], _I),
     "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _F, _P], _I),
+    "sdmi_adam_ema_bf16": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _F, _P, _P], _I),
+    "sdmi_cast_bf16": ([_P, _P, _L, _P], _I),
+    "sdmi_resize_nearest": ([_P, _I, _I, _I, _P, _I, _I, _P], _I),
+    "sdmi_chan_copy": ([_P, _I, _I, _P, _I, _I, _I, _I, _L, _P], _I),
+    "sdmi_modulate_fwd": ([_P, _P, _P, _P, _I, _F, _P, _I, _I, _I, _P], _I),
+    "sdmi_modulate_bwd": ([_P, _P, _P, _I, _F, _P, _P, _P, _I, _I, _I, _P], _I),
+    "sdmi_attn_map": ([_P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P], _I),
     "sdmi_ln_chunk_rows": ([_I], _I),
     "sdmi_ln_mod_fwd": ([_P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P, _P, _I, _I, _I, _F, _I, _P], _I),
     "sdmi_ln_mod_bwd": ([_P, _I, _P, _P, _P, _I, _P, _I, _P, _I, _P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P,

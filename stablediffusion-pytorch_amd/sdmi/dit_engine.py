@@ -84,7 +84,7 @@ def position_embedding(D, gh, gw):
 class DiTEngine:
     EPS = 1e-6  # nn.LayerNorm(..., eps=1E-6), transformer_layer.py:27,30; transformer.py:137
 
-    def __init__(self, cfg, params, grads=None, im_channels=4):
+    def __init__(self, cfg, params, grads=None, im_channels=4, shadow=None):
         self.cfg = cfg
         self.L = dit_layout(cfg, im_channels)
         L = self.L
@@ -101,6 +101,7 @@ class DiTEngine:
         # the chunk's parameters or packed weights (same protocol as the UNet engine)
         self._pending = {}
         self._key_chunk = {}
+        self.shadow = shadow  # (flat fp32 parameters, bf16 image): see PackPlan
         self.P = _WaitingParams(params, self)
         self.Gd = grads
         self.im_channels = im_channels
@@ -122,7 +123,7 @@ class DiTEngine:
     def _build_pack(self):
         P, L = self.P, self.L
         D, p = L["D"], L["p"]
-        pk = PackPlan(self.device)
+        pk = PackPlan(self.device, self.shadow)
 
         def lin(key, name=None, t=False):
             w = P[key]
@@ -188,10 +189,7 @@ class DiTEngine:
     _need = UNetEngine._need
     _need_all = UNetEngine._need_all
 
-    def refresh_weights(self):
-        if self.pack.stale():
-            self.pack.finalize()
-        self.pack.run()
+    refresh_weights = UNetEngine.refresh_weights
 
     def pos_table(self, gh, gw):
         key = (gh, gw)

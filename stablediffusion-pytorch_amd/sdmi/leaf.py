@@ -12,8 +12,10 @@ blocks compose their leaves exactly like the reference's forwards (models/blocks
 Per-op path: each leaf is one autograd Function over NCHW / row-major fp32 torch tensors (the interface a
 swapped layer expects); inside, activations are converted to NHWC bf16 for the MFMA implicit-GEMM / GroupNorm /
 attention kernels, results come back as fp32, and the backward runs the same kernels' data / weight gradients.
-Packed bf16 weights are cached per module and repacked when the parameter's version changes. Elementwise glue
-between leaves (residual adds, broadcasts, concatenation) is torch, as in the reference's block code."""
+Packed bf16 weights are cached per module and repacked when the parameter's version changes. The glue between
+leaves that is more than an add -- mask resize, channel concatenation, the DiT's adaLN modulation and gated residuals,
+need_weights attention maps -- runs on csrc/leafops.hip; plain residual adds stay torch, as in the reference's
+block code."""
 import weakref
 
 import torch
@@ -580,6 +582,125 @@ def quantize(embedding, x):
     'commitment_loss'}, indices (B, h, w))."""
     zq, cb, cm, idx = _Quantize.apply(x, embedding.weight)
     return zq, {"codebook_loss": cb, "commitment_loss": cm}, idx
+
+
+# ---- glue between leaves (csrc/leafops.hip): nearest resize, channel concatenation, adaLN modulation, attention map --
+def resize_nearest(x, size):
+    """F.interpolate(x, size) with the default mode 'nearest' (unet_cond_base.py:132, transformer.py:169) of a
+    (B, C, H, W) fp32 tensor. The mask condition is data: no gradient flows to it."""
+    if x.requires_grad:
+        raise NotImplementedError("HIP leaf resize_nearest: no gradient w.r.t. the resized tensor")
+    x = x.float().contiguous()
+    B, C, H, W = x.shape
+    OH, OW = int(size[0]), int(size[1])
+    out = torch.empty(B, C, OH, OW, dtype=torch.float32, device=x.device)
+    _lib.check(_lib.lib().sdmi_resize_nearest(x.data_ptr(), B * C, H, W, out.data_ptr(), OH, OW, K._stream()),
+               "sdmi_resize_nearest")
+    return out
+
+
+def _chan_copy(src, s0, dst, d0, C):
+    B, sC, dC = src.shape[0], src.shape[1], dst.shape[1]
+    P = src[0, 0].numel()
+    _lib.check(_lib.lib().sdmi_chan_copy(src.data_ptr(), sC, s0, dst.data_ptr(), dC, d0, B, C, P, K._stream()),
+               "sdmi_chan_copy")
+
+
+class _CatChannels(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *xs):
+        B, sp = xs[0].shape[0], tuple(xs[0].shape[2:])
+        cs = [x.shape[1] for x in xs]
+        out = torch.empty(B, sum(cs), *sp, dtype=torch.float32, device=xs[0].device)
+        c0 = 0
+        for x, c in zip(xs, cs):
+            _chan_copy(x, 0, out, c0, c)
+            c0 += c
+        ctx.cs = cs
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = dout.float().contiguous()
+        grads, c0 = [], 0
+        for c, need in zip(ctx.cs, ctx.needs_input_grad):
+            g = None
+            if need:
+                g = torch.empty(dout.shape[0], c, *dout.shape[2:], dtype=torch.float32, device=dout.device)
+                _chan_copy(dout, c0, g, 0, c)
+            grads.append(g)
+            c0 += c
+        return tuple(grads)
+
+
+def cat_channels(xs):
+    """torch.cat(xs, dim=1) of (B, C_i, *spatial) fp32 tensors (unet_cond_base.py:136, blocks.py:463-464,
+    transformer.py:170); its backward splits the gradient with the same kernel."""
+    xs = [x.float().contiguous() for x in xs]
+    if any(x.shape[0] != xs[0].shape[0] or x.shape[2:] != xs[0].shape[2:] for x in xs):
+        raise ValueError("cat_channels: batch and spatial sizes must match")
+    return _CatChannels.apply(*xs)
+
+
+class _Modulate(torch.autograd.Function):
+    """y = r + x * (alpha + s[:, None]) + t[:, None] over x (B, N, C); s, t (B, C) rows of stride ls."""
+
+    @staticmethod
+    def forward(ctx, x, s, t, r, alpha, ls):
+        B, N, C = x.shape
+        y = torch.empty_like(x)
+        _lib.check(_lib.lib().sdmi_modulate_fwd(x.data_ptr(), K._p(r), s.data_ptr(), K._p(t), ls, float(alpha),
+                                                y.data_ptr(), B, N, C, K._stream()), "sdmi_modulate_fwd")
+        ctx.save_for_backward(x, s)
+        ctx.alpha, ctx.ls, ctx.has_t, ctx.has_r = alpha, ls, t is not None, r is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, s = ctx.saved_tensors
+        dy = dy.float().contiguous()
+        B, N, C = x.shape
+        dev = dy.device
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        # ds / dt are written with the same row stride as s / t (ls): a (B, ls) buffer, returned as (B, C) views
+        ds = torch.zeros(B, ctx.ls, dtype=torch.float32, device=dev) if ctx.needs_input_grad[1] else None
+        dt = torch.zeros(B, ctx.ls, dtype=torch.float32, device=dev) if ctx.has_t and ctx.needs_input_grad[2] else None
+        _lib.check(_lib.lib().sdmi_modulate_bwd(x.data_ptr(), dy.data_ptr(), s.data_ptr(), ctx.ls, float(ctx.alpha),
+                                                K._p(dx), K._p(ds), K._p(dt), B, N, C, K._stream()),
+                   "sdmi_modulate_bwd")
+        dr = dy if ctx.has_r and ctx.needs_input_grad[3] else None
+        return (dx, ds[:, :C] if ds is not None else None, dt[:, :C] if dt is not None else None, dr, None, None)
+
+
+def modulate(x, s, t=None, r=None, alpha=1.0):
+    """(r +) x * (alpha + s.unsqueeze(1)) (+ t.unsqueeze(1)) for x (B, N, C) and per-(sample, channel) s, t (B, C):
+    the DiT's adaLN modulation (alpha 1, t = shift) and gated residual (alpha 0, r = the residual stream)."""
+    x = x.float().contiguous()
+    r = r.float().contiguous() if r is not None else None
+    B, N, C = x.shape
+
+    def rows(v):  # (B, C) with unit column stride: pass its row stride; else a compact copy
+        return v if v.dtype == torch.float32 and v.stride(1) == 1 else v.float().contiguous()
+    s = rows(s)
+    t = rows(t) if t is not None else None
+    if t is not None and t.stride(0) != s.stride(0):
+        s, t = s.contiguous(), t.contiguous()
+    if tuple(s.shape) != (B, C) or (t is not None and tuple(t.shape) != (B, C)):
+        raise ValueError("modulate: s / t must be (B, C)")
+    return _Modulate.apply(x, s, t, r, alpha, s.stride(0))
+
+
+def attention_map(q, k, heads, scaling, average=True):
+    """The attention weights of an MHA call with need_weights=True (multihead_attention.py:107-118):
+    softmax(q_h k_h^T * scaling) over the keys, averaged over heads -> (B, N, S), else (B, H, N, S). A diagnostic
+    output (the flash kernels never materialise it): returned without a gradient."""
+    q, k = q.detach().float().contiguous(), k.detach().float().contiguous()
+    B, N, E = q.shape
+    S = k.shape[1]
+    out = torch.empty((B, N, S) if average else (B, heads, N, S), dtype=torch.float32, device=q.device)
+    _lib.check(_lib.lib().sdmi_attn_map(q.data_ptr(), E, k.data_ptr(), E, B, heads, N, S, E // heads, float(scaling),
+                                        1 if average else 0, out.data_ptr(), K._stream()), "sdmi_attn_map")
+    return out
 
 
 # ---- dispatch -----------------------------------------------------------------------------------------------------

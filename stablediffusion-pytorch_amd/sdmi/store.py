@@ -89,7 +89,9 @@ class FlatStore:
             for s in shapes[k]:
                 n *= s
             self.offsets[k] = (off, n)
-            off += (n + 3) // 4 * 4  # 16-B aligned starts (vector epilogue loads of biases)
+            # 32-B aligned starts: 16-B vector loads of fp32 biases, and 16-B aligned rows of the trainer's bf16
+            # image of this buffer (weights read from it directly, PackPlan shadow)
+            off += (n + 7) // 8 * 8
         self.numel = off
         self.params = torch.zeros(off, dtype=torch.float32, device=device)
         self.grads = torch.zeros(off + grad_tail, dtype=torch.float32, device=device) if with_grads else None

@@ -83,12 +83,17 @@ def cross_list(L):
 class PackPlan:
     """bf16 GEMM-layout copies of the fp32 weights, refreshed by one batched pack launch."""
 
-    def __init__(self, device):
+    def __init__(self, device, shadow=None):
+        """shadow: (flat fp32 parameter buffer, its bf16 image) kept current by the trainer's optimizer
+        (sdmi_adam_ema_bf16): a view whose packed layout IS its source's flat layout (linears, GEMM-natural conv
+        weights, concatenations of consecutive flat runs) then aliases the bf16 image instead of being packed."""
         self.device = device
         self.items = []  # (name, src tensor, dims, shape of packed view)
         self.titems = []  # layouts derived from packed views by per-tap transposes (add_transpose)
         self.total = 0
         self.views = {}
+        self.shadow = shadow
+        self.alias = {}  # view name -> element offset of its first row in the bf16 image
 
     def add(self, name, src, O, I, Ipad, KH, KW, so, si, skh, skw, kh_off=0, kh_mul=1, kw_off=0, kw_mul=1,
             rows=None, into=None, row0=0, col0=0):
@@ -139,6 +144,22 @@ class PackPlan:
         self.n_declared = n
         self.finalize()
 
+    def _flat_elem(self, it):
+        """Element offset of item `it`'s source in the shadow's flat buffer when the item is a plain copy of
+        consecutive flat elements into consecutive packed elements (identity layout), else None."""
+        if self.shadow is None or it["dst_ld"] or it["Ipad"] != it["I"]:
+            return None
+        if (it["kh_off"], it["kh_mul"], it["kw_off"], it["kw_mul"]) != (0, 1, 0, 1) or it["si"] != 1:
+            return None
+        I, KH, KW = it["I"], it["KH"], it["KW"]
+        if (KW > 1 and it["skw"] != I) or (KH > 1 and it["skh"] != KW * I) or (it["O"] > 1 and it["so"] != KH * KW * I):
+            return None
+        flat = self.shadow[0]
+        nb = it["src"].data_ptr() - flat.data_ptr()
+        if nb < 0 or nb % 4 or nb // 4 + it["O"] * KH * KW * I > flat.numel():
+            return None
+        return nb // 4
+
     def finalize(self):
         self.buf = torch.zeros(max(self.total, 64), dtype=torch.bfloat16, device=self.device)
         chunk = _lib.lib().sdmi_pack_chunk()
@@ -154,6 +175,22 @@ class PackPlan:
                     break
                 name = nm
             return name
+
+        # views that alias the bf16 parameter image: every item writing the view is an identity copy, all at the
+        # same (flat element - packed element) distance, together covering the whole view, 16-B aligned rows
+        self.alias, by_view = {}, {}
+        for j, it in enumerate(self.items):
+            by_view.setdefault(view_of(it["dst_off"]), []).append(j)
+        for nm, js in by_view.items():
+            base, rows, width = self.views[nm]
+            fe = [self._flat_elem(self.items[j]) for j in js]
+            if any(e is None for e in fe):
+                continue
+            delta = {e - self.items[j]["dst_off"] for e, j in zip(fe, js)}
+            size = sum(self.items[j]["O"] * self.items[j]["KH"] * self.items[j]["KW"] * self.items[j]["I"] for j in js)
+            if len(delta) == 1 and size == rows * width and (base + delta.pop()) % 8 == 0 and width % 8 == 0:
+                self.alias[nm] = base + (fe[0] - self.items[js[0]]["dst_off"])
+        aliased = {j for nm in self.alias for j in by_view[nm]}
 
         for j, it in enumerate(self.items):  # a view is complete after the latest chunk of the items writing it
             nm = view_of(it["dst_off"])
@@ -179,6 +216,8 @@ class PackPlan:
         descs = (_lib.PackDesc * len(self.items))()
         bmaps = [[] for _ in range(self.nchunks)]
         for j, it in enumerate(self.items):
+            if j in aliased:
+                continue
             d = descs[j]
             d.src = it["src"].data_ptr()
             d.dst = self.buf.data_ptr() + 2 * it["dst_off"]
@@ -197,7 +236,10 @@ class PackPlan:
         for j, it in enumerate(self.titems):
             d = tdescs[j]
             sbase, _, swidth = self.views[it["src_view"]]
-            d.src = self.buf.data_ptr() + 2 * (sbase + it["src_col0"])
+            if it["src_view"] in self.alias:
+                d.src = self.shadow[1].data_ptr() + 2 * (self.alias[it["src_view"]] + it["src_col0"])
+            else:
+                d.src = self.buf.data_ptr() + 2 * (sbase + it["src_col0"])
             d.dst = self.buf.data_ptr() + 2 * it["dst_off"]
             d.O, d.I, d.taps = it["O"], it["I"], it["taps"]
             d.src_ld, d.src_tap, d.dst_ld, d.dst_tap = swidth, it["src_tap"], it["dst_ld"], it["dst_tap"]
@@ -213,9 +255,17 @@ class PackPlan:
 
     def view(self, name):
         off, rows, width = self.views[name]
+        if name in self.alias:
+            a = self.alias[name]
+            return self.shadow[1][a:a + rows * width].view(rows, width)
         return self.buf[off:off + rows * width].view(rows, width)
 
-    def run(self):
+    def run(self, cast=True):
+        """Refresh every packed view; cast=False when the bf16 image is already current (the optimizer wrote it)."""
+        if self.shadow is not None and cast:
+            flat, img = self.shadow
+            _lib.check(_lib.lib().sdmi_cast_bf16(flat.data_ptr(), img.data_ptr(), flat.numel(), K._stream()),
+                       "sdmi_cast_bf16")
         for c in range(self.nchunks):
             self.run_chunk(c)
 
@@ -301,9 +351,11 @@ def side_stream(device):
 
 
 class UNetEngine:
-    def __init__(self, cfg, params, grads=None, base=None, im_channels=4):
-        """params / grads: {state-dict key: fp32 CUDA tensor}; grads may be None (inference)."""
+    def __init__(self, cfg, params, grads=None, base=None, im_channels=4, shadow=None):
+        """params / grads: {state-dict key: fp32 CUDA tensor}; grads may be None (inference). shadow: (flat fp32
+        parameter buffer holding every params view, its bf16 image) -- see PackPlan."""
         self.cfg = cfg
+        self.shadow = shadow
         self.L = layout(cfg)
         self.base = base or ("cond" if cfg.get("condition_config") else "uncond")
         self.P = _WaitingParams(params, self)
@@ -356,7 +408,7 @@ class UNetEngine:
     # ------------------------------------------------------------------------------------------
     def _build_pack(self):
         P, L = self.P, self.L
-        pk = PackPlan(self.device)
+        pk = PackPlan(self.device, self.shadow)
         conv, lin = self._pk_conv, self._pk_lin
 
         cin_img = self.im_channels + (L["im_out"] if L["image"] else 0)
@@ -501,10 +553,10 @@ class UNetEngine:
         for c in sorted(self._pending):
             self._need(c)
 
-    def refresh_weights(self):
+    def refresh_weights(self, cast=True):
         if self.pack.stale():
             self.pack.finalize()
-        self.pack.run()
+        self.pack.run(cast=cast)
 
     # ------------------------------------------------------------------------------------------
     def _new(self, rows, C, dtype=torch.bfloat16):

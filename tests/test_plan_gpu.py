@@ -59,3 +59,37 @@ def test_plan_replay_matches_eager(model):
     assert torch.equal(eager.state, planned.state)
     if eager.ema is not None:
         assert torch.equal(eager.ema, planned.ema)
+
+
+@pytest.mark.parametrize("model", ["unet", "dit"])
+def test_bf16_image_matches_full_repack(model, monkeypatch):
+    """The optimizer writes a bf16 image of the flat parameters (sdmi_adam_ema_bf16) and the engine reads every
+    identity-layout weight from it (PackPlan aliases): three steps bit-identical to packing every weight from the fp32
+    masters (SDMI_SHADOW=0), and the aliases really are used."""
+    from sdmi.trainer import DDPMTrainer
+    if model == "dit":
+        sd = O.deterministic_state(DO.dit_param_shapes(SMALL_DIT), seed=3)
+        mk = lambda: DDPMTrainer(SMALL_DIT, sd, "cuda", base="dit", lr=1e-3, ema_decay=None)  # noqa: E731
+    else:
+        sd = O.deterministic_state(O.unet_param_shapes(SMALL_COND), seed=3)
+        mk = lambda: DDPMTrainer(SMALL_COND, sd, "cuda", lr=1e-3)  # noqa: E731
+    monkeypatch.setenv("SDMI_SHADOW", "1")
+    img = mk()
+    monkeypatch.setenv("SDMI_SHADOW", "0")
+    full = mk()  # the default
+    assert full.shadow is None and not full.engine.pack.alias
+    assert img.shadow is not None and len(img.engine.pack.alias) >= 8, sorted(img.engine.pack.alias)
+    for s in range(3):
+        ins = _inputs(s)
+        for tr in (img, full):
+            tr.step(*ins[:5], mask_keep=ins[5])
+    torch.cuda.synchronize()
+    img.sync_optimizer()
+    full.sync_optimizer()
+    torch.cuda.synchronize()
+    assert torch.equal(img.store.params, full.store.params)
+    assert torch.equal(img.m, full.m) and torch.equal(img.state, full.state)
+    # the image is the bf16 rounding of the masters
+    assert torch.equal(img.shadow, img.store.params.to(torch.bfloat16))
+    for name in img.engine.pack.alias:  # aliased views equal the packed copies of the fp32 masters
+        assert torch.equal(img.engine.pack.view(name), full.engine.pack.view(name)), name
