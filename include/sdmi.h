@@ -344,6 +344,12 @@ size_t sdmi_optim_workspace(void);
 int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws, int growth_interval,
                       int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
 int sdmi_loss_flag(const float* src, float* dst, int mode, sdmi_stream_t stream);
+/* The same norm in pieces (the trainer overlaps them with the backward): sdmi_sumsq_partials writes nblocks
+ * sum-of-squares partials of grads[0 .. n) (16-B aligned) into partial[0 .. nblocks); sdmi_clip_finalize reduces the
+ * first n partials (double accumulation, index order) and applies the clip / skip / scaler update above. */
+int sdmi_sumsq_partials(const float* grads, long long n, float* partial, int nblocks, sdmi_stream_t stream);
+int sdmi_clip_finalize(const float* partial, int n, float max_norm, float* state, int growth_interval,
+                       int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
 /* ema_alpha: the fp32 value of (1 - ema_decay) as the caller computes it (the reference passes alpha = 1 - 0.9999
  * from Python doubles, :376-378) */
 int sdmi_adam_ema(float* params, const float* grads, float* m, float* v, float* ema, long long n, const float* state,

@@ -40,7 +40,8 @@ def time_launch(L, d, ws, stream, iters=10, rounds=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "dit"))
+    ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "dit", "sample"))
+    ap.add_argument("--sample-batch", type=int, default=1)
     ap.add_argument("--out", default=os.path.join(REPO, "stablediffusion-pytorch_amd", "sdmi", "tuned_gemm.json"))
     args = ap.parse_args()
     from sdmi import _lib, kernels as K
@@ -70,6 +71,17 @@ def main():
     keep = torch.ones(B, device=dev)
     K.TUNED = {}  # tune from the built-in heuristic, not from a previous table
     step = lambda: tr.step(x0, noise, t, text, mask, mask_keep=keep)  # noqa: E731
+    if args.workload == "sample":  # the captured sampler's reverse step at --sample-batch (bench.py main_sample)
+        from scheduler.linear_noise_scheduler import LinearNoiseScheduler
+        from sdmi.sampling import DDPMSampleLoop
+        Bs = args.sample_batch
+        torch.manual_seed(1111)
+        model = mc.Unet(4, cfg).to(dev).eval()
+        xs, ts_, es, ms = bench.synthetic_batch(Bs, dev, 1111)
+        loop = DDPMSampleLoop(model, LinearNoiseScheduler(1000, 0.00085, 0.012), (Bs, 4, 32, 32),
+                              cond_input={"text": ts_, "image": ms}, seed=0)
+        xT = torch.randn(Bs, 4, 32, 32, device=dev)
+        step = lambda: loop.run(xT, steps=1, captured=False)  # noqa: E731
     for _ in range(2):
         step()
     K.GEMM_CAPTURE = []

@@ -175,8 +175,8 @@ using Ragged = std::true_type;
 // ONES (d % 16 == 8: the last output tile has free padded columns): column d of every valid V row is 1, so the
 // PV MFMA accumulates the softmax row sum into o[g][DT-1] (tile row 8: lane group 2, element 0) -- no per-score
 // VALU row-sum adds in the loop; the sum is of the bf16 P the MFMA consumes, i.e. exactly what O accumulated
-template <int DT, bool ONES>
-__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
+template <int DT, bool ONES, int OCC = 2>
+__global__ __launch_bounds__(NT, OCC) void attn_fwd_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -317,8 +317,8 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
 // =============================================================================================
 // backward: dK, dV (keys on lanes, 128 keys per workgroup, query tiles streamed)
 // =============================================================================================
-template <int DT>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
+template <int DT, int OCC = 2>
+__global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][Q|dO]
   __shared__ __attribute__((aligned(16))) float sLD[2][2][64];               // [buf][-lse|-delta]
@@ -426,8 +426,8 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
 // =============================================================================================
 // backward: dQ (queries on lanes, 128 queries per workgroup, key tiles streamed)
 // =============================================================================================
-template <int DT>
-__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
+template <int DT, int OCC = 2>
+__global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -793,6 +793,20 @@ __global__ __launch_bounds__(NT) void attn_delta_kernel(AttnArgs a) {
 constexpr int ATTN_CTR_SLOTS = 4, ATTN_CTR_SLOT = 1 << 16;
 __device__ unsigned g_attn_counters[ATTN_CTR_SLOTS * ATTN_CTR_SLOT];
 
+// workgroups per CU the kernel is register-budgeted for (__launch_bounds__ minimum): kind 0 forward, 1 dQ, 2 dK/dV;
+// head dims <= 32 only (DT <= 2: the larger tiles spill at 3 / 4). SDMI_ATTN_OCC_FWD / _DQ / _DKV override (A/B
+// runs); default 2 (the round-2 measured setting)
+int attn_occ(int kind, int d) {
+  static int v[3] = {-1, -1, -1};
+  if (v[kind] < 0) {
+    const char* names[3] = {"SDMI_ATTN_OCC_FWD", "SDMI_ATTN_OCC_DQ", "SDMI_ATTN_OCC_DKV"};
+    const char* e = getenv(names[kind]);
+    v[kind] = e ? atoi(e) : 2;
+  }
+  (void)d;
+  return v[kind];
+}
+
 int check_args(const AttnArgs& a) {
   if (a.B <= 0 || a.H <= 0 || a.N <= 0 || a.S <= 0 || a.d <= 0) return -1;
   if (a.d % 8 || a.d > 64) return -2;
@@ -817,9 +831,16 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
     ones_ok = e ? atoi(e) != 0 : 1;
   }
   const bool ones = ones_ok && d % 16 == 8;
-#define SDMI_ATTN_FWD(DT)                                                          \
-  if (ones) sdmi_rt::launch(attn_fwd_kernel<DT, true>, grid, dim3(NT), 0, s, a);  \
-  else sdmi_rt::launch(attn_fwd_kernel<DT, false>, grid, dim3(NT), 0, s, a);
+  const int occ = attn_occ(0, d);
+#define SDMI_ATTN_FWD_OCC(DT, O)                                                          \
+  if (ones) sdmi_rt::launch(attn_fwd_kernel<DT, true, O>, grid, dim3(NT), 0, s, a);      \
+  else sdmi_rt::launch(attn_fwd_kernel<DT, false, O>, grid, dim3(NT), 0, s, a);
+#define SDMI_ATTN_FWD(DT)                                                \
+  if constexpr (DT <= 2) {                                               \
+    if (occ >= 4) { SDMI_ATTN_FWD_OCC(DT, 4) }                           \
+    else if (occ == 3) { SDMI_ATTN_FWD_OCC(DT, 3) }                      \
+    else { SDMI_ATTN_FWD_OCC(DT, 2) }                                    \
+  } else { SDMI_ATTN_FWD_OCC(DT, 2) }
   switch ((d + 15) / 16) {
     case 1: SDMI_ATTN_FWD(1) break;
     case 2: SDMI_ATTN_FWD(2) break;
@@ -827,6 +848,7 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
     default: SDMI_ATTN_FWD(4) break;
   }
 #undef SDMI_ATTN_FWD
+#undef SDMI_ATTN_FWD_OCC
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -846,11 +868,19 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
   hipStream_t s = (hipStream_t)stream;
   // the dQ kernel also produces delta = rowsum(dO * O) (written to delta_ws) for the dK/dV kernel after it
   dim3 gk((S + ROWS - 1) / ROWS, B * H), gq((N + ROWS - 1) / ROWS, B * H);
+  const int oq = attn_occ(1, d), ok = attn_occ(2, d);
   switch ((d + 15) / 16) {
-#define SDMI_ATTN_BWD(DT)                                            \
-  case DT:                                                           \
-    sdmi_rt::launch(attn_bwd_dq_kernel<DT>, gq, dim3(NT), 0, s, a);  \
-    sdmi_rt::launch(attn_bwd_dkv_kernel<DT>, gk, dim3(NT), 0, s, a); \
+#define SDMI_ATTN_BWD(DT)                                                                                  \
+  case DT:                                                                                                 \
+    if constexpr (DT <= 2) {                                                                               \
+      if (oq >= 3) sdmi_rt::launch(attn_bwd_dq_kernel<DT, 3>, gq, dim3(NT), 0, s, a);                     \
+      else sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2>, gq, dim3(NT), 0, s, a);                              \
+      if (ok >= 3) sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 3>, gk, dim3(NT), 0, s, a);                    \
+      else sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2>, gk, dim3(NT), 0, s, a);                             \
+    } else {                                                                                               \
+      sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2>, gq, dim3(NT), 0, s, a);                                   \
+      sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2>, gk, dim3(NT), 0, s, a);                                  \
+    }                                                                                                      \
     break;
     SDMI_ATTN_BWD(1)
     SDMI_ATTN_BWD(2)

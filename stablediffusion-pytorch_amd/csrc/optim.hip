@@ -168,6 +168,25 @@ extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm
   return 0;
 }
 
+// Gradient norm in pieces: sum-of-squares partials of one range of the flat gradient buffer (nblocks partials into
+// partial[0 .. nblocks)), issued while the backward is still producing later ranges; sdmi_clip_finalize then reduces
+// every partial written (in index order, double accumulation) exactly as sdmi_clip_unscale's second kernel does.
+extern "C" int sdmi_sumsq_partials(const float* grads, long long n, float* partial, int nblocks, sdmi_stream_t stream) {
+  if (!grads || !partial || n < 0 || nblocks <= 0 || ((uintptr_t)grads & 15)) return -1;
+  sdmi_rt::launch(sumsq_kernel, dim3(nblocks), dim3(NT), 0, (hipStream_t)stream, grads, n, partial);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_clip_finalize(const float* partial, int n, float max_norm, float* state, int growth_interval,
+                                  int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream) {
+  if (!partial || !state || n <= 0) return -1;
+  sdmi_rt::launch(norm_finalize_kernel, dim3(1), dim3(NT), 0, (hipStream_t)stream, partial, n, max_norm, state,
+                  growth_interval, skip_if_loss_nonfinite, grad_div);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int sdmi_loss_flag(const float* src, float* dst, int mode, sdmi_stream_t stream) {
   if (!src || !dst || mode < 0 || mode > 1) return -1;
   sdmi_rt::launch(loss_flag_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, src, dst, mode);

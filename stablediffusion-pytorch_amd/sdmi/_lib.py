@@ -105,6 +105,8 @@ SIGNATURES = {
     "sdmi_optim_workspace": ([], _SZ),
     "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
     "sdmi_loss_flag": ([_P, _P, _I, _P], _I),
+    "sdmi_sumsq_partials": ([_P, _L, _P, _I, _P], _I),
+    "sdmi_clip_finalize": ([_P, _I, _F, _P, _I, _I, _F, _P], _I),
     "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _F, _P], _I),
     "sdmi_adam_ema_bf16": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _F, _P, _P], _I),
     "sdmi_cast_bf16": ([_P, _P, _L, _P], _I),

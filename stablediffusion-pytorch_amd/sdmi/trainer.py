@@ -34,6 +34,61 @@ def scheduler_tables(num_timesteps, beta_start, beta_end):
     return torch.sqrt(abar), torch.sqrt(1 - abar)
 
 
+class NormParts:
+    """clip_grad_norm_'s sum of squares in pieces overlapped with the backward (one GPU): as soon as the backward has
+    finalised a >= `chunk` slice of the flat gradient buffer (the same watermarks the data-parallel reducer uses), its
+    partial sums run on a stream of their own behind every gradient producer; the last slice and the finalisation run
+    on the compute stream, so the step boundary (backward end -> norm -> first optimizer chunk -> next forward) no
+    longer waits for a full pass over the 474 MB of gradients. Partials land in fixed slots and are reduced in slot
+    order: deterministic, eager and plan-replayed steps identical."""
+
+    MAX_PARTIALS = 8192
+
+    def __init__(self, grads, numel, producers=(), chunk_elems=16 << 20):
+        self.g, self.numel = grads, numel
+        self.chunk = chunk_elems
+        self.producers = list(producers)
+        self.stream = torch.cuda.Stream(device=grads.device)
+        self.partials = torch.zeros(self.MAX_PARTIALS, dtype=torch.float32, device=grads.device)
+        self.reset()
+
+    def reset(self):
+        self.launched = 0
+        self.used = 0
+
+    @staticmethod
+    def _blocks(n):
+        return max(16, min(1024, n // (256 * 4 * 16)))
+
+    def _launch(self, lo, hi, stream):
+        nb = self._blocks(hi - lo)
+        assert self.used + nb <= self.MAX_PARTIALS
+        _lib.check(_lib.lib().sdmi_sumsq_partials(self.g[lo:hi].data_ptr(), hi - lo, self.partials[self.used:].data_ptr(),
+                                                  nb, stream.cuda_stream), "sdmi_sumsq_partials")
+        self.used += nb
+
+    def ready(self, upto):
+        """Gradients at flat offsets < upto are final (called during the backward)."""
+        upto = min(upto, self.numel)
+        if upto - self.launched < self.chunk:
+            return
+        for st in [torch.cuda.current_stream(self.g.device)] + self.producers:
+            ev = torch.cuda.Event()
+            plan.record_event(ev, st)
+            plan.wait_event(self.stream, ev)
+        self._launch(self.launched, upto, self.stream)
+        self.launched = upto
+
+    def finish(self, max_norm, state, growth, skip_mode, grad_div):
+        """After the backward (side streams joined into the current stream): the rest, then clip / skip / scaler."""
+        cur = torch.cuda.current_stream(self.g.device)
+        if self.launched < self.numel:
+            self._launch(self.launched, self.numel, cur)
+        plan.wait_stream(cur, self.stream)
+        _lib.check(_lib.lib().sdmi_clip_finalize(self.partials.data_ptr(), self.used, max_norm, state.data_ptr(), growth,
+                                                 skip_mode, grad_div, K._stream()), "sdmi_clip_finalize")
+
+
 class DDPMTrainer:
     """base: "cond" / "uncond" (UNet, train_ddpm_cond_celebhq_multi_gpu.py:299-378, EMA 0.9999) or "dit"
     (Model_DiT_12L_train.py:300-375: same step, no EMA -- pass ema_decay=None -- and lr 1e-4)."""
@@ -91,6 +146,13 @@ class DDPMTrainer:
         self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes, wire=self.grad_wire)
                         if self.world > 1 or force_reducer else None)
         self.tail_events = None  # (after backward, after the all-reduce drain): set by measure_exchange_tail()
+        # one GPU: the gradient norm in pieces overlapped with the backward (SDMI_NORM_PARTS=0: one pass afterwards).
+        # With N > 1 the norm needs the all-reduced gradients, so it stays one pass after the exchange.
+        self.norm_parts = None
+        if (self.world == 1 and self.reducer is None and self.device.type == "cuda"
+                and os.environ.get("SDMI_NORM_PARTS", "1") != "0"):
+            self.norm_parts = NormParts(self.store.grads, self.store.numel,
+                                        getattr(self.engine, "sides", None) or [])
         if self.reducer is not None and getattr(self.engine, "side", None) is not None:
             self.reducer.producers.extend(getattr(self.engine, "sides", None) or [self.engine.side])
         self._progress = None
@@ -150,7 +212,10 @@ class DDPMTrainer:
                 upto = end
             else:
                 break
-        self.reducer.ready(upto)
+        if self.reducer is not None:
+            self.reducer.ready(upto)
+        if self.norm_parts is not None:
+            self.norm_parts.ready(upto)
 
     # ------------------------------------------------------------------------------------------
     def step(self, x0, noise, t, text=None, mask=None, mask_keep=None, klass=None):
@@ -193,6 +258,14 @@ class DDPMTrainer:
             self._tail_mark(0)
             self.reducer.finish()
             self._tail_mark(1)
+        elif self.norm_parts is not None:
+            self.norm_parts.reset()
+            if self.base == "dit":
+                eng.backward(ctx, dpred, on_progress=self._on_progress_dit)
+            else:
+                if self._progress is None:
+                    self._progress = self._watermarks(ctx["tape"])
+                eng.backward(ctx, dpred, on_progress=self._on_progress)
         else:
             eng.backward(ctx, dpred)
         ws = torch.empty(L.sdmi_optim_workspace() // 4, dtype=torch.float32, device=self.device)
@@ -204,9 +277,12 @@ class DDPMTrainer:
         if self.world > 1:
             _lib.check(L.sdmi_loss_flag(st.grads[st.numel:].data_ptr(), self.state[S_DPFLAG:].data_ptr(), 1,
                                         K._stream()), "sdmi_loss_flag")
-        _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(), ws.data_ptr(),
-                                       hp["growth"], 1 if self.world == 1 else 2, float(self.world), K._stream()),
-                   "sdmi_clip_unscale")
+        if self.norm_parts is not None:
+            self.norm_parts.finish(hp["clip"], self.state, hp["growth"], 1, 1.0)
+        else:
+            _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(),
+                                           ws.data_ptr(), hp["growth"], 1 if self.world == 1 else 2, float(self.world),
+                                           K._stream()), "sdmi_clip_unscale")
         ema_decay = hp["ema"] if hp["ema"] is not None else 0.0
         if self.opt_ranges is None:
             _lib.check(L.sdmi_adam_ema_bf16(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(),
@@ -261,7 +337,10 @@ class DDPMTrainer:
                     off, n = self.store.offsets[key]
                     marks[li] = max(marks.get(li, 0), off + n)
             self._dit_marks = marks
-        self.reducer.ready(self._dit_marks[i])
+        if self.reducer is not None:
+            self.reducer.ready(self._dit_marks[i])
+        if self.norm_parts is not None:
+            self.norm_parts.ready(self._dit_marks[i])
 
     _dit_marks = None
 

@@ -93,3 +93,36 @@ def test_bf16_image_matches_full_repack(model, monkeypatch):
     assert torch.equal(img.shadow, img.store.params.to(torch.bfloat16))
     for name in img.engine.pack.alias:  # aliased views equal the packed copies of the fp32 masters
         assert torch.equal(img.engine.pack.view(name), full.engine.pack.view(name)), name
+
+
+@pytest.mark.parametrize("model", ["unet", "dit"])
+def test_norm_in_pieces_matches_one_pass(model, monkeypatch):
+    """clip_grad_norm_'s sum of squares issued in pieces during the backward (sdmi.trainer.NormParts) gives the norm of
+    the one-pass sdmi_clip_unscale (SDMI_NORM_PARTS=0) to fp32 rounding, and the same steps."""
+    from sdmi.trainer import DDPMTrainer
+    if model == "dit":
+        sd = O.deterministic_state(DO.dit_param_shapes(SMALL_DIT), seed=4)
+        mk = lambda: DDPMTrainer(SMALL_DIT, sd, "cuda", base="dit", lr=1e-3, ema_decay=None)  # noqa: E731
+    else:
+        sd = O.deterministic_state(O.unet_param_shapes(SMALL_COND), seed=4)
+        mk = lambda: DDPMTrainer(SMALL_COND, sd, "cuda", lr=1e-3)  # noqa: E731
+    monkeypatch.setenv("SDMI_NORM_PARTS", "1")
+    parts = mk()
+    monkeypatch.setenv("SDMI_NORM_PARTS", "0")
+    one = mk()
+    assert parts.norm_parts is not None and one.norm_parts is None
+    parts.norm_parts.chunk = 1 << 16  # several pieces for the small model (the default is 64 MB)
+    for s in range(3):
+        ins = _inputs(s)
+        for tr in (parts, one):
+            tr.step(*ins[:5], mask_keep=ins[5])
+        torch.cuda.synchronize()
+        assert parts.norm_parts.used > parts.norm_parts._blocks(1 << 16)  # more than one piece
+        a, b = parts.state[0].item(), one.state[0].item()
+        assert abs(a - b) <= 1e-5 * b, (s, a, b)
+    parts.sync_optimizer()
+    one.sync_optimizer()
+    torch.cuda.synchronize()
+    assert torch.equal(parts.state[2:6], one.state[2:6])  # scale, growth tracker, step, skip flag
+    d = (parts.store.params - one.store.params).abs().max().item()
+    assert d <= 1e-6, d
