@@ -16,10 +16,11 @@ for r in 1 2; do
   echo "old$r $(ms gpurun_out/ab_old$r.log)"
   timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 --workload $W > gpurun_out/ab_new$r.log 2>&1 || { tail -5 gpurun_out/ab_new$r.log; exit 1; }
   echo "new$r $(ms gpurun_out/ab_new$r.log)"
-  if [ -n "$AB_ENV_NEW" ]; then
-    env $AB_ENV_NEW timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 --workload $W > gpurun_out/ab_env$r.log 2>&1 || { tail -5 gpurun_out/ab_env$r.log; exit 1; }
-    echo "new+$AB_ENV_NEW $r $(ms gpurun_out/ab_env$r.log)"
-  fi
+  for E in "$AB_ENV_NEW" "$AB_ENV_NEW2" "$AB_ENV_NEW3"; do
+    [ -n "$E" ] || continue
+    env $E timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 --workload $W > gpurun_out/ab_env$r.log 2>&1 || { tail -5 gpurun_out/ab_env$r.log; exit 1; }
+    echo "new+$E $r $(ms gpurun_out/ab_env$r.log)"
+  done
 done
 if [ -n "$AB_ATTN" ]; then
   timeout -k 10 300 python -u scripts/attn_bench.py > gpurun_out/attn_new.txt 2>&1 && cat gpurun_out/attn_new.txt
