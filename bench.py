@@ -391,17 +391,26 @@ def main_sample(args, wl, world, rank, device):
     B = args.sample_batch
     x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
     sched = LinearNoiseScheduler(1000, 0.00085, 0.012)
-    loop = DDPMSampleLoop(model, sched, (B, 4, 32, 32), cond_input={"text": text, "image": mask}, seed=rank)
+    cond = {"text": text, "image": mask}
     xT = torch.randn(B, 4, 32, 32, generator=torch.Generator().manual_seed(5 + rank)).to(device)
+    if args.sampler == "ddim":  # DDIMSampler.forward (scheduler :209-256): `--steps` (t, t_prev) pairs, eta 0
+        from scheduler.linear_noise_scheduler import DDIMSampler
+        from sdmi.sampling import DDIMSampleLoop
+        abar = DDIMSampler(model, (0.00085, 0.012), 1000).alpha_t_bar
+        loop = DDIMSampleLoop(model, abar, (B, 4, 32, 32), cond_input=cond, steps=args.steps, seed=rank)
+        run = lambda n, cap: loop.run(xT, captured=cap)  # noqa: E731  (always the whole `--steps` loop)
+    else:
+        loop = DDPMSampleLoop(model, sched, (B, 4, 32, 32), cond_input=cond, seed=rank)
+        run = lambda n, cap: loop.run(xT, steps=n, captured=cap)  # noqa: E731
     res = {}
     for mode in ("captured", "eager"):
         cap = mode == "captured"
-        loop.run(xT, steps=args.warmup + 1, captured=cap)
+        run(args.warmup + 1, cap)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        loop.run(xT, steps=args.steps, captured=cap)
+        run(args.steps, cap)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -412,14 +421,32 @@ def main_sample(args, wl, world, rank, device):
             el = e.item()
         res[mode] = args.steps / el
     sps = res["captured"]
-    result = {"metric": wl["metric"], "value": sps * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
+    # roofline of the step's GEMM launches (every implicit-GEMM conv and linear of the forward, HIP events on their
+    # stream, one eager reverse step): at B = 1 the grids are small and each launch is latency-bound
+    from sdmi import kernels as K
+    K.PROFILE = []
+    loop._refresh()
+    loop._step()  # one eager reverse step (model forward + the sampler's update kernel)
+    torch.cuda.synchronize()
+    prof, K.PROFILE = K.PROFILE, None
+    gfl = sum(p[1] for p in prof if p[0].startswith("gemm"))
+    gms = sum(p[2].elapsed_time(p[3]) for p in prof if p[0].startswith("gemm"))
+    ngemm = sum(1 for p in prof if p[0].startswith("gemm"))
+    roof = {"bound": "mfma", "kernel": "sdmi gemm (all implicit-GEMM conv / linear launches of one reverse step)",
+            "achieved": gfl / (gms * 1e-3) / 1e12 if gms else None, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
+            "frac": gfl / (gms * 1e-3) / PEAK_BF16 if gms else None, "traffic": None, "launches": ngemm,
+            "avg_launch_us": gms * 1e3 / max(1, ngemm), "flop_per_launch": gfl / max(1, ngemm),
+            "gemm_ms_per_step": gms}
+    result = {"metric": wl["metric"].replace("DDPM", "DDIM") if args.sampler == "ddim" else wl["metric"], "value": sps * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
               "warmup": args.warmup, "ms_per_step": 1000.0 / sps, "higher_is_better": True, "scaling": "weak",
               "vs_baseline": None, "dtype": "bf16", "data": "synthetic latents / text / masks, random-init weights",
-              "config": {"workload": "cond-UNet DDPM reverse step (model forward + sample_prev_timestep), captured",
+              "config": {"workload": f"cond-UNet {args.sampler.upper()} reverse step (model forward + "
+                                     f"{'DDIM update' if args.sampler == 'ddim' else 'sample_prev_timestep'}), captured",
+                         "sampler": args.sampler,
                          "model": "cond-UNet 118.5M", "samples_per_gpu": B, "latent": [4, 32, 32],
                          "parallelism": f"replicas{world}"},
               "eager_steps_per_s": res["eager"], "captured_speedup": sps / res["eager"],
-              "model_flops_utilization": wl["flop"] * B * sps / PEAK_BF16}
+              "model_flops_utilization": wl["flop"] * B * sps / PEAK_BF16, "roofline": roof}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -451,6 +478,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--sample-batch", type=int, default=1, help="samples per GPU of --workload sample (reference: 1)")
+    ap.add_argument("--sampler", default="ddpm", choices=("ddpm", "ddim"),
+                    help="--workload sample: DDPM (T steps of sample_prev_timestep) or DDIM (--steps pairs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="cond-unet", choices=sorted(WORKLOADS),
                     help="cond-unet (the headline metric, default), uncond-unet (celebhq.yaml), dit (DiT-12L training "

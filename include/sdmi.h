@@ -120,6 +120,17 @@ int sdmi_gemm_kernel_info(const sdmi_gemm_desc* d, int* variant, int* tile_n);
 int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* workspace_bytes);
 int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t workspace_bytes, sdmi_stream_t stream);
 
+/* Grouped launch: ngroups (<= SDMI_GEMM_GROUP_MAX) independent problems d[0..ngroups) that are identical in every
+ * descriptor field but the a / b / c / sum_out pointers (e.g. the same-shape weight gradients of one UNet block's
+ * attention projections), in ONE launch (and one split-K reducer launch): the grid's z dimension runs over
+ * (problem, split). No bias / resid / rowbias / aux / second A source / sum_out2 / gsum_out. The split count is the
+ * single problem's (tuned, via splits_hint, or heuristic) divided by ngroups; per problem the result is bitwise the
+ * single launch's at that split count. */
+#define SDMI_GEMM_GROUP_MAX 8
+int sdmi_gemm_grouped_plan(const sdmi_gemm_desc* d, int ngroups, int* splits, size_t* workspace_bytes);
+int sdmi_gemm_grouped(const sdmi_gemm_desc* d, int ngroups, void* workspace, size_t workspace_bytes,
+                      sdmi_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Fused multi-head attention (flash-style), bf16 in/out, fp32 softmax statistics.
  * Replaces the core of torch nn.MultiheadAttention as called at models/blocks.py:128 (self) and

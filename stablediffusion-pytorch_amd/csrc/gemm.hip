@@ -47,6 +47,15 @@ struct Args {
   // 1: row sums of A over k accumulated from the staged A chunks in VALU (bias gradient without the extra tile
   // column the synthesised-column path costs; used when no per-group sums are wanted)
   int rowsum;
+  // grouped launch (sdmi_gemm_grouped): ngroups > 1 independent problems of one shape; the grid's z runs over
+  // (problem, split) and problem p reads its operands from Ag[p] / Bg[p] (Ag[0] = A, Bg[0] = B)
+  int ngroups;
+  const bf16_t* Ag[SDMI_GEMM_GROUP_MAX];
+  const bf16_t* Bg[SDMI_GEMM_GROUP_MAX];
+  // the outputs of problem p (copies of EpiArgs::Cg / sum_g: indexed here, in the kernel-argument segment, so the
+  // epilogue's local EpiArgs copy is never indexed dynamically -- that would put it in scratch)
+  void* Cg[SDMI_GEMM_GROUP_MAX];
+  float* sum_g[SDMI_GEMM_GROUP_MAX];
 };
 
 __device__ __forceinline__ void pixel_coords(const Args& g, int m, int& b, int& oy, int& ox) {
@@ -103,7 +112,21 @@ struct EpiArgs {
   bf16_t* gsum;
   int n_gemm;  // columns the MFMA tiles produce (N, or N plus the synthesised reduction columns); with split-K the
                // slab row width N is n_gemm + 8 when the VALU row sums ride along in slab column n_x0 = n_gemm
+  // grouped launch: problem p stores to Cg[p] / sum_g[p], its split-K slabs start p * ws_gstride floats into ws and
+  // its arrival counters p * tiles after counters
+  void* Cg[SDMI_GEMM_GROUP_MAX];
+  float* sum_g[SDMI_GEMM_GROUP_MAX];
+  long long ws_gstride;
+  int ctr_gstride;
 };
+
+// the epilogue arguments of problem p of a grouped launch (C / sum read from the kernel-argument segment)
+__device__ __forceinline__ void group_epi(EpiArgs& e, void* C, float* sum, int p) {
+  e.C = C;
+  e.sum_out = sum;
+  e.ws += (long long)p * e.ws_gstride;
+  if (e.counters) e.counters += (long long)p * e.ctr_gstride;
+}
 
 __device__ __forceinline__ long long rb_row(const EpiArgs& g, int row) {
   long long r = g.pix_d.div((unsigned)row);
@@ -368,7 +391,7 @@ __device__ __forceinline__ TileId tile_id() {
 // Split-K without a second launch: every split of a tile publishes its slab and bumps the tile's
 // arrival counter; the split that arrives last sums the slabs in fixed z order (deterministic) and
 // applies the epilogue, then re-arms the counter for the next launch (graph replays included).
-template <int TBN = BN>
+template <int TBN = BN, int TBM = BM, int NTH = NT>
 __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0, int n0, int tile) {
   // Slabs were written with device-coherent (sc1) stores, so no L2 write-back fence is needed: wait
   // for this block's stores to complete, then count the arrival with a relaxed device-scope atomic.
@@ -387,9 +410,9 @@ __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
   const int zstride = (int)(e.split_stride * 4);
   if (e.n8) {
-    // 2048 chunks of 8 columns, 8 per thread; 4 splits (8 loads) in flight per thread
+    // TBM x TBN/8 chunks of 8 columns; 4 splits (8 loads) in flight per thread
 #pragma unroll 1
-    for (int ch = threadIdx.x; ch < BM * (TBN / 8); ch += NT) {
+    for (int ch = threadIdx.x; ch < TBM * (TBN / 8); ch += NTH) {
       const int rl = ch / (TBN / 8);
       const int row = m0 + rl, col = n0 + (ch - rl * (TBN / 8)) * 8;
       const bool xcol = e.n_x0 && col >= e.n_x0;
@@ -416,7 +439,7 @@ __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0
     return;
   }
 #pragma unroll 1
-  for (int idx = threadIdx.x; idx < BM * TBN; idx += NT) {
+  for (int idx = threadIdx.x; idx < TBM * TBN; idx += NTH) {
     const int row = m0 + idx / TBN, col = n0 + idx % TBN;
     if (row >= e.M || col >= e.N) continue;
     float acc = 0.f;
@@ -442,7 +465,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   const TileId tl = tile_id();
   const int m0 = tl.m0, n0 = tl.n0;
-  const int z = tl.z;
+  const int grp = g.ngroups > 1 ? tl.z / g.nsplit : 0;  // grouped launch: problem index, then the split within it
+  const int z = tl.z - grp * g.nsplit;
+  const bf16_t* const opA = grp ? g.Ag[grp] : g.A;
+  const bf16_t* const opB = grp ? g.Bg[grp] : g.B;
   const int nkt_total = (g.K + BK - 1) / BK;
   const int kt0 = z * g.ktiles_per_split;
   const int kt1 = min(nkt_total, kt0 + g.ktiles_per_split);
@@ -477,10 +503,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   uint4 ra[4], rb[4];
   // Buffer descriptors: out-of-range offsets return zeros in hardware, which is how padding taps,
   // ragged tiles and k >= K are zero-filled without a select on a pointer.
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)opA, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)opB, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsA2 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(g.A2 ? g.A2 : g.A), (short)0, 0x7fffffff, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.A2 ? g.A2 : opA), (short)0, 0x7fffffff, 0x00020000);
   constexpr int OOB = (int)0x80000000;
 #define BUF_LD(rs, off) __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128((rs), (off), 0, 0))
 
@@ -658,7 +684,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   // The epilogue arguments are read through a laundered pointer into the kernel-argument segment: the compiler
   // cannot hoist those scalar loads above this point, so ~50 EpiArgs fields are not held (and spilled) in SGPRs
   // across the main loop.
-  const EpiArgs ev = epi_args_late();
+  EpiArgs ev = epi_args_late();
+  if (grp) group_epi(ev, g.Cg[grp], g.sum_g[grp], grp);
   const EpiArgs* ep = &ev;
   if (rowsum) {  // combine the 16 k-row lanes of each 8-column chunk in LDS (workgroup-uniform branch)
     float* red = (float*)smem;  // [16][128]
@@ -824,16 +851,19 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   const int wm = (wave / NWN) * 64, wn = (wave % NWN) * WTN;
   const TileId tl = tile_id<TBN, TBM>();
   const int m0 = tl.m0, n0 = tl.n0;
-  const int z = tl.z;
+  const int grp = g.ngroups > 1 ? tl.z / g.nsplit : 0;  // grouped launch: problem index, then the split within it
+  const int z = tl.z - grp * g.nsplit;
+  const bf16_t* const opA = grp ? g.Ag[grp] : g.A;
+  const bf16_t* const opB = grp ? g.Bg[grp] : g.B;
   const int nkt_total = (g.K + KBK - 1) / KBK;
   const int kt0 = z * g.ktiles_per_split * (BK / KBK);
   const int kt1 = min(nkt_total, kt0 + g.ktiles_per_split * (BK / KBK));
   constexpr int OOB = (int)0x80000000;
 
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)opA, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)opB, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsA2 =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(g.A2 ? g.A2 : g.A), (short)0, 0x7fffffff, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.A2 ? g.A2 : opA), (short)0, 0x7fffffff, 0x00020000);
 
   // ---- per-lane, per-instruction coordinates, fixed over the K loop ----
   // instruction q = wave * PW + j writes 1 KiB at tile + q * 1024 (lane-linear):
@@ -1118,7 +1148,8 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
     }
   }
   __syncthreads();
-  const EpiArgs ev = epi_args_late();  // epilogue arguments loaded only from here on (see gemm_kernel)
+  EpiArgs ev = epi_args_late();  // epilogue arguments loaded only from here on (see gemm_kernel)
+  if (grp) group_epi(ev, g.Cg[grp], g.sum_g[grp], grp);
   const EpiArgs* ep = &ev;
   if (RED != 0 && red_tile) {
     // lane holds C[wm + 16i + 4(lane>>4) + q][r*16 + (lane & 15)]: column 0 = row sums, 8 + j = group j
@@ -1139,9 +1170,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
     }
   }
   gemm_epilogue<TBN, false, TBM, NJ, NTH>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
-  if constexpr (TBM == BM && NTH == NT) {
-    if (ep->raw && ep->counters) splitk_tail<TBN>(*ep, smem, m0, n0, tl.tile);
-  }
+  if (ep->raw && ep->counters) splitk_tail<TBN, TBM, NTH>(*ep, smem, m0, n0, tl.tile);
 }
 
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
@@ -1149,7 +1178,9 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
 // contiguous 2 KiB) and are merged in LDS in a fixed order, so the result is deterministic. SL > 1 spreads the
 // deep split-K of small weight gradients (a 128 x 128 dW = 2048 items) over enough workgroups to fill the chip.
 template <int SL>
-__global__ __launch_bounds__(256) void splitk_reduce_n8_kernel(const EpiArgs g) {
+__global__ __launch_bounds__(256) void splitk_reduce_n8_kernel(const EpiArgs g0) {
+  EpiArgs g = g0;  // grid.y = problem of a grouped launch
+  if (blockIdx.y) group_epi(g, g0.Cg[blockIdx.y], g0.sum_g[blockIdx.y], blockIdx.y);
   constexpr int IPB = 256 / SL;
   __shared__ float4 part[SL > 1 ? SL : 1][IPB][2];
   const float* ws = g.ws;
@@ -1201,7 +1232,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_n8_kernel(const EpiArgs g) 
 }
 
 // Sum split-K slabs and apply the epilogue, general N (one element per thread).
-__global__ void splitk_reduce_kernel(const EpiArgs g) {
+__global__ void splitk_reduce_kernel(const EpiArgs g0) {
+  EpiArgs g = g0;  // grid.y = problem of a grouped launch
+  if (blockIdx.y) group_epi(g, g0.Cg[blockIdx.y], g0.sum_g[blockIdx.y], blockIdx.y);
   const float* ws = g.ws;
   long long stride = (long long)gridDim.x * blockDim.x;
   long long total = (long long)g.M * g.N;
@@ -1213,10 +1246,10 @@ __global__ void splitk_reduce_kernel(const EpiArgs g) {
   }
 }
 
-hipError_t launch_reduce(const EpiArgs& red, hipStream_t s) {
+hipError_t launch_reduce(const EpiArgs& red, hipStream_t s, int G = 1) {
   if (!red.n8) {
     const long long total = (long long)red.M * red.N;
-    sdmi_rt::launch(splitk_reduce_kernel, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096)), dim3(256),
+    sdmi_rt::launch(splitk_reduce_kernel, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096), G), dim3(256),
                        0, s, red);
     return hipGetLastError();
   }
@@ -1224,13 +1257,14 @@ hipError_t launch_reduce(const EpiArgs& red, hipStream_t s) {
   int sl = 1;  // slab lanes: aim for >= 1024 workgroups
   while (sl < 32 && sl * 2 <= red.nsplit && items * sl / 256 < 1024) sl *= 2;
   const unsigned blocks = (unsigned)std::min<long long>((items * sl + 255) / 256, 8192);
+  const dim3 grid(blocks, G);  // y: problem of a grouped launch
   switch (sl) {
-    case 1: sdmi_rt::launch(splitk_reduce_n8_kernel<1>, dim3(blocks), dim3(256), 0, s, red); break;
-    case 2: sdmi_rt::launch(splitk_reduce_n8_kernel<2>, dim3(blocks), dim3(256), 0, s, red); break;
-    case 4: sdmi_rt::launch(splitk_reduce_n8_kernel<4>, dim3(blocks), dim3(256), 0, s, red); break;
-    case 8: sdmi_rt::launch(splitk_reduce_n8_kernel<8>, dim3(blocks), dim3(256), 0, s, red); break;
-    case 16: sdmi_rt::launch(splitk_reduce_n8_kernel<16>, dim3(blocks), dim3(256), 0, s, red); break;
-    default: sdmi_rt::launch(splitk_reduce_n8_kernel<32>, dim3(blocks), dim3(256), 0, s, red); break;
+    case 1: sdmi_rt::launch(splitk_reduce_n8_kernel<1>, grid, dim3(256), 0, s, red); break;
+    case 2: sdmi_rt::launch(splitk_reduce_n8_kernel<2>, grid, dim3(256), 0, s, red); break;
+    case 4: sdmi_rt::launch(splitk_reduce_n8_kernel<4>, grid, dim3(256), 0, s, red); break;
+    case 8: sdmi_rt::launch(splitk_reduce_n8_kernel<8>, grid, dim3(256), 0, s, red); break;
+    case 16: sdmi_rt::launch(splitk_reduce_n8_kernel<16>, grid, dim3(256), 0, s, red); break;
+    default: sdmi_rt::launch(splitk_reduce_n8_kernel<32>, grid, dim3(256), 0, s, red); break;
   }
   return hipGetLastError();
 }
@@ -1569,16 +1603,48 @@ extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) 
   return 0;
 }
 
-extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_bytes, sdmi_stream_t stream) {
+namespace {
+// descriptors that may share one grouped launch: identical in every field but the operand / output pointers
+bool same_problem_shape(const sdmi_gemm_desc* a, const sdmi_gemm_desc* b) {
+  sdmi_gemm_desc x = *a, y = *b;
+  x.a = y.a = nullptr;
+  x.b = y.b = nullptr;
+  x.c = y.c = nullptr;
+  x.sum_out = y.sum_out = nullptr;
+  return memcmp(&x, &y, sizeof(x)) == 0;
+}
+
+// split count of a launch carrying G problems: the single problem's (tuned / heuristic) count shared out over them
+int group_splits(const sdmi_gemm_desc* d, int G) {
+  const int s = plan_splits(d);
+  return G > 1 ? std::max(1, (s + G / 2) / G) : s;
+}
+
+int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, hipStream_t s) {
   Args a;
   EpiArgs e;
-  int rc = fill_args(d, a, e);
+  int rc = fill_args(&d[0], a, e);
   if (rc) return rc;
-  hipStream_t s = (hipStream_t)stream;
-  int splits = plan_splits(d);
+  if (G < 1 || G > SDMI_GEMM_GROUP_MAX) return -15;
+  if (G > 1) {
+    // grouped: plain / bias-summing GEMMs only (no second A source, no per-row / residual / auxiliary inputs)
+    if (d[0].a2 || d[0].resid || d[0].rowbias || d[0].aux || d[0].bias || d[0].bias2 || d[0].sum_out2 || d[0].gsum_out)
+      return -16;
+    for (int i = 1; i < G; ++i)
+      if (!same_problem_shape(&d[0], &d[i]) || (!d[i].sum_out) != (!d[0].sum_out)) return -17;
+  }
+  a.ngroups = G;
+  for (int i = 0; i < G; ++i) {
+    a.Ag[i] = (const bf16_t*)d[i].a;
+    a.Bg[i] = (const bf16_t*)d[i].b;
+    a.Cg[i] = e.Cg[i] = d[i].c;
+    a.sum_g[i] = e.sum_g[i] = d[i].sum_out;
+  }
+  int splits = group_splits(d, G);
   const int nt = n_total(d), ns = slab_n(d);
-  if (splits > 1 && (!workspace || ws_bytes < (size_t)splits * d->m * ns * sizeof(float))) splits = 1;
-  if ((long long)splits * d->m * ns * 4 >= (1LL << 31)) splits = 1;  // slab offsets are 32-bit
+  const long long slab = (long long)d->m * ns;  // floats per split slab of one problem
+  if (splits > 1 && (!workspace || ws_bytes < (size_t)G * splits * slab * sizeof(float))) splits = 1;
+  if ((long long)G * splits * slab * 4 >= (1LL << 31)) splits = 1;  // slab offsets are 32-bit
   int nkt = (d->k + BK - 1) / BK;
   a.ktiles_per_split = (nkt + splits - 1) / splits;
   splits = (nkt + a.ktiles_per_split - 1) / a.ktiles_per_split;
@@ -1586,16 +1652,17 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
   EpiArgs run = e;
   const int variant = pick_variant(d), tbn = pick_tbn(d, variant), tbm = tile_m(d, variant);
   const int ng = n_grid(d, variant);
-  dim3 grid((ng + tbn - 1) / tbn, (d->m + tbm - 1) / tbm, splits);
+  dim3 grid((ng + tbn - 1) / tbn, (d->m + tbm - 1) / tbm, splits * G);
   if (splits > 1) {
     run.raw = 1;
     run.ws = (const float*)workspace;
     run.nsplit = splits;
-    run.split_stride = (long long)d->m * ns;
+    run.split_stride = slab;
+    run.ws_gstride = (long long)splits * slab;
+    run.ctr_gstride = (int)(grid.x * grid.y);
     // the in-launch combine reduces whole tiles only: the VALU row-sum chunk (outside every tile) needs the reducer
-    // (and only the 128-row, 4-wave tiles carry it)
-    run.counters = (ns != nt || variant >= 4 || (variant != 0 && has_reductions(d)))
-                       ? nullptr : splitk_counters((long long)grid.x * grid.y, splits);
+    run.counters = (ns != nt || (variant != 0 && has_reductions(d)))
+                       ? nullptr : splitk_counters((long long)grid.x * grid.y * G, splits);
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
@@ -1612,10 +1679,37 @@ extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_byt
     EpiArgs red = e;
     red.raw = 0;
     red.nsplit = splits;
-    red.split_stride = (long long)d->m * ns;
+    red.split_stride = slab;
+    red.ws_gstride = (long long)splits * slab;
     red.ws = (const float*)workspace;
-    err = launch_reduce(red, s);
+    err = launch_reduce(red, s, G);
     if (err != hipSuccess) return (int)err;
   }
   return 0;
+}
+}  // namespace
+
+extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_bytes, sdmi_stream_t stream) {
+  if (!d) return -1;
+  return run_gemm(d, 1, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int sdmi_gemm_grouped_plan(const sdmi_gemm_desc* d, int ngroups, int* splits, size_t* ws) {
+  if (!d || ngroups < 1 || ngroups > SDMI_GEMM_GROUP_MAX) return -1;
+  Args a;
+  EpiArgs e;
+  int rc = fill_args(d, a, e);
+  if (rc) return rc;
+  for (int i = 1; i < ngroups; ++i)
+    if (!same_problem_shape(&d[0], &d[i])) return -17;
+  const int sp = group_splits(d, ngroups);
+  if (splits) *splits = sp;
+  if (ws) *ws = sp > 1 ? (size_t)ngroups * sp * d->m * slab_n(d) * sizeof(float) : 0;
+  return 0;
+}
+
+extern "C" int sdmi_gemm_grouped(const sdmi_gemm_desc* d, int ngroups, void* workspace, size_t ws_bytes,
+                                 sdmi_stream_t stream) {
+  if (!d) return -1;
+  return run_gemm(d, ngroups, workspace, ws_bytes, (hipStream_t)stream);
 }

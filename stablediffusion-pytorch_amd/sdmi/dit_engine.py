@@ -399,6 +399,28 @@ class DiTEngine:
         with torch.cuda.stream(side):
             yield
 
+    # SDMI_DIT_WG_GROUP = n: the projections' weight gradients of n consecutive layers go out as one launch per shape
+    # (1: every weight gradient its own launch, issued where it becomes computable)
+    _dit_group = max(1, int(os.environ.get("SDMI_DIT_WG_GROUP", "3")))
+    _pending_wg = {}
+
+    def _wgrad_linear(self, dy, x, gW, gb=None):
+        """dW = dy^T x (+ db) on a side stream; deferred and grouped by shape (UNetEngine._wgrad_linear)."""
+        if self._dit_group <= 1 or self.side is None:
+            with self._wg(dy, x):
+                K.linear_wgrad(dy, x, gW, bias_grad=gb)
+            return
+        self._keep.extend([dy, x])
+        key = (tuple(dy.shape), K.ld_of(dy), tuple(x.shape), K.ld_of(x), gb is not None, gW.stride(0))
+        self._pending_wg.setdefault(key, []).append((dy, x, gW, gb))
+
+    def _flush_wg(self):
+        pend, self._pending_wg = self._pending_wg, {}
+        for items in pend.values():
+            for j in range(0, len(items), 8):
+                with self._wg():
+                    K.linear_wgrad_grouped(items[j:j + 8])
+
     def _join(self):
         """The current stream waits for all weight-gradient work issued so far."""
         if self.side is None:
@@ -413,6 +435,7 @@ class DiTEngine:
         assert self.Gd is not None, "engine built without gradient buffers"
         self._need_all()  # the optimizer chunks read the gradient buffers the backward is about to overwrite
         self._wg_next = 0
+        self._pending_wg = {}
         L, P = self.L, self.P
         st = ctx["st"]
         B, H, W, N, M = st["B"], st["H"], st["W"], st["N"], st["M"]
@@ -444,12 +467,10 @@ class DiTEngine:
             c = st["layers"][i]
             q = f"transformer_layers.{i}."
             # MLP (transformer_layer.py:104-106)
-            with self._wg(dv2, c["h"]):
-                K.linear_wgrad(dv2, c["h"], self.g(q + "mlp_block.2.weight"), bias_grad=self.g(q + "mlp_block.2.bias"))
+            self._wgrad_linear(dv2, c["h"], self.g(q + "mlp_block.2.weight"), self.g(q + "mlp_block.2.bias"))
             dh = self._new(M, 4 * D)
             self._dgrad(dv2, q + "mlp_block.2.weight", dh, relu_of=c["h"])
-            with self._wg(dh, c["y2"]):
-                K.linear_wgrad(dh, c["y2"], self.g(q + "mlp_block.0.weight"), bias_grad=self.g(q + "mlp_block.0.bias"))
+            self._wgrad_linear(dh, c["y2"], self.g(q + "mlp_block.0.weight"), self.g(q + "mlp_block.0.bias"))
             dy2 = self._new(M, D)
             self._dgrad(dh, q + "mlp_block.0.weight", dy2)
             dv1 = self._new(M, D)
@@ -459,28 +480,22 @@ class DiTEngine:
                 self._ln_bwd(c["x2"], c["m2"], c["r2"], dy2, dxs, scale=mcol(mod, i, 4), dres=dxs,
                              psh=mcol(ws, i, 3), psc=mcol(ws, i, 4), dx16=dvc, N=N)
                 S = st["S"]
-                with self._wg(dvc, c["co"]):
-                    K.linear_wgrad(dvc, c["co"], self.g(q + "cross_attn_block.out_proj.weight"),
-                                   bias_grad=self.g(q + "cross_attn_block.out_proj.bias"))
+                self._wgrad_linear(dvc, c["co"], self.g(q + "cross_attn_block.out_proj.weight"),
+                                   self.g(q + "cross_attn_block.out_proj.bias"))
                 dco = self._new(M, D)
                 self._dgrad(dvc, q + "cross_attn_block.out_proj.weight", dco)
                 dcq, dckv = self._new(M, D), self._new(B * S, 2 * D)
                 K.attn_bwd(c["cq"], c["ckv"][:, :D], c["ckv"][:, D:], c["co"], dco, c["clse"], dcq, dckv[:, :D],
                            dckv[:, D:], B, Hh, N, S, D // Hh)
-                with self._wg(dcq, c["yc"]):
-                    K.linear_wgrad(dcq, c["yc"], self.g(q + "cross_attn_block.q_proj.weight"),
-                                   bias_grad=self.g(q + "cross_attn_block.q_proj.bias"))
-                with self._wg(dckv[:, :D], c["cp"]):
-                    K.linear_wgrad(dckv[:, :D], c["cp"], self.g(q + "cross_attn_block.k_proj.weight"),
-                                   bias_grad=self.g(q + "cross_attn_block.k_proj.bias"))
-                with self._wg(dckv[:, D:], c["cp"]):
-                    K.linear_wgrad(dckv[:, D:], c["cp"], self.g(q + "cross_attn_block.v_proj.weight"),
-                                   bias_grad=self.g(q + "cross_attn_block.v_proj.bias"))
+                self._wgrad_linear(dcq, c["yc"], self.g(q + "cross_attn_block.q_proj.weight"),
+                                   self.g(q + "cross_attn_block.q_proj.bias"))
+                self._wgrad_linear(dckv[:, :D], c["cp"], self.g(q + "cross_attn_block.k_proj.weight"),
+                                   self.g(q + "cross_attn_block.k_proj.bias"))
+                self._wgrad_linear(dckv[:, D:], c["cp"], self.g(q + "cross_attn_block.v_proj.weight"),
+                                   self.g(q + "cross_attn_block.v_proj.bias"))
                 dcp = self._new(B * S, D)
                 self._dgrad(dckv, q + "kv", dcp)
-                with self._wg(dcp, st["ctx"]):
-                    K.linear_wgrad(dcp, st["ctx"], self.g(q + "context_proj.weight"),
-                                   bias_grad=self.g(q + "context_proj.bias"))
+                self._wgrad_linear(dcp, st["ctx"], self.g(q + "context_proj.weight"), self.g(q + "context_proj.bias"))
                 dyc = self._new(M, D)
                 self._dgrad(dcq, q + "cross_attn_block.q_proj.weight", dyc)
                 self._ln_bwd(c["xc"], c["mc"], c["rc"], dyc, dxs, dres=dxs, gate=mcol(mod, i, 2), v=c["v1"], dv=dv1,
@@ -489,18 +504,16 @@ class DiTEngine:
                 self._ln_bwd(c["x2"], c["m2"], c["r2"], dy2, dxs, scale=mcol(mod, i, 4), dres=dxs, psh=mcol(ws, i, 3),
                              psc=mcol(ws, i, 4), gate=mcol(mod, i, 2), v=c["v1"], dv=dv1, pg=mcol(ws, i, 2), N=N)
             # self attention (attention.py:33-78)
-            with self._wg(dv1, c["o"]):
-                K.linear_wgrad(dv1, c["o"], self.g(q + "attn_block.output_proj.0.weight"),
-                               bias_grad=self.g(q + "attn_block.output_proj.0.bias"))
+            self._wgrad_linear(dv1, c["o"], self.g(q + "attn_block.output_proj.0.weight"),
+                               self.g(q + "attn_block.output_proj.0.bias"))
             do = self._new(M, A)
             self._dgrad(dv1, q + "attn_block.output_proj.0.weight", do)
             qkv = c["qkv"]
             dqkv = self._new(M, 3 * A)
             K.attn_bwd(qkv[:, :A], qkv[:, A:2 * A], qkv[:, 2 * A:], c["o"], do, c["lse"], dqkv[:, :A],
                        dqkv[:, A:2 * A], dqkv[:, 2 * A:], B, Hh, N, N, hd)
-            with self._wg(dqkv, c["y1"]):
-                K.linear_wgrad(dqkv, c["y1"], self.g(q + "attn_block.qkv_proj.weight"),
-                               bias_grad=self.g(q + "attn_block.qkv_proj.bias"))
+            self._wgrad_linear(dqkv, c["y1"], self.g(q + "attn_block.qkv_proj.weight"),
+                               self.g(q + "attn_block.qkv_proj.bias"))
             dy1 = self._new(M, D)
             self._dgrad(dqkv, q + "attn_block.qkv_proj.weight", dy1)
             prev = st["layers"][i - 1] if i > 0 else None
@@ -510,8 +523,13 @@ class DiTEngine:
                          psc=mcol(ws, i, 1), gate=mcol(mod, i - 1, 5) if prev else None,
                          v=prev["v2"] if prev else None, dv=dv2, pg=mcol(ws, i - 1, 5) if prev else None, dx16=dtok,
                          N=N)
-            if on_progress is not None:
+            # grouped weight gradients: issued every SDMI_DIT_WG_GROUP layers (same-shape projections of those
+            # layers in one launch each); the layers are reported final only once their gradients are issued
+            if self._pending_wg and ((L["n_layers"] - i) % self._dit_group == 0 or i == 0):
+                self._flush_wg()
+            if on_progress is not None and not self._pending_wg:
                 on_progress(i)
+        self._flush_wg()
         # ---- adaLN tables of every layer: one reduction, one weight-gradient GEMM ----
         dmod = self._new(B, L["mod_w"])
         _lib.check(_lib.lib().sdmi_mod_finalize(ws.data_ptr(), B, chunks, L["mod_w"], L["mod_w"], dmod.data_ptr(),

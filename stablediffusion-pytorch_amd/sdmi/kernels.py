@@ -84,6 +84,10 @@ WG_CAP = 0
 DIAG_SKIP = set(filter(None, os.environ.get("SDMI_DIAG_SKIP", "").split(",")))
 
 
+# running total of the GEMM FLOPs issued (the UNet engine balances its weight-gradient side streams by it)
+FLOPS_ISSUED = 0.0
+
+
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
          rb_ld=0, rb_div=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0,
          a2=None, lda2=0, k_split=0, bias2=None, rb_mod=0, aux=None, ld_aux=0, sum_out=None, sum_out2=None,
@@ -92,6 +96,8 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
     offsets already applied by slicing); see include/sdmi.h for the operand modes."""
     if "wg" in DIAG_SKIP and PHASE == "wg":
         return c
+    global FLOPS_ISSUED
+    FLOPS_ISSUED += 2.0 * m * n * k
     L = _lib.lib()
     d = GemmDesc()
     d.m, d.n, d.k = m, n, k
@@ -276,6 +282,61 @@ def linear_wgrad(dy, x, out, *, bias_grad=None, bias_grad2=None, group_sums=None
     K = x.shape[1]
     return gemm(N, K, M, dy, _lib.A_COLMAJOR, ld_of(dy), x, _lib.B_KN, ld_of(x), out, out.stride(0),
                 sum_out=bias_grad, sum_out2=bias_grad2, gsum=group_sums, sum_group=group, m_store=m_store)
+
+
+def linear_wgrad_grouped(items):
+    """linear_wgrad of several same-shape problems in ONE launch (sdmi_gemm_grouped): items = [(dy, x, out,
+    bias_grad or None)], all dy / x of one shape and row stride, all bias_grad present or all None. The split count is
+    the single problem's tuned one shared out over the group."""
+    if "wg" in DIAG_SKIP and PHASE == "wg":
+        return
+    global FLOPS_ISSUED
+    G = len(items)
+    if G == 1:
+        dy, x, out, bg = items[0]
+        linear_wgrad(dy, x, out, bias_grad=bg)
+        return
+    L = _lib.lib()
+    descs = (GemmDesc * G)()
+    M, N = items[0][0].shape
+    K = items[0][1].shape[1]
+    FLOPS_ISSUED += 2.0 * M * N * K * G
+    for i, (dy, x, out, bg) in enumerate(items):
+        d = descs[i]
+        d.m, d.n, d.k = N, K, M
+        d.a_mode, d.b_mode = _lib.A_COLMAJOR, _lib.B_KN
+        d.a, d.lda = dy.data_ptr(), ld_of(dy)
+        d.b, d.ldb = x.data_ptr(), ld_of(x)
+        d.c, d.ldc, d.c_f32 = out.data_ptr(), out.stride(0), 1
+        d.alpha = 1.0
+        d.sum_out = _p(bg)
+        d.tile_n_hint = 0 if (not PHASE or PHASE in TILE192_PHASES) else 128
+    tuned = _tuned()
+    if tuned:
+        e = tuned.get(gemm_key(descs[0]), 0)
+        for i in range(G):
+            if isinstance(e, list):
+                descs[i].splits_hint, descs[i].variant_hint = e[0], e[1]
+            else:
+                descs[i].splits_hint = e
+    splits = ctypes.c_int(1)
+    ws_bytes = ctypes.c_size_t(0)
+    check(L.sdmi_gemm_grouped_plan(descs, G, ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_grouped_plan")
+    ws = torch.empty(ws_bytes.value // 4, dtype=torch.float32, device=items[0][2].device) if ws_bytes.value else None
+    if GEMM_LOG is not None:
+        var, tn = ctypes.c_int(0), ctypes.c_int(0)
+        check(L.sdmi_gemm_kernel_info(ctypes.byref(descs[0]), ctypes.byref(var), ctypes.byref(tn)), "kernel_info")
+        GEMM_LOG.append(dict(m=N, n=K, k=M, a=_lib.A_COLMAJOR, b=_lib.B_KN, splits=splits.value, tile_n=tn.value,
+                             variant=var.value, phase=PHASE, conv=False, flops=2.0 * M * N * K * G, groups=G))
+    info = ""
+    if PROFILE is not None:
+        var, tn = ctypes.c_int(0), ctypes.c_int(0)
+        check(L.sdmi_gemm_kernel_info(ctypes.byref(descs[0]), ctypes.byref(var), ctypes.byref(tn)), "kernel_info")
+        info = f" variant={var.value} tile_n={tn.value}"
+    with _Prof(f"gemm_a{_lib.A_COLMAJOR}b{_lib.B_KN}", 2.0 * M * N * K * G,
+               f"M={N} N={K} K={M} splits={splits.value} groups={G}{info}"):
+        check(L.sdmi_gemm_grouped(descs, G, ws.data_ptr() if ws is not None else None, ws_bytes.value, _stream()),
+              "sdmi_gemm_grouped")
 
 
 def gn_stats(x, B, P, C, G, gamma, beta, eps=1e-5):

@@ -856,7 +856,7 @@ class UNetEngine:
             K.conv_wgrad(dy, ldy, c["h2"], B, h, w, cout, cout, cout, 3, 3, 1, 1, self.g(b + ".2.weight"), h, w,
                          perm=self.wperm(b + ".2.weight"), bias_grad=self.g(b + ".2.bias"),
                          bias_grad2=self.g(rc + ".bias"))
-            K.linear_wgrad(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
+        self._wgrad_linear(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
         dh2 = self._new(B * Pn, cout)
         K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout)
         dx, fresh = grads.get(c["xn"])
@@ -924,9 +924,8 @@ class UNetEngine:
         C, B, N, mk, nk = c["C"], c["B"], c["N"], c["mk"], c["nk"]
         d = C // Hh
         dy, _ = grads.get(c["yn"])
-        with self._wg(dy):
-            K.linear_wgrad(dy, c["o"], self.g(mk + ".out_proj.weight"), bias_grad=self.g(mk + ".out_proj.bias"))
-        dy_read = self.wg_event if self.side is not None else None
+        self._wgrad_linear(dy, c["o"], self.g(mk + ".out_proj.weight"), self.g(mk + ".out_proj.bias"))
+        dy_read = self.wg_event if (self.side is not None and not self._grouping()) else None
         do = self._new(B * N, C)
         self._dgrad(dy, mk + ".out_proj", do)
         Win = self.W(mk + ".in_proj_weight#f")
@@ -939,8 +938,7 @@ class UNetEngine:
             dqkv = self._new(B * N, 3 * C)
             K.attn_bwd(qkv[:, :C], qkv[:, C:2 * C], qkv[:, 2 * C:], c["o"], do, c["lse"], dqkv[:, :C],
                        dqkv[:, C:2 * C], dqkv[:, 2 * C:], B, Hh, N, N, d)
-            with self._wg(dqkv):
-                K.linear_wgrad(dqkv, c["a"], gW, bias_grad=gb)
+            self._wgrad_linear(dqkv, c["a"], gW, gb)
             if WinT is not None:
                 K.linear_dgrad_t(dqkv, WinT, da)
             else:
@@ -956,9 +954,9 @@ class UNetEngine:
             # layer at the end of the backward, _bwd_time)
             off = self.ctx_off[(c["p"], c["l"])]
             dcp = self.dcp_all[:, off:off + C]
-            with self._wg(dq, dkv):
-                K.linear_wgrad(dq, c["a"], gW[:C], bias_grad=gb[:C])
-                K.linear_wgrad(dkv, c["cp"], gW[C:], bias_grad=gb[C:])
+            self._wgrad_linear(dq, c["a"], gW[:C], gb[:C])
+            self._wgrad_linear(dkv, c["cp"], gW[C:], gb[C:])
+            with self._wg(dkv):
                 if WinT is not None:
                     K.linear_dgrad_t(dkv, WinT[:, C:], dcp)
                 else:
@@ -969,8 +967,9 @@ class UNetEngine:
                 K.linear_dgrad(dq, Win[:C], da)
         # x receives dy (residual) + GroupNorm-branch gradient
         key, off, _ = grads.groups[c["xn"]]
-        if self._dy_alias and not grads.init.get(c["xn"], False) and dy.is_contiguous() and K.ld_of(dy) == C and \
-                grads.shapes.get(key, (0, 0))[1] == C:
+        # (no alias while weight gradients are grouped: the deferred out_proj gradient still has to read dy)
+        if self._dy_alias and not self._grouping() and not grads.init.get(c["xn"], False) and dy.is_contiguous() and \
+                K.ld_of(dy) == C and grads.shapes.get(key, (0, 0))[1] == C:
             grads.alias(c["xn"], dy)
             dx, addend = dy, dy
             if dy_read is not None:  # the GroupNorm backward below rewrites dy in place
@@ -1129,16 +1128,56 @@ class UNetEngine:
                 K.PHASE = prev
             return
         self._keep.extend(keep)
-        side = self.sides[self._wg_next % len(self.sides)]
+        if self._wg_balance:  # the side stream with the fewest weight-gradient FLOPs issued so far this backward
+            si = min(range(len(self.sides)), key=lambda j: (self._wg_flops[j], j))
+        else:  # round-robin
+            si = self._wg_next % len(self.sides)
+        side = self.sides[si]
         self._wg_next += 1
         plan.wait_stream(side, torch.cuda.current_stream(self.device))
+        f0 = K.FLOPS_ISSUED
         try:
             with torch.cuda.stream(side):
                 yield
         finally:
             K.PHASE = prev
+        self._wg_flops[si] += K.FLOPS_ISSUED - f0
         self.wg_event = torch.cuda.Event()
         plan.record_event(self.wg_event, side)
+
+    # SDMI_WG_GROUP=0: every linear weight gradient its own launch, issued where it becomes computable
+    _group_wg = os.environ.get("SDMI_WG_GROUP", "1") != "0"
+    # SDMI_WG_BALANCE=1: a weight-gradient block goes to the side stream with the fewest FLOPs issued so far (else
+    # round-robin)
+    _wg_balance = os.environ.get("SDMI_WG_BALANCE", "0") == "1"
+    _wg_flops = [0.0] * 8
+
+    def _grouping(self):
+        return self._group_wg and self.side is not None
+
+    def _wgrad_linear(self, dy, x, gW, gb=None):
+        """A linear / 1x1-conv weight gradient (dW = dy^T x, db = column sums of dy) on the side stream. Grouped
+        (default): deferred to the end of its block's backward (tape label) and issued there together with the
+        block's other same-shape ones as ONE launch (K.linear_wgrad_grouped: one grid, one split-K reducer) -- e.g. a
+        32^2 down block's self-attention out_proj, cross-attention q_proj and out_proj of both layers, six
+        [384 x 384] x 32768 launches (and six reducers) before."""
+        if not self._grouping():
+            with self._wg(dy, x):
+                K.linear_wgrad(dy, x, gW, bias_grad=gb)
+            return
+        self._keep.extend([dy, x])
+        key = (tuple(dy.shape), K.ld_of(dy), tuple(x.shape), K.ld_of(x), gb is not None, gW.stride(0))
+        self._pending_wg.setdefault(key, []).append((dy, x, gW, gb))
+
+    def _flush_wg(self):
+        """Issue the deferred weight gradients (groups of at most SDMI_GEMM_GROUP_MAX = 8)."""
+        pend, self._pending_wg = self._pending_wg, {}
+        for items in pend.values():
+            for i in range(0, len(items), 8):
+                with self._wg():
+                    K.linear_wgrad_grouped(items[i:i + 8])
+
+    _pending_wg = {}
 
     def _join(self):
         """The current stream waits for all weight-gradient work issued so far."""
@@ -1167,14 +1206,19 @@ class UNetEngine:
         self._need_all()  # the optimizer chunks read the gradient buffers the backward is about to overwrite
         self._wg_next = 0  # same side-stream assignment every step
         K.PHASE = "bwd"
+        self._pending_wg = {}
+        self._wg_flops = [0.0] * max(1, len(self.sides))
         for k in range(len(tape) - 1, -1, -1):
             fn, c = tape[k]
             # SDMI_WG_CAP_EARLY = n: weight gradients of every block but the tail ones (the first down level, the
             # input / time-embedding ends) split at most n ways (kernels.WG_CAP)
             K.WG_CAP = 0 if c.get("label") in self._tail_labels else self._wg_cap_early
             fn(c, grads)
+            if self._pending_wg and (k == 0 or tape[k - 1][1].get("label") != c.get("label")):
+                self._flush_wg()  # the block's grouped weight gradients, before its gradients are reported final
             if on_progress is not None:
                 on_progress(tape, k)
+        self._flush_wg()
         self._join()
         self._keep = []
         self.dpred = None

@@ -28,6 +28,8 @@ S_NORM, S_COEF, S_SCALE, S_GROWTH, S_STEP, S_SKIP, S_LOSS = range(7)
 class VQVAETrainEngine(UNetEngine):
     """Forward + backward of models/vqvae.py VQVAE. Parameters / gradients: {state-dict key: fp32 CUDA tensor}."""
 
+    _group_wg = False  # its own backward loop issues every weight gradient in place (no per-block grouping)
+
     def __init__(self, cfg, params, grads=None, im_channels=3):
         import os
         self.cfg = cfg

@@ -201,3 +201,66 @@ def test_conv_wgrad_with_fused_bias_and_group_sums():
     close(dw, ref, 2e-3)
     close(bg, dyn.sum((0, 2, 3)), 1e-5)
     close(gs, dyn.sum((2, 3)), 1e-2)
+
+
+@pytest.mark.parametrize("G,M,N,K,bias", [(3, 4096, 384, 384, True), (6, 512, 512, 512, True), (2, 2464, 768, 384, False),
+                                         (8, 1024, 128, 128, True)])
+def test_grouped_weight_gradients_match_single_launches(G, M, N, K, bias):
+    """sdmi_gemm_grouped: G same-shape weight gradients in one launch give, per problem, exactly the single launch's
+    result at the same split count (weights and bias sums bitwise), with and without split-K."""
+    from sdmi import _lib, kernels as K_
+    import ctypes
+    saved, K_.TUNED = K_.TUNED, {}  # built-in heuristics on both sides (no per-shape table hints)
+    try:
+        _grouped_check(G, M, N, K, bias, _lib, K_, ctypes)
+    finally:
+        K_.TUNED = saved
+
+
+def _grouped_check(G, M, N, K, bias, _lib, K_, ctypes):
+    g = torch.Generator().manual_seed(11)
+    items, ref = [], []
+    for i in range(G):
+        dy = (torch.randn(M, N, generator=g) * 0.5).to(torch.bfloat16).cuda()
+        x = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+        out = torch.full((N, K), float("nan"), device="cuda")
+        bg = torch.full((N,), float("nan"), device="cuda") if bias else None
+        items.append((dy, x, out, bg))
+    K_.linear_wgrad_grouped(items)
+    # the same split count the grouped launch used, one problem at a time
+    d = K_.GemmDesc()
+    d.m, d.n, d.k = N, K, M
+    d.a_mode, d.b_mode = _lib.A_COLMAJOR, _lib.B_KN
+    d.a, d.lda, d.b, d.ldb = items[0][0].data_ptr(), N, items[0][1].data_ptr(), K
+    d.c, d.ldc, d.c_f32, d.alpha = items[0][2].data_ptr(), K, 1, 1.0
+    d.sum_out = K_._p(items[0][3])
+    descs = (K_.GemmDesc * G)(*([d] * G))
+    sp = ctypes.c_int(0)
+    wsb = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().sdmi_gemm_grouped_plan(descs, G, ctypes.byref(sp), ctypes.byref(wsb)), "plan")
+    torch.cuda.synchronize()
+    for dy, x, out, bg in items:
+        o1 = torch.empty_like(out)
+        b1 = torch.empty_like(bg) if bias else None
+        K_.gemm(N, K, M, dy, _lib.A_COLMAJOR, N, x, _lib.B_KN, K, o1, K, sum_out=b1)  # heuristic / tuned split
+        fp = (dy.float().t() @ x.float())
+        assert (out - fp).abs().max().item() <= 2e-3 * fp.abs().max().item() + 1e-3
+        if bias:
+            assert (bg - dy.float().sum(0)).abs().max().item() <= 1e-2 * (1 + dy.float().sum(0).abs().max().item())
+    # bitwise vs single launches forced to the grouped split count
+    for dy, x, out, bg in items:
+        o1 = torch.empty_like(out)
+        b1 = torch.empty_like(bg) if bias else None
+        dd = K_.GemmDesc.from_buffer_copy(d)
+        dd.a, dd.b, dd.c, dd.sum_out = dy.data_ptr(), x.data_ptr(), o1.data_ptr(), K_._p(b1)
+        dd.splits_hint = sp.value
+        s1 = ctypes.c_int(0)
+        w1 = ctypes.c_size_t(0)
+        _lib.check(_lib.lib().sdmi_gemm_plan(ctypes.byref(dd), ctypes.byref(s1), ctypes.byref(w1)), "plan1")
+        assert s1.value == sp.value
+        ws = torch.empty(max(1, w1.value // 4), device="cuda")
+        _lib.check(_lib.lib().sdmi_gemm(ctypes.byref(dd), ws.data_ptr(), w1.value, K_._stream()), "gemm1")
+        torch.cuda.synchronize()
+        assert torch.equal(o1, out)
+        if bias:
+            assert torch.equal(b1, bg)
