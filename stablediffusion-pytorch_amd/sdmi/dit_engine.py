@@ -400,8 +400,9 @@ class DiTEngine:
             yield
 
     # SDMI_DIT_WG_GROUP = n: the projections' weight gradients of n consecutive layers go out as one launch per shape
-    # (1: every weight gradient its own launch, issued where it becomes computable)
-    _dit_group = max(1, int(os.environ.get("SDMI_DIT_WG_GROUP", "3")))
+    # (1: every weight gradient its own launch, issued where it becomes computable). Measured DiT-12L step, same box:
+    # 1 -> 4.44 / 4.43 ms, 3 -> 4.11 / 4.13, 6 -> 4.04 / 4.05
+    _dit_group = max(1, int(os.environ.get("SDMI_DIT_WG_GROUP", "6")))
     _pending_wg = {}
 
     def _wgrad_linear(self, dy, x, gW, gb=None):
