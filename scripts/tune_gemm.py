@@ -40,7 +40,7 @@ def time_launch(L, d, ws, stream, iters=10, rounds=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "dit", "sample"))
+    ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "uncond-unet", "dit", "sample"))
     ap.add_argument("--sample-batch", type=int, default=1)
     ap.add_argument("--out", default=os.path.join(REPO, "stablediffusion-pytorch_amd", "sdmi", "tuned_gemm.json"))
     args = ap.parse_args()
@@ -59,12 +59,20 @@ def main():
                 v.normal_(0, 0.02)
         tr = DDPMTrainer(cfg, sd, dev, base="dit", lr=1e-4, ema_decay=None)
         text = None
+    elif args.workload == "uncond-unet":  # config/celebhq.yaml (bench.py --workload uncond-unet)
+        import models.unet_base as mu
+        cfg = bench.uncond_config()
+        torch.manual_seed(0)
+        tr = DDPMTrainer(cfg, mu.Unet(4, cfg).state_dict(), dev, base="uncond", sched=(1000, 0.0015, 0.0195))
+        text = None
     else:
         cfg = bench.cond_config()
         torch.manual_seed(0)
         tr = DDPMTrainer(cfg, mc.Unet(4, cfg).state_dict(), dev)
     x0, text_, empty, mask = bench.synthetic_batch(B, dev, 1)
-    if args.workload != "dit":
+    if args.workload == "uncond-unet":
+        mask = None
+    if args.workload not in ("dit", "uncond-unet"):
         text = text_
     noise = torch.randn_like(x0)
     t = torch.randint(0, 1000, (B,), device=dev)
