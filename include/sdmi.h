@@ -310,6 +310,15 @@ int sdmi_affine_step(const float* x, const float* eps, const float* z, long long
 int sdmi_randn(float* out, long long n, unsigned long long seed, unsigned long long* offset_dev, int advance,
                sdmi_stream_t stream);
 
+/* Every random draw of one training step in ONE launch (train_ddpm_cond_celebhq_multi_gpu.py:299-330 /
+ * diffusion_utils.py:21-37 draw them with torch.randn / randint / rand + where): noise[n] ~ N(0,1), t[b] uniform in
+ * [0, T), txt[b] = (u < p_text) ? empty : text[b] (rows of row_elems fp32; txt == NULL skips the text drop),
+ * keep[b] = (u > p_keep) ? 1 : 0 (keep == NULL skips it). Philox4x32-10 keyed by seed at draw offset `offset`
+ * (the caller advances it every step). */
+int sdmi_step_draw(float* noise, long long n, long long* t, int B, int T, const float* text, const float* empty,
+                   float* txt, long long row_elems, float p_text, float* keep, float p_keep, unsigned long long seed,
+                   unsigned long long offset, sdmi_stream_t stream);
+
 /* bf16 GEMM-layout weight packing (the per-step fp32 -> bf16 cast that autocast performs,
  * train_ddpm_cond_celebhq_multi_gpu.py:281-283, fused with the layout change):
  * dst[o][a][b][i] = bf16(src[o*so + i*si + (kh_off + kh_mul*a)*skh + (kw_off + kw_mul*b)*skw]), 0 for i >= I. */

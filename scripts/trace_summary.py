@@ -1,5 +1,5 @@
 """Per-kernel time of ONE training step from a rocprofv3 --kernel-trace CSV (true kernel durations,
-no host gaps): takes the dispatches between the last two optimizer launches, groups them by kernel
+no host gaps): takes the dispatches between the last two step markers (add_noise), groups them by kernel
 name + grid, and prints the groups by total time, plus the step's busy time and idle gaps.
 Usage: python scripts/trace_summary.py <run_kernel_trace.csv> [--top 50]"""
 import argparse
@@ -20,10 +20,11 @@ def main():
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # one gradient-norm launch per step (the optimizer itself runs in chunks pipelined into the next forward)
-    marks = [i for i, r in enumerate(rows) if "sumsq_kernel" in r["Kernel_Name"]]
+    # one step marker per step: the noise draw of the step's batch (add_noise_kernel; the gradient norm now runs in
+    # several sumsq pieces per step, so it no longer marks steps), the optimizer chunks pipeline into the next forward
+    marks = [i for i, r in enumerate(rows) if "add_noise_kernel" in r["Kernel_Name"]]
     if len(marks) < 2:
-        raise SystemExit("need >= 2 gradient-norm launches in the trace")
+        raise SystemExit("need >= 2 add_noise launches (steps) in the trace")
     step = rows[marks[-2] + 1: marks[-1] + 1]
     t0 = int(step[0]["Start_Timestamp"])
     t1 = int(step[-1]["End_Timestamp"])

@@ -24,6 +24,7 @@
 #include "common.h"
 #include "../../include/sdmi.h"
 #include <cstdlib>
+#include <algorithm>
 #include <type_traits>
 
 namespace {
@@ -317,7 +318,9 @@ __global__ __launch_bounds__(NT, OCC) void attn_fwd_kernel(AttnArgs a) {
 // =============================================================================================
 // backward: dK, dV (keys on lanes, 128 keys per workgroup, query tiles streamed)
 // =============================================================================================
-template <int DT, int OCC = 2>
+// G: 16-key groups per wave (2: 128 keys per workgroup; 4: 256, every staged Q / dO tile and LDS fragment serves twice
+// the keys). The query tile is consumed in two 32-query halves so the live P / dS accumulators stay at G x 2.
+template <int DT, int OCC = 2, int G = 2>
 __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][Q|dO]
@@ -328,12 +331,12 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
   const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
   const bf16_t* dO = a.dout + (long long)b * a.N * a.lddo;
 
-  int mykey[2];
-  s16x8 kf[2][KS], vf[2][KS];
-  f32x4 dk[2][DT], dv[2][DT];
+  int mykey[G];
+  s16x8 kf[G][KS], vf[G][KS];
+  f32x4 dk[G][DT], dv[G][DT];
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    mykey[g] = blockIdx.x * ROWS + wave * 32 + g * 16 + (lane & 15);
+  for (int g = 0; g < G; ++g) {
+    mykey[g] = blockIdx.x * (64 * G) + wave * 16 * G + g * 16 + (lane & 15);
     row_frags<DP>(kf[g], a.k + (long long)b * a.S * a.ldk, a.ldk, mykey[g], a.S, h * a.d, a.d, lane);
     row_frags<DP>(vf[g], a.v + (long long)b * a.S * a.ldv, a.ldv, mykey[g], a.S, h * a.d, a.d, lane);
 #pragma unroll
@@ -368,39 +371,47 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
     if (more) fetch(q0 + TILE);
     const bf16_t* sQ = smem + cur * 2 * Tile<DP>::ELEMS;
     const bf16_t* sO = sQ + Tile<DP>::ELEMS;
-    f32x4 p[2][4], ds[2][4];
 #pragma unroll
-    for (int qb = 0; qb < 4; ++qb) {
-      const int qi = qb * 16 + (lane >> 4) * 4;
-      const f32x4 nL = *(const f32x4*)&sLD[cur][0][qi], nD = *(const f32x4*)&sLD[cur][1][qi];
-      // dP accumulates on top of -delta: the MFMA yields dP - delta directly (no per-element subtraction)
-      p[0][qb] = p[1][qb] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      ds[0][qb] = ds[1][qb] = nD;
+    for (int s2 = 0; s2 < 2; ++s2) {  // query rows 32*s2 .. +32 of the tile
+      f32x4 p[G][2], ds[G][2];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        s16x8 qa = frag_rows<DP>(sQ, qb * 16, ks * 32, lane);
-        s16x8 oa = frag_rows<DP>(sO, qb * 16, ks * 32, lane);
-        p[0][qb] = mfma(qa, kf[0][ks], p[0][qb]);
-        p[1][qb] = mfma(qa, kf[1][ks], p[1][qb]);
-        ds[0][qb] = mfma(oa, vf[0][ks], ds[0][qb]);
-        ds[1][qb] = mfma(oa, vf[1][ks], ds[1][qb]);
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int qb = 2 * s2 + h2;
+        const int qi = qb * 16 + (lane >> 4) * 4;
+        const f32x4 nL = *(const f32x4*)&sLD[cur][0][qi], nD = *(const f32x4*)&sLD[cur][1][qi];
+        // dP accumulates on top of -delta: the MFMA yields dP - delta directly (no per-element subtraction)
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          p[g][h2] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          ds[g][h2] = nD;
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s16x8 qa = frag_rows<DP>(sQ, qb * 16, ks * 32, lane);
+          s16x8 oa = frag_rows<DP>(sO, qb * 16, ks * 32, lane);
+#pragma unroll
+          for (int g = 0; g < G; ++g) p[g][h2] = mfma(qa, kf[g][ks], p[g][h2]);
+#pragma unroll
+          for (int g = 0; g < G; ++g) ds[g][h2] = mfma(oa, vf[g][ks], ds[g][h2]);
+        }
+        const float nl[4] = {nL[0], nL[1], nL[2], nL[3]};
+#pragma unroll
+        for (int g = 0; g < G; ++g) p_ds(p[g][h2], ds[g][h2], c, nl);
       }
-      const float nl[4] = {nL[0], nL[1], nL[2], nL[3]};
+      s16x8 pf[G], df[G];
 #pragma unroll
-      for (int g = 0; g < 2; ++g) p_ds(p[g][qb], ds[g][qb], c, nl);
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      s16x8 pf0 = pack_acc(p[0][2 * s2], p[0][2 * s2 + 1]), pf1 = pack_acc(p[1][2 * s2], p[1][2 * s2 + 1]);
-      s16x8 df0 = pack_acc(ds[0][2 * s2], ds[0][2 * s2 + 1]), df1 = pack_acc(ds[1][2 * s2], ds[1][2 * s2 + 1]);
+      for (int g = 0; g < G; ++g) {
+        pf[g] = pack_acc(p[g][0], p[g][1]);
+        df[g] = pack_acc(ds[g][0], ds[g][1]);
+      }
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         s16x8 ot = frag_tr<DP>(sO, 32 * s2, 16 * t, lane);
-        dv[0][t] = mfma(ot, pf0, dv[0][t]);
-        dv[1][t] = mfma(ot, pf1, dv[1][t]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) dv[g][t] = mfma(ot, pf[g], dv[g][t]);
         s16x8 qt = frag_tr<DP>(sQ, 32 * s2, 16 * t, lane);
-        dk[0][t] = mfma(qt, df0, dk[0][t]);
-        dk[1][t] = mfma(qt, df1, dk[1][t]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) dk[g][t] = mfma(qt, df[g], dk[g][t]);
       }
     }
     if (more) put(cur ^ 1);
@@ -408,7 +419,7 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
     cur ^= 1;
   }
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < G; ++g)
     if (mykey[g] < a.S) {
       bf16_t* DK = a.dk + ((long long)b * a.S + mykey[g]) * a.lddk + h * a.d;
       bf16_t* DV = a.dv + ((long long)b * a.S + mykey[g]) * a.lddv + h * a.d;
@@ -424,9 +435,9 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
 }
 
 // =============================================================================================
-// backward: dQ (queries on lanes, 128 queries per workgroup, key tiles streamed)
+// backward: dQ (queries on lanes, 64 * G queries per workgroup, key tiles streamed)
 // =============================================================================================
-template <int DT, int OCC = 2>
+template <int DT, int OCC = 2, int G = 2>
 __global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
@@ -436,13 +447,13 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   const bf16_t* K = a.k + (long long)b * a.S * a.ldk;
   const bf16_t* V = a.v + (long long)b * a.S * a.ldv;
 
-  int myq[2];
-  s16x8 qf[2][KS], of[2][KS];
-  float nlse[2], ndlt[2];
-  f32x4 dq[2][DT];
+  int myq[G];
+  s16x8 qf[G][KS], of[G][KS];
+  float nlse[G], ndlt[G];
+  f32x4 dq[G][DT];
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    myq[g] = blockIdx.x * ROWS + wave * 32 + g * 16 + (lane & 15);
+  for (int g = 0; g < G; ++g) {
+    myq[g] = blockIdx.x * (64 * G) + wave * 16 * G + g * 16 + (lane & 15);
     row_frags<DP>(qf[g], a.q + (long long)b * a.N * a.ldq, a.ldq, myq[g], a.N, h * a.d, a.d, lane);
     row_frags<DP>(of[g], a.dout + (long long)b * a.N * a.lddo, a.lddo, myq[g], a.N, h * a.d, a.d, lane);
     const bool ok = myq[g] < a.N;
@@ -485,45 +496,50 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
     }
     const bf16_t* sK = smem + cur * 2 * Tile<DP>::ELEMS;
     const bf16_t* sV = sK + Tile<DP>::ELEMS;
-    f32x4 ds[2][4];
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      f32x4 sc[2], dp[2];
-      sc[0] = sc[1] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      // dP accumulates on top of -delta (per query = per lane): the MFMA yields dP - delta directly
-      dp[0] = (f32x4){ndlt[0], ndlt[0], ndlt[0], ndlt[0]};
-      dp[1] = (f32x4){ndlt[1], ndlt[1], ndlt[1], ndlt[1]};
+    for (int s2 = 0; s2 < 2; ++s2) {  // keys 32*s2 .. +32 of the tile
+      f32x4 ds[G][2];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        s16x8 ka = frag_rows<DP>(sK, kb * 16, ks * 32, lane);
-        s16x8 va = frag_rows<DP>(sV, kb * 16, ks * 32, lane);
-        sc[0] = mfma(ka, qf[0][ks], sc[0]);
-        sc[1] = mfma(ka, qf[1][ks], sc[1]);
-        dp[0] = mfma(va, of[0][ks], dp[0]);
-        dp[1] = mfma(va, of[1][ks], dp[1]);
-      }
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int kb = 2 * s2 + h2;
+        f32x4 sc[G], dp[G];
+        // dP accumulates on top of -delta (per query = per lane): the MFMA yields dP - delta directly
 #pragma unroll
-      for (int g = 0; g < 2; ++g) {
-        float e[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) e[i] = fast_exp2(fmaf(sc[g][i], c, nlse[g]));
-        if constexpr (decltype(rag)::value) {  // keys >= S of the last ragged tile contribute nothing
-          const int lim = a.S - k0 - kb * 16 - (lane >> 4) * 4;
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (i >= lim) e[i] = 0.f;
+        for (int g = 0; g < G; ++g) {
+          sc[g] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          dp[g] = (f32x4){ndlt[g], ndlt[g], ndlt[g], ndlt[g]};
         }
-        ds[g][kb] = (f32x4){e[0] * dp[g][0], e[1] * dp[g][1], e[2] * dp[g][2], e[3] * dp[g][3]};
-      }
-    }
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      s16x8 df0 = pack_acc(ds[0][2 * s2], ds[0][2 * s2 + 1]), df1 = pack_acc(ds[1][2 * s2], ds[1][2 * s2 + 1]);
+        for (int ks = 0; ks < KS; ++ks) {
+          s16x8 ka = frag_rows<DP>(sK, kb * 16, ks * 32, lane);
+          s16x8 va = frag_rows<DP>(sV, kb * 16, ks * 32, lane);
+#pragma unroll
+          for (int g = 0; g < G; ++g) sc[g] = mfma(ka, qf[g][ks], sc[g]);
+#pragma unroll
+          for (int g = 0; g < G; ++g) dp[g] = mfma(va, of[g][ks], dp[g]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          float e[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) e[i] = fast_exp2(fmaf(sc[g][i], c, nlse[g]));
+          if constexpr (decltype(rag)::value) {  // keys >= S of the last ragged tile contribute nothing
+            const int lim = a.S - k0 - kb * 16 - (lane >> 4) * 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (i >= lim) e[i] = 0.f;
+          }
+          ds[g][h2] = (f32x4){e[0] * dp[g][0], e[1] * dp[g][1], e[2] * dp[g][2], e[3] * dp[g][3]};
+        }
+      }
+      s16x8 df[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) df[g] = pack_acc(ds[g][0], ds[g][1]);
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         s16x8 kt = frag_tr<DP>(sK, 32 * s2, 16 * t, lane);
-        dq[0][t] = mfma(kt, df0, dq[0][t]);
-        dq[1][t] = mfma(kt, df1, dq[1][t]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) dq[g][t] = mfma(kt, df[g], dq[g][t]);
       }
     }
     if (more) {
@@ -538,7 +554,7 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
   for (; k0 + TILE <= a.S; k0 += TILE) step(k0, Full{});
   if (k0 < a.S) step(k0, Ragged{});
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < G; ++g)
     if (myq[g] < a.N) {
       bf16_t* DQ = a.dq + ((long long)b * a.N + myq[g]) * a.lddq + h * a.d;
 #pragma unroll
@@ -866,13 +882,31 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
   int rc = check_args(a);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  // the dQ kernel also produces delta = rowsum(dO * O) (written to delta_ws) for the dK/dV kernel after it
-  dim3 gk((S + ROWS - 1) / ROWS, B * H), gq((N + ROWS - 1) / ROWS, B * H);
+  // the dQ kernel also produces delta = rowsum(dO * O) (written to delta_ws) for the dK/dV kernel after it.
+  // 16-row groups per wave of both kernels (head dims <= 32): 4 (256 rows per workgroup) when N, S <= 256 -- measured
+  // at B = 32, 16 heads: 16^2 d = 24 56.7 -> 48.6 us, d = 32 49.0 -> 44.2 us -- else 2 (128 rows; at 32^2 the two
+  // forms measured equal: 279 / 291 / 352 vs 270 / 292 / 348 us at d = 8 / 16 / 24). SDMI_ATTN_G=2 / 4 forces one.
+  static int G = -1;
+  if (G < 0) {
+    const char* e = getenv("SDMI_ATTN_G");
+    G = e ? atoi(e) : 0;
+  }
+  // (and only while the 256-row grids keep >= 512 workgroups, two per CU: DiT-12L's 9-head 16^2 attention, 288
+  // workgroups, measured 3.90 / 3.91 -> 3.92 / 3.92 ms per step with G = 4)
+  const long long wg4 = (long long)B * H * ((std::min(N, S) + 255) / 256);
+  const int g4 = d <= 32 && (G == 4 || (G != 2 && N <= 256 && S <= 256 && wg4 >= 512));
+  const int rows = g4 ? 256 : ROWS;
+  dim3 gk((S + rows - 1) / rows, B * H), gq((N + rows - 1) / rows, B * H);
   const int oq = attn_occ(1, d), ok = attn_occ(2, d);
   switch ((d + 15) / 16) {
 #define SDMI_ATTN_BWD(DT)                                                                                  \
   case DT:                                                                                                 \
     if constexpr (DT <= 2) {                                                                               \
+      if (g4) {                                                                                            \
+        sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2, 4>, gq, dim3(NT), 0, s, a);                              \
+        sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2, 4>, gk, dim3(NT), 0, s, a);                             \
+        break;                                                                                             \
+      }                                                                                                    \
       if (oq >= 3) sdmi_rt::launch(attn_bwd_dq_kernel<DT, 3>, gq, dim3(NT), 0, s, a);                     \
       else sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2>, gq, dim3(NT), 0, s, a);                              \
       if (ok >= 3) sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 3>, gk, dim3(NT), 0, s, a);                    \

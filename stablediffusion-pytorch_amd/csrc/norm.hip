@@ -152,10 +152,24 @@ __device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, f
   if (cw > nthr) {  // narrow workgroup, wide strip: one thread per channel, all batch rows in order
     for (int ch = t; ch < cw; ch += blockDim.x) {
       float x1 = 0.f, x2 = 0.f;
-      for (int b = 0; b < a.nb; ++b) {
-        const float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
-        x1 += ld_coherent(rp);
-        x2 += ld_coherent(rp + 1);
+      // 16 rows' coherent loads in flight before they are summed (in row order): one cross-XCD round trip per 16
+      // rows instead of one per row
+      for (int b0 = 0; b0 < a.nb; b0 += 16) {
+        float r1[16], r2[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int b = min(b0 + u, a.nb - 1);
+          const float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
+          r1[u] = ld_coherent(rp);
+          r2[u] = ld_coherent(rp + 1);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          if (b0 + u < a.nb) {
+            x1 += r1[u];
+            x2 += r2[u];
+          }
+        }
       }
       const int c = c0 + ch;
       if (c < c_store) {
@@ -169,19 +183,19 @@ __device__ __forceinline__ void batch_tail(const StripArgs& a, int c0, int cw, f
   const int ch = t % cw, bg = t / cw;
   float x1 = 0.f, x2 = 0.f;
   if (t < nthr && bg < nbg && t < nbg * cw) {
-    // issue 8 rows' coherent loads before summing them: the sum then waits once per batch of loads instead of
+    // issue 16 rows' coherent loads before summing them: the sum then waits once per batch of loads instead of
     // once per load (a dependent chain of cross-XCD round trips otherwise)
-    for (int b0 = bg; b0 < a.nb; b0 += 8 * nbg) {
-      float r1[8], r2[8];
+    for (int b0 = bg; b0 < a.nb; b0 += 16 * nbg) {
+      float r1[16], r2[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         const int b = min(b0 + u * nbg, a.nb - 1);
         const float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
         r1[u] = ld_coherent(rp);
         r2[u] = ld_coherent(rp + 1);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         if (b0 + u * nbg < a.nb) {
           x1 += r1[u];
           x2 += r2[u];

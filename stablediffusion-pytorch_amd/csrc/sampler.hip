@@ -209,6 +209,70 @@ __global__ void randn_kernel(float* out, long long n, unsigned long long seed, c
   }
 }
 
+__device__ __forceinline__ void philox10(uint32_t (&c)[4], unsigned long long seed) {
+  uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c, k);
+    k[0] += 0x9E3779B9u;
+    k[1] += 0xBB67AE85u;
+  }
+}
+
+// per-sample draws of one training step: Philox block (B-independent quad index 2^40 + b, offset) ->
+// c[0]: timestep, c[1]: text-drop uniform, c[2]: image-keep uniform (24-bit uniforms in [0, 1), as torch.rand)
+__device__ __forceinline__ void sample_draw(int b, unsigned long long seed, unsigned long long off, uint32_t (&c)[4]) {
+  const unsigned long long q = (1ull << 40) + (unsigned long long)b;
+  c[0] = (uint32_t)q; c[1] = (uint32_t)(q >> 32); c[2] = (uint32_t)off; c[3] = (uint32_t)(off >> 32);
+  philox10(c, seed);
+}
+
+// One launch for every random draw of a training step (train_ddpm_cond_celebhq_multi_gpu.py:299-330 draws them with
+// five torch calls + a where): grid-stride over [noise quads | text rows (float4) | samples].
+//   noise[i] ~ N(0, 1) (Philox quad i / 4, Box-Muller as randn_kernel); t[b] = floor(u * T);
+//   txt[b] = (u_text < p_text) ? empty : text[b] (diffusion_utils.py:21-28); keep[b] = (u_keep > p_keep) (:31-37)
+__global__ void step_draw_kernel(float* noise, long long n, long long* t, int B, int T, const float4* text,
+                                 const float4* empty, float4* txt, long long row4, float p_text, float* keep,
+                                 float p_keep, unsigned long long seed, unsigned long long off) {
+  const long long nq = (n + 3) / 4, ntx = txt ? (long long)B * row4 : 0;
+  const long long total = nq + ntx + B;
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    if (i < nq) {
+      uint32_t c[4] = {(uint32_t)i, (uint32_t)((unsigned long long)i >> 32), (uint32_t)off, (uint32_t)(off >> 32)};
+      philox10(c, seed);
+      float z[4];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float u1 = ((c[2 * p] >> 8) + 1) * (1.0f / 16777216.0f);  // (0, 1]
+        const float u2 = (c[2 * p + 1] >> 8) * (1.0f / 16777216.0f);    // [0, 1)
+        const float rad = sqrtf(-2.0f * logf(u1));
+        float sn, co;
+        sincosf(6.28318530717958647692f * u2, &sn, &co);
+        z[2 * p] = rad * co;
+        z[2 * p + 1] = rad * sn;
+      }
+      const long long i0 = i * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (i0 + e < n) noise[i0 + e] = z[e];
+    } else if (i < nq + ntx) {
+      const long long j = i - nq;
+      const int b = (int)(j / row4);
+      const long long r = j - (long long)b * row4;
+      uint32_t c[4];
+      sample_draw(b, seed, off, c);
+      const bool drop = (c[1] >> 8) * (1.0f / 16777216.0f) < p_text;
+      txt[j] = drop ? empty[r] : text[j];
+    } else {
+      const int b = (int)(i - nq - ntx);
+      uint32_t c[4];
+      sample_draw(b, seed, off, c);
+      t[b] = (long long)(((unsigned long long)c[0] * (unsigned long long)T) >> 32);
+      if (keep) keep[b] = (c[2] >> 8) * (1.0f / 16777216.0f) > p_keep ? 1.0f : 0.0f;
+    }
+  }
+}
+
 __global__ void advance_kernel(unsigned long long* offset) {
   if (threadIdx.x == 0) *offset = *offset + 1;
 }
@@ -225,5 +289,20 @@ extern "C" int sdmi_randn(float* out, long long n, unsigned long long seed, unsi
     sdmi_rt::launch(advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, offset_dev);
     SDMI_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+extern "C" int sdmi_step_draw(float* noise, long long n, long long* t, int B, int T, const float* text,
+                              const float* empty, float* txt, long long row_elems, float p_text, float* keep,
+                              float p_keep, unsigned long long seed, unsigned long long offset, sdmi_stream_t stream) {
+  if (!noise || n <= 0 || !t || B <= 0 || T <= 0) return -1;
+  if (txt && (!text || !empty || row_elems <= 0 || row_elems % 4 || (uintptr_t)text % 16 || (uintptr_t)empty % 16 ||
+              (uintptr_t)txt % 16))
+    return -2;
+  const long long items = (n + 3) / 4 + (txt ? (long long)B * (row_elems / 4) : 0) + B;
+  sdmi_rt::launch(step_draw_kernel, dim3(grid_for(items)), dim3(NT), 0, (hipStream_t)stream, noise, n, t, B, T,
+                  (const float4*)text, (const float4*)empty, (float4*)txt, row_elems / 4, p_text, keep, p_keep, seed,
+                  offset);
+  SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -134,6 +134,8 @@ SIGNATURES = {
     "sdmi_affine_step": ([_P, _P, _P, _L, _F, _F, _F, _P, _P], _I),
     "sdmi_mse_patch": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P], _I),
     "sdmi_randn": ([_P, _L, ctypes.c_ulonglong, _P, _I, _P], _I),
+    "sdmi_step_draw": ([_P, _L, _P, _I, _I, _P, _P, _P, _L, ctypes.c_float, _P, ctypes.c_float, ctypes.c_ulonglong,
+                        ctypes.c_ulonglong, _P], _I),
     "sdmi_relu": ([_P, _P, _P, _L, _P], _I),
     "sdmi_vq_bwd_workspace": ([], _SZ),
     "sdmi_vq_bwd": ([_P, _I, _P, _P, _P, _P, _P, _I, _P, _I, _P, _I, _I, _I, _F, _F, _P, _I, _P, _P, _P, _P, _P, _P,
