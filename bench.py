@@ -442,7 +442,7 @@ def main_sample(args, wl, world, rank, device):
               "vs_baseline": None, "dtype": "bf16", "data": "synthetic latents / text / masks, random-init weights",
               "config": {"workload": f"cond-UNet {args.sampler.upper()} reverse step (model forward + "
                                      f"{'DDIM update' if args.sampler == 'ddim' else 'sample_prev_timestep'}), captured",
-                         "sampler": args.sampler,
+                         "sampler": args.sampler, "issue": loop.issue,
                          "model": "cond-UNet 118.5M", "samples_per_gpu": B, "latent": [4, 32, 32],
                          "parallelism": f"replicas{world}"},
               "eager_steps_per_s": res["eager"], "captured_speedup": sps / res["eager"],

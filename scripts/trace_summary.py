@@ -17,14 +17,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=50)
+    ap.add_argument("--marker", default="add_noise_kernel",
+                    help="kernel name marking one step per occurrence (sampling: ddpm_prev_kernel)")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # one step marker per step: the noise draw of the step's batch (add_noise_kernel; the gradient norm now runs in
     # several sumsq pieces per step, so it no longer marks steps), the optimizer chunks pipeline into the next forward
-    marks = [i for i, r in enumerate(rows) if "add_noise_kernel" in r["Kernel_Name"]]
+    marks = [i for i, r in enumerate(rows) if args.marker in r["Kernel_Name"]]
     if len(marks) < 2:
-        raise SystemExit("need >= 2 add_noise launches (steps) in the trace")
+        raise SystemExit(f"need >= 2 {args.marker} launches (steps) in the trace")
     step = rows[marks[-2] + 1: marks[-1] + 1]
     t0 = int(step[0]["Start_Timestamp"])
     t1 = int(step[-1]["End_Timestamp"])

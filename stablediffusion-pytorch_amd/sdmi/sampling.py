@@ -1,7 +1,8 @@
 """Captured sampling loops: the reference's samplers -- T x [model(x_t, t) -> LinearNoiseScheduler.sample_prev_timestep]
 (tools/sample_ddpm_vqvae.py:29-52, tools/sample_ddpm_text_image_cond.py) and DDIMSampler.forward's
-`steps` x [model(x_t, t, cond) -> DDIM update] (scheduler/linear_noise_scheduler.py:209-256) -- recorded ONCE as a
-native launch plan and replayed per step with no host work.
+`steps` x [model(x_t, t, cond) -> DDIM update] (scheduler/linear_noise_scheduler.py:209-256) -- captured ONCE (as
+one hipGraph per reverse step, default, or as sdmi.plan's native launch list: SDMI_SAMPLE_ISSUE=plan) and replayed
+per step with no host work.
 
 Everything a step needs lives on the device: the model's timestep is an int64 device scalar read by the
 time-embedding kernel; the DDPM step kernel (sdmi_ddpm_prev) decrements it after the step, the DDIM step kernel
@@ -13,6 +14,7 @@ on the CPU, scheduler :72) and syncs on `t == 0` every step.
 A model that does not run on the fused engine (a swapped leaf, SURVEY.md §8(b), or sdmi_leaf_path = True) is
 sampled stepwise through its own forward (`model(x, t, cond)`), with the same step kernels and noise."""
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -48,6 +50,14 @@ class _Loop:
         self.cond = cond_input
         self.text, self.mask, self.klass = c.get("text"), c.get("image"), c.get("class")
         self.plan = None
+        # captured issue: "graph" (default) -- the reverse step as ONE hipGraph launch (torch.cuda.CUDAGraph of the
+        # eager step: every kernel node, the context stream's fork / join as graph edges); "plan" -- sdmi.plan's
+        # native launch list re-issued per step. Both bit-identical to the stepwise loop; the graph removes the
+        # per-launch host issue that bounds the small-batch step (scripts/sample_graph_probe.py)
+        self.issue = os.environ.get("SDMI_SAMPLE_ISSUE", "graph")
+        if self.issue not in ("graph", "plan"):
+            raise ValueError(f"SDMI_SAMPLE_ISSUE={self.issue!r}: graph or plan")
+        self.graph = None
 
     def _refresh(self):
         """Pack the current weights (plain kernel launches into the engine's fixed buffers, outside the plan): a loop
@@ -76,6 +86,14 @@ class _Loop:
         for _ in range(steps):
             if not captured:
                 self._step()
+            elif self.issue == "graph":
+                if self.graph is None:  # the first step runs eagerly, then the step is captured (capture runs nothing)
+                    self._step()
+                    self.graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(self.graph):
+                        self._step()
+                else:
+                    self.graph.replay()
             elif self.plan is None:  # the first step is recorded while it runs
                 self.plan = StepPlan(self._step, self.dev)
             else:

@@ -660,7 +660,11 @@ class UNetEngine:
             st["S"] = S
         st["ctx"] = ctx
         time_c["ctx"] = ctx
-        if ctx is not None and self.ctx_stream is not None:
+        # inference (no backward) keeps the context branch inline: the sampler's reverse step measured 1.75 vs 2.02 ms
+        # at B = 1 and 2.51 vs 2.64 ms at B = 8 (scripts/sample_graph_probe.py) -- its small launches gain nothing
+        # from running beside the forward and the stream's event edges cost a dispatch each; it also keeps the step
+        # one stream, which a hipGraph replays as one batch (multi-stream graphs replay at eager host cost)
+        if ctx is not None and self.ctx_stream is not None and need_backward:
             self._ctx_ahead(st, B)
         elif ctx is not None:  # every context_proj in one GEMM (inline context branch)
             st["cp_all"] = self._new(B * st["S"], self.ctx_total)

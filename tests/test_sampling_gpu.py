@@ -26,8 +26,10 @@ def _model(cond, seed=3):
     return m.cuda().eval()
 
 
+@pytest.mark.parametrize("issue", ["graph", "plan"])
 @pytest.mark.parametrize("cond", [False, True])
-def test_captured_loop_matches_stepwise(cond):
+def test_captured_loop_matches_stepwise(cond, issue, monkeypatch):
+    monkeypatch.setenv("SDMI_SAMPLE_ISSUE", issue)  # one hipGraph per step, or the native launch plan
     from sdmi.sampling import DDPMSampleLoop
     from scheduler.linear_noise_scheduler import LinearNoiseScheduler
     model = _model(cond)
@@ -40,13 +42,14 @@ def test_captured_loop_matches_stepwise(cond):
     xT = torch.randn(B, 4, 32, 32, generator=g).cuda()
     sched = LinearNoiseScheduler(1000, 0.00085, 0.012)
     cap = DDPMSampleLoop(model, sched, (B, 4, 32, 32), cond_input=c, seed=11)
+    assert cap.issue == issue
     xa, x0a = (v.clone() for v in cap.run(xT, steps=6, captured=True))
     assert cap.t.item() == 1000 - 1 - 6
     eag = DDPMSampleLoop(model, sched, (B, 4, 32, 32), cond_input=c, seed=11)
     xb, x0b = eag.run(xT, steps=6, captured=False)
     torch.cuda.synchronize()
     assert torch.equal(xa, xb) and torch.equal(x0a, x0b)
-    # a second captured run from the same start replays the recorded plan: same result again
+    # a second captured run from the same start replays the recorded graph / plan: same result again
     xc, _ = cap.run(xT, steps=6, captured=True)
     assert torch.equal(xc, xa)
 
@@ -97,12 +100,14 @@ def test_device_noise_is_standard_normal_and_fresh():
     assert torch.equal(z1, z2) and off.item() == 0
 
 
+@pytest.mark.parametrize("issue", ["graph", "plan"])
 @pytest.mark.parametrize("method,eta", [("linear", 0.0), ("quadratic", 0.5)])
-def test_captured_ddim_matches_stepwise(method, eta):
+def test_captured_ddim_matches_stepwise(method, eta, issue, monkeypatch):
     """DDIMSampler.forward (reference scheduler/linear_noise_scheduler.py:209-256) as a recorded loop: device (t, t_prev)
     tables + device step index + device noise, bit-identical to issuing every step eagerly; the drop-in
     DDIMSampler.forward(captured=True) returns the same x_0; one step equals the module's eager sample_one_step
-    (host-table alphas) on the same noise."""
+    (host-table alphas) on the same noise. Both captured issue modes (one hipGraph per step / the native plan)."""
+    monkeypatch.setenv("SDMI_SAMPLE_ISSUE", issue)
     from sdmi.sampling import DDIMSampleLoop, ddim_time_steps
     from scheduler.linear_noise_scheduler import DDIMSampler
     model = _model(True)
