@@ -24,6 +24,8 @@ from . import kernels as K
 from .module_glue import engine_path_ok
 from .plan import StepPlan
 
+_CTX_CACHE = os.environ.get("SDMI_SAMPLE_CTX_CACHE", "1") != "0"  # 0: the context branch recomputed every step (A/B)
+
 
 class _Loop:
     """Shared state of a captured loop: the model binding (fused engine, or a stepwise model call), x_t / noise /
@@ -51,24 +53,31 @@ class _Loop:
         self.text, self.mask, self.klass = c.get("text"), c.get("image"), c.get("class")
         self.plan = None
         # captured issue: "graph" (default) -- the reverse step as ONE hipGraph launch (torch.cuda.CUDAGraph of the
-        # eager step: every kernel node, the context stream's fork / join as graph edges); "plan" -- sdmi.plan's
+        # eager step; one stream, since inference keeps the context branch inline); "plan" -- sdmi.plan's
         # native launch list re-issued per step. Both bit-identical to the stepwise loop; the graph removes the
         # per-launch host issue that bounds the small-batch step (scripts/sample_graph_probe.py)
         self.issue = os.environ.get("SDMI_SAMPLE_ISSUE", "graph")
         if self.issue not in ("graph", "plan"):
             raise ValueError(f"SDMI_SAMPLE_ISSUE={self.issue!r}: graph or plan")
         self.graph = None
+        self.ctx_cache = None
 
     def _refresh(self):
         """Pack the current weights (plain kernel launches into the engine's fixed buffers, outside the plan): a loop
         reused after a training update or an EMA swap samples with the weights of the moment it runs."""
         if self.fused:
             self.eng.refresh_weights()
+            # the context branch (text -> context_proj -> every cross-attention's k|v) is the same for every step of
+            # the loop: computed once per run into fixed buffers (UNetEngine.context_cache) instead of per step
+            if self.text is not None and hasattr(self.eng, "context_cache") and _CTX_CACHE:
+                self.ctx_cache = self.eng.context_cache(self.text, self.ctx_cache)
 
     def _model_eps(self):
         B, C, H, W = self.shape
         if self.fused:
-            pred, _ = self.eng.forward(self.xt, self.t, self.text, self.mask, need_backward=False, klass=self.klass)
+            kw = {"ctx_cache": self.ctx_cache} if self.ctx_cache is not None else {}
+            pred, _ = self.eng.forward(self.xt, self.t, self.text, self.mask, need_backward=False, klass=self.klass,
+                                       **kw)
             self.eps = self.eng.pred_to_nchw(pred, B, H, W)
         else:
             with torch.no_grad():

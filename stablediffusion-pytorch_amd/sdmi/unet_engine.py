@@ -571,9 +571,10 @@ class UNetEngine:
         (sdmi.store.unet_gemm_natural)."""
         return self.g(key).is_contiguous()
 
-    def forward(self, x, t, text=None, mask=None, need_backward=True, mask_keep=None, klass=None):
+    def forward(self, x, t, text=None, mask=None, need_backward=True, mask_keep=None, klass=None, ctx_cache=None):
         """x: (B, C, H, W) fp32; t: int64 (B,), (1,) or 0-d; text: (B, S, ctx) ; mask: (B, cmi, MH, MW) fp32;
-        klass: (B, num_classes) fp32 (one-hot, cond-drop already applied) for class-conditional configs.
+        klass: (B, num_classes) fp32 (one-hot, cond-drop already applied) for class-conditional configs;
+        ctx_cache: context_cache() of the text (inference only: the context branch is then read, not recomputed).
         Returns (pred NHWC fp32 [B*H*W, 8] with the first im_channels valid, tape)."""
         L, P = self.L, self.P
         B, Cx, H, W = x.shape
@@ -651,7 +652,14 @@ class UNetEngine:
         st["temb_all"] = temb_all
 
         ctx = None
-        if L["text"]:
+        if L["text"] and ctx_cache is not None:
+            if need_backward:
+                raise ValueError("ctx_cache is an inference-only input (the backward needs the step's own context)")
+            if ctx_cache["B"] != B:
+                raise ValueError(f"ctx_cache was built for B={ctx_cache['B']}, forward has B={B}")
+            ctx = ctx_cache["ctx"]
+            st.update(S=ctx_cache["S"], cp_all=ctx_cache["cp_all"], kv_cache=ctx_cache["kv"])
+        elif L["text"]:
             txt = plan.as_operand(text)
             S = txt.shape[1]
             ctx = self._new(B * S, txt.shape[2])
@@ -664,7 +672,9 @@ class UNetEngine:
         # at B = 1 and 2.51 vs 2.64 ms at B = 8 (scripts/sample_graph_probe.py) -- its small launches gain nothing
         # from running beside the forward and the stream's event edges cost a dispatch each; it also keeps the step
         # one stream, which a hipGraph replays as one batch (multi-stream graphs replay at eager host cost)
-        if ctx is not None and self.ctx_stream is not None and need_backward:
+        if ctx_cache is not None:
+            pass
+        elif ctx is not None and self.ctx_stream is not None and need_backward:
             self._ctx_ahead(st, B)
         elif ctx is not None:  # every context_proj in one GEMM (inline context branch)
             st["cp_all"] = self._new(B * st["S"], self.ctx_total)
@@ -796,6 +806,33 @@ class UNetEngine:
         st["cp_all"] = cp_all
         st["ctx_pre"] = pre
 
+    def context_cache(self, text, cache=None):
+        """The forward's context branch -- the text context cast to bf16, every context_proj (ONE GEMM) and every
+        cross-attention's k|v rows of its packed in-projection (blocks.py:139-140) -- depends only on the text and
+        the weights. A sampling loop (one condition for all its steps) computes it once per run with this and passes
+        it to forward(ctx_cache=...); `cache` (a previous result) is refilled in place, so a captured step keeps
+        reading the same memory. The launches are the inline branch's own (same shapes, phase and tiles), so the
+        forward's output is bitwise the uncached one's. Returns the cache, or None for a model without text."""
+        if not self.L["text"]:
+            return None
+        B, S, D = text.shape
+        if cache is None:
+            cache = dict(B=B, S=S, ctx=self._new(B * S, D), cp_all=self._new(B * S, self.ctx_total),
+                         kv={(p, l): self._new(B * S, 2 * C) for (p, l, C) in self._cross_layers()})
+        elif (cache["B"], cache["S"], cache["ctx"].shape[1]) != (B, S, D):
+            raise ValueError("context_cache: text shape differs from the cached one")
+        txt = text.float().contiguous()
+        K.PHASE = "fwd"
+        _lib.check(_lib.lib().sdmi_nchw_to_nhwc_bf16(txt.data_ptr(), B * S, D, 1, cache["ctx"].data_ptr(), D,
+                                                     K._stream()), "cast")
+        K.linear(cache["ctx"], self.W("ctxp_all"), cache["cp_all"], bias=self._ctx_bias(self.P))
+        for (p, l, C) in self._cross_layers():
+            mk = f"{p}.cross_attentions.{l}"
+            off = self.ctx_off[(p, l)]
+            K.linear(cache["cp_all"][:, off:off + C], self.W(mk + ".in_proj_weight#f")[C:], cache["kv"][(p, l)],
+                     bias=self.P[mk + ".in_proj_bias"][C:])
+        return cache
+
     def _ctx_bias_keys(self):
         return [f"{p}.context_proj.{l}.bias" for (p, l, c) in self._cross_layers()]
 
@@ -911,6 +948,10 @@ class UNetEngine:
             if pre is not None:  # issued ahead on the context stream (_ctx_ahead)
                 cp, kv, ev = pre[(p, l)]
                 plan.wait_event(torch.cuda.current_stream(self.device), ev)
+            elif st.get("kv_cache") is not None:  # computed once per sampling run (context_cache)
+                off = self.ctx_off[(p, l)]
+                cp = st["cp_all"][:, off:off + C]
+                kv = st["kv_cache"][(p, l)]
             else:
                 off = self.ctx_off[(p, l)]
                 cp = st["cp_all"][:, off:off + C]

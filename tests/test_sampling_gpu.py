@@ -52,6 +52,13 @@ def test_captured_loop_matches_stepwise(cond, issue, monkeypatch):
     # a second captured run from the same start replays the recorded graph / plan: same result again
     xc, _ = cap.run(xT, steps=6, captured=True)
     assert torch.equal(xc, xa)
+    if cond:  # the loop reads the context branch from its per-run cache: bitwise the module's own (uncached) forward
+        one = DDPMSampleLoop(model, sched, (B, 4, 32, 32), cond_input=c, seed=11)
+        one.run(xT, steps=1, captured=False)
+        assert one.ctx_cache is not None
+        with torch.no_grad():
+            eps = model(xT, torch.tensor([999]).cuda(), c)
+        assert torch.equal(eps, one.eps)
 
 
 def test_one_step_matches_reference_arithmetic():
