@@ -407,6 +407,8 @@ __device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0
   }
   __syncthreads();
   if (!*flag) return;
+  // acquire at agent scope before reading the other splits' slabs (they may sit in another XCD's L2 history)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
   const int zstride = (int)(e.split_stride * 4);
   if (e.n8) {

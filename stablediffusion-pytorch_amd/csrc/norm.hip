@@ -67,6 +67,7 @@ __device__ __forceinline__ bool arrive_last(unsigned* ctr, int n) {
     flag = last;
   }
   __syncthreads();
+  if (flag) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // acquire before reading the other arrivals' rows
   return flag != 0;
 }
 

@@ -176,11 +176,13 @@ class DDIMSampler(nn.Module):
 
     @torch.no_grad()
     def forward(self, x_t, cond_input, uncond_input, steps=1, method="linear", eta=0.0, only_return_x_0=True,
-                interval=1, captured=True, seed=0):
+                interval=1, captured=True, seed=None):
         """captured (default): a drop-in denoiser on the fused engine samples through sdmi.sampling.DDIMSampleLoop --
-        the loop recorded once and replayed with device timestep tables and device noise (Philox, `seed`) -- when only
-        x_0 is returned; otherwise (intermediates, foreign models) every step is issued eagerly with torch.randn_like
-        noise as the reference does (:200)."""
+        the loop recorded once and replayed with device timestep tables and device noise (Philox) -- when only x_0 is
+        returned; otherwise (intermediates, foreign models) every step is issued eagerly with torch.randn_like noise as
+        the reference does (:200). seed=None (default): every call draws fresh noise, its Philox stream chosen by
+        torch's default generator (as the reference's randn_like is, so torch.manual_seed makes a call repeatable);
+        an explicit seed makes every call with that seed repeat the same noise."""
         self.cond_input = cond_input
         self.uncond_input = uncond_input
         if captured and only_return_x_0 and hasattr(self.model, "_sdmi"):
@@ -189,13 +191,17 @@ class DDIMSampler(nn.Module):
             if engine_path_ok(self.model):
                 cond_key = tuple(sorted((k, v.data_ptr(), tuple(v.shape)) for k, v in (cond_input or {}).items()
                                         if isinstance(v, torch.Tensor)))
-                key = (tuple(x_t.shape), steps, method, float(eta), int(seed), cond_key)
+                # the parameters' identity is part of the key: replaced (not updated-in-place) weights rebuild the loop
+                params = tuple(p.data_ptr() for p in self.model.parameters())
+                key = (tuple(x_t.shape), steps, method, float(eta), -1 if seed is None else int(seed), cond_key,
+                       hash(params))
                 loop = getattr(self, "_loop", None)
                 if loop is None or self._loop_key != key:
                     loop = DDIMSampleLoop(self.model, self.alpha_t_bar, tuple(x_t.shape), cond_input, steps=steps,
-                                          method=method, eta=eta, seed=seed)
+                                          method=method, eta=eta, seed=0 if seed is None else seed)
                     self._loop, self._loop_key = loop, key
-                return loop.run(x_t.float()).clone()
+                draw = loop.fresh_draw() if seed is None else 0
+                return loop.run(x_t.float(), draw=draw).clone()
         ts, tp = self.time_steps(self.T, steps, method)
         x = [x_t]
         for i in reversed(range(0, steps)):

@@ -31,7 +31,7 @@ class CapturedTrainStep:
         self.txt = torch.empty_like(text) if text is not None else None
         self.keep = torch.empty(B, dtype=torch.float32, device=dev)
         self.mode = mode
-        self.seed = (generator.initial_seed() if generator is not None else 0) & ((1 << 64) - 1)
+        self.seed = self.draw_seed(generator)
         self.draws = 0
         self._draw()
         for _ in range(warmup):  # allocator / lazy init outside the recording
@@ -52,6 +52,18 @@ class CapturedTrainStep:
             torch.cuda.synchronize(dev)
         else:
             raise ValueError(mode)
+
+    @staticmethod
+    def draw_seed(generator=None):
+        """The Philox key of this captured step's draws, taken FROM the generator (its state advances, so a rebuilt
+        CapturedTrainStep -- resume, per-epoch rebuild -- draws a new sequence, as the reference's per-step torch draws
+        would). Without a generator: torch's default generator, with the rank mixed in so DP ranks draw different
+        noise / t / cond-drop, as the reference's per-process RNG does (train_seed + rank)."""
+        dev = generator.device if generator is not None else torch.device("cpu")
+        seed = int(torch.randint(0, 1 << 62, (1,), generator=generator, device=dev).item())
+        if generator is None and torch.distributed.is_available() and torch.distributed.is_initialized():
+            seed ^= (torch.distributed.get_rank() + 1) * 0x9E3779B97F4A7C15 & ((1 << 62) - 1)
+        return seed
 
     def _run(self):
         self.tr.step(self.x0, self.noise, self.t, self.txt, self.mask, mask_keep=self.keep)

@@ -64,13 +64,28 @@ class _Loop:
 
     def _refresh(self):
         """Pack the current weights (plain kernel launches into the engine's fixed buffers, outside the plan): a loop
-        reused after a training update or an EMA swap samples with the weights of the moment it runs."""
+        reused after a training update or an EMA swap samples with the weights of the moment it runs. Parameters
+        REPLACED rather than updated in place (load_state_dict(assign=True), .to(), ...) rebind the engine; a new
+        engine or a re-allocated pack buffer drops the recorded graph / plan, which hold the old pointers."""
         if self.fused:
+            eng = self.model._sdmi.ensure(self.dev)
+            buf = getattr(getattr(eng, "pack", None), "buf", None)
+            if eng is not self.eng:
+                self.eng = eng
+                self._drop_recording()
             self.eng.refresh_weights()
+            nbuf = getattr(getattr(self.eng, "pack", None), "buf", None)
+            if nbuf is not buf:  # refresh_weights re-finalised the pack into a new buffer
+                self._drop_recording()
             # the context branch (text -> context_proj -> every cross-attention's k|v) is the same for every step of
             # the loop: computed once per run into fixed buffers (UNetEngine.context_cache) instead of per step
             if self.text is not None and hasattr(self.eng, "context_cache") and _CTX_CACHE:
                 self.ctx_cache = self.eng.context_cache(self.text, self.ctx_cache)
+
+    def _drop_recording(self):
+        self.graph = None
+        self.plan = None
+        self.ctx_cache = None
 
     def _model_eps(self):
         B, C, H, W = self.shape
@@ -84,6 +99,12 @@ class _Loop:
                 tt = self.t.expand(B)
                 out = self.model(self.xt, tt) if self.cond is None else self.model(self.xt, tt, self.cond)
             self.eps = out.float().contiguous()
+
+    @staticmethod
+    def fresh_draw():
+        """A random 62-bit starting draw counter from torch's default generator: torch.manual_seed governs it, and runs
+        started from different counters draw disjoint Philox streams (a run uses `steps` consecutive counters)."""
+        return int(torch.randint(0, 1 << 62, (1,)).item())
 
     def _draw(self):
         _lib.check(_lib.lib().sdmi_randn(self.z.data_ptr(), self.xt.numel(), ctypes.c_ulonglong(self.seed),
@@ -194,7 +215,9 @@ class DDIMSampleLoop(_Loop):
         self.offset.fill_(int(draw))
 
     def run(self, x_T, captured=True, draw=0):
-        """The whole reversed loop (i = steps - 1 .. 0) from x_T; returns x_0 (the loop's buffer)."""
+        """The whole reversed loop (i = steps - 1 .. 0) from x_T; returns x_0 (the loop's buffer). `draw` is the Philox
+        draw counter the run starts at: runs from the same (seed, draw) repeat their noise exactly; fresh_draw() gives
+        a run noise of its own."""
         self._refresh()
         self.reset(x_T, draw)
         self._iterate(self.steps, captured)

@@ -351,14 +351,20 @@ class DDPMTrainer:
         if self.ema is None:
             raise RuntimeError("this trainer keeps no EMA copy (ema_decay=None)")
         self.sync_optimizer()
-        return {k: self.store.view(self.ema, k) for k in self.store.order}
+        return {k: self._export(self.store.view(self.ema, k)) for k in self.store.order}
+
+    @staticmethod
+    def _export(v):
+        # GEMM-natural (co, kh, kw, ci) weights are permuted views: hand out contiguous torch-order copies so saved
+        # checkpoints match the reference's state dicts (safetensors and .view() consumers need contiguity)
+        return v if v.is_contiguous() else v.contiguous()
 
     def state_dict(self):
         """Model state dict (views of the flat fp32 master weights), safe to read or save on the current stream:
         it first waits for the chunked optimizer step still in flight on the side stream. Never read
         store.params / store.p directly after step() without sync_optimizer()."""
         self.sync_optimizer()
-        return {k: self.store.p[k] for k in self.store.order}
+        return {k: self._export(self.store.p[k]) for k in self.store.order}
 
     def sync_optimizer(self):
         """The current stream waits for the chunked optimizer step still in flight (parameters, EMA and packed

@@ -146,6 +146,36 @@ def test_captured_ddim_matches_stepwise(method, eta, issue, monkeypatch):
     assert torch.equal(one.xt, ref)
 
 
+def test_ddim_sampler_fresh_noise_per_call():
+    """DDIMSampler.forward without a seed draws fresh noise per call like the reference's torch.randn_like (:200): two
+    consecutive eta > 0 calls differ, torch.manual_seed makes a call repeatable, an explicit seed repeats its noise; a
+    model whose parameters were replaced (not updated in place) rebuilds the captured loop."""
+    from scheduler.linear_noise_scheduler import DDIMSampler
+    model = _model(True)
+    g = torch.Generator().manual_seed(13)
+    B = 2
+    c = {"text": torch.randn(B, 77, 64, generator=g).cuda(),
+         "image": one_hot(torch.randint(0, 19, (B, 64, 64), generator=g)).cuda()}
+    xT = torch.randn(B, 4, 32, 32, generator=g).cuda()
+    sampler = DDIMSampler(model, (0.0001, 0.02), 1000)
+    a = sampler(xT, c, None, steps=5, eta=1.0).clone()
+    b = sampler(xT, c, None, steps=5, eta=1.0).clone()
+    assert not torch.equal(a, b)
+    torch.manual_seed(77)
+    r1 = sampler(xT, c, None, steps=5, eta=1.0).clone()
+    torch.manual_seed(77)
+    r2 = sampler(xT, c, None, steps=5, eta=1.0).clone()
+    assert torch.equal(r1, r2)
+    s1 = sampler(xT, c, None, steps=5, eta=1.0, seed=4).clone()
+    s2 = sampler(xT, c, None, steps=5, eta=1.0, seed=4).clone()
+    assert torch.equal(s1, s2)
+    loop = sampler._loop
+    model.load_state_dict({k: v * 0.5 if k == "conv_out.weight" else v for k, v in model.state_dict().items()},
+                          assign=True)
+    s3 = sampler(xT, c, None, steps=5, eta=1.0, seed=4).clone()
+    assert sampler._loop is not loop and not torch.equal(s3, s1)
+
+
 def test_loop_refreshes_weights_and_honours_leaf_path():
     """A loop reused after a weight update written through `.data` (no version bump: the reference's EMA update)
     samples with the new weights; a model forced onto the leaf path is sampled stepwise through its own forward."""

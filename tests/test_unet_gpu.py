@@ -350,6 +350,20 @@ def test_cond_trainer_two_steps_match_reference():
     p = torch.cat([sd[k].flatten().cpu() - sd0[k].flatten() for k in tr.store.order])
     r = torch.cat([ref[k].flatten() - sd0[k].flatten() for k in tr.store.order])
     assert cos(p, r) >= 0.95, cos(p, r)
+    # a checkpoint written from the trainer's state dicts (GEMM-natural conv weights included) is a plain contiguous
+    # torch-order state dict: safetensors saves it and the reference-shaped module loads it with identical tensors
+    import tempfile
+    import models.unet_cond_base as mc
+    from safetensors.torch import save_file
+    for d in (sd, ema_hip):
+        assert all(v.is_contiguous() for v in d.values())
+        with tempfile.TemporaryDirectory() as tmp:
+            save_file({k: v.cpu() for k, v in d.items()}, os.path.join(tmp, "ckpt.safetensors"))
+            back = load_file(os.path.join(tmp, "ckpt.safetensors"))
+        m = mc.Unet(4, cfg)
+        m.load_state_dict(back)
+        for k, v in m.state_dict().items():
+            assert torch.equal(v, d[k].cpu()), k
 
 
 def test_ema_follows_oracle_at_large_lr():
