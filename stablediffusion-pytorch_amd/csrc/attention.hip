@@ -45,10 +45,23 @@ struct AttnArgs {
 };
 
 template <int DP> struct Tile {
-  static constexpr int LD = DP + 8;  // row padded by 16 B
+  static constexpr int LD = DP;  // unpadded rows; the 16-B chunks are XOR-swizzled per row (toff)
   static constexpr int ELEMS = 64 * LD;
   static constexpr int CPT = 64 * DP / 8 / NT;  // 16-B chunks per thread per tile (1 or 2)
 };
+
+// Element offset of 16-B chunk c (8 columns) of row r in a tile image with DP-column rows. The chunk is stored at slot
+// c ^ f(r) so that every accessor is conflict-free on the LDS banks (MI355X guide, LDS table; checked for all three
+// access shapes by scripts/lds_banks.py): frag_rows' ds_read_b128 (rows rbase + lane&15, chunk lane>>4: 4 lane groups
+// x 16 lanes), frag_tr's ds_read_b64_tr_b16 (rows rbase + 8-row block, a 32-B column strip: 2 x 32 lanes) and
+// tile_store's ds_write_b128 (8 lanes = 128 contiguous bytes). 128-B rows (DP 64): f = r & 7; 64-B rows (DP 32):
+// f = {0, 2, 3, 1}[(r >> 2) & 3]. The padded rows used before (LD = DP + 8) cost 2x on every read (8 vs 4 cycles per
+// ds_read_b128, 4 vs 2 per transposed read).
+template <int DP>
+__device__ __forceinline__ int toff(int r, int c) {
+  if constexpr (DP == 64) return r * 64 + ((c ^ (r & 7)) << 3);
+  return r * 32 + ((c ^ ((0x1320 >> (((r >> 2) & 3) * 4)) & 3)) << 3);
+}
 
 // register prefetch of one 64-row x DP tile (zero outside rows < nrows, head columns < d)
 template <int DP>
@@ -71,29 +84,30 @@ __device__ __forceinline__ void tile_store(bf16_t* t, const uint4 (&r)[Tile<DP>:
   for (int j = 0; j < Tile<DP>::CPT; ++j) {
     int c = threadIdx.x + j * NT;
     int rr = c / CPR, ch = c - rr * CPR;
-    *(uint4*)(t + rr * Tile<DP>::LD + ch * 8) = r[j];
+    *(uint4*)(t + toff<DP>(rr, ch)) = r[j];
   }
 }
 
 // fragment with MFMA row = tile row (rbase + lane&15), k = tile columns kbase + 8*(lane>>4) .. +7
 template <int DP>
 __device__ __forceinline__ s16x8 frag_rows(const bf16_t* t, int rbase, int kbase, int lane) {
-  return *(const s16x8*)(t + (rbase + (lane & 15)) * Tile<DP>::LD + kbase + (lane >> 4) * 8);
+  return *(const s16x8*)(t + toff<DP>(rbase + (lane & 15), (kbase >> 3) + (lane >> 4)));
 }
 
 // transposed fragment: MFMA row = tile column (cbase + lane&15), k = tile rows permuted as
-// {rbase + 4g + j (j<4), rbase + 16 + 4g + j-4 (j>=4)} for lane group g = lane>>4
+// {rbase + 4g + j (j<4), rbase + 16 + 4g + j-4 (j>=4)} for lane group g = lane>>4 (rbase % 8 == 0, cbase % 16 == 0)
 template <int DP>
 __device__ __forceinline__ s16x8 frag_tr(const bf16_t* t, int rbase, int cbase, int lane) {
   int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const bf16_t* a1 = t + (rbase + 4 * g + q) * Tile<DP>::LD + cbase + 4 * p;
-  const bf16_t* a2 = a1 + 16 * Tile<DP>::LD;
+  const int r = rbase + 4 * g + q, c = (cbase >> 3) + (p >> 1), w = (p & 1) * 4;
+  const bf16_t* a1 = t + toff<DP>(r, c) + w;
+  const bf16_t* a2 = t + toff<DP>(r + 16, c) + w;
   s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SDMI_LDS s16x4*)a1);
   s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((SDMI_LDS s16x4*)a2);
-  s16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
-  return r;
+  s16x8 r8;
+  r8[0] = lo[0]; r8[1] = lo[1]; r8[2] = lo[2]; r8[3] = lo[3];
+  r8[4] = hi[0]; r8[5] = hi[1]; r8[6] = hi[2]; r8[7] = hi[3];
+  return r8;
 }
 
 // B-operand fragment from two accumulator tiles (rows = k): elements j<4 from a[j], j>=4 from b[j-4]
@@ -719,7 +733,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_fused_kernel(AttnArgs a) {
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       tile_fetch<DP>(rk, Kb, a.ldk, kb * ROWS + half * TILE, a.S, h * a.d, a.d);
-      tile_store<DP>(sK + half * TILE * LDK, rk);
+      tile_store<DP>(sK + half * Tile<DP>::ELEMS, rk);
     }
   }
   int mykey[2];
@@ -817,7 +831,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_fused_kernel(AttnArgs a) {
     for (int ks = 0; ks < ROWS / 32; ++ks) {
       s16x8 sb = frag_tr_ld<LDQ>(sDS, ks * 32, wave * 16, lane);
 #pragma unroll
-      for (int t = 0; t < DT; ++t) dq[t] = mfma(frag_tr_ld<LDK>(sK, ks * 32, t * 16, lane), sb, dq[t]);
+      for (int t = 0; t < DT; ++t) dq[t] = mfma(frag_tr<DP>(sK, ks * 32, t * 16, lane), sb, dq[t]);
     }
     const int myq = q0 + wave * 16 + (lane & 15);
     if (nkb == 1) {
@@ -853,6 +867,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_fused_kernel(AttnArgs a) {
       }
       __syncthreads();
       if (sflag) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the other key blocks' partials: acquire before reading
         const int c4 = a.d / 4;
         for (int i = threadIdx.x; i < TILE * c4; i += NT) {
           const int r = i / c4, d0 = (i - r * c4) * 4, q = q0 + r;
