@@ -528,6 +528,7 @@ def main():
     cfg = dit_config() if is_dit else (uncond_config() if is_uncond else cond_config())
     torch.manual_seed(1111)  # identical initial weights on every rank (DDP broadcasts rank 0's)
     group = dist.group.WORLD if world > 1 else None
+    single = args.issue == "graph" and world == 1  # single-stream hipGraph capture (weight gradients inline)
     if is_dit:
         from models.transformer import DIT
         init = DIT(4, cfg).state_dict()
@@ -535,15 +536,16 @@ def main():
             if v.abs().max() == 0:  # the timed step runs on non-trivial data (zeros clock higher, MI355X DVFS)
                 v.normal_(0.0, 0.02)
         trainer = DDPMTrainer(cfg, init, device, base="dit", lr=1e-4, ema_decay=None, group=group,
-                              grad_wire=args.grad_wire)
+                              grad_wire=args.grad_wire, single_stream=single)
     elif is_uncond:  # tools/train_ddpm_vqvae.py:76-104: Adam(ldm_lr 5e-6, celebhq.yaml:54), no clip, no EMA
         import models.unet_base as mu
         init = mu.Unet(4, cfg).state_dict()
         trainer = DDPMTrainer(cfg, init, device, base="uncond", lr=5e-6, ema_decay=None, max_grad_norm=float("inf"),
-                              sched=(1000, 0.0015, 0.0195), group=group, grad_wire=args.grad_wire)
+                              sched=(1000, 0.0015, 0.0195), group=group, grad_wire=args.grad_wire,
+                              single_stream=single)
     else:
         init = mc.Unet(4, cfg).state_dict()
-        trainer = DDPMTrainer(cfg, init, device, group=group, grad_wire=args.grad_wire)
+        trainer = DDPMTrainer(cfg, init, device, group=group, grad_wire=args.grad_wire, single_stream=single)
     B = args.batch
     x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
     gen = torch.Generator(device=device).manual_seed(1111 + rank)
@@ -570,8 +572,6 @@ def main():
         issue = "plan"
     if issue != "eager":
         from sdmi.graph import CapturedTrainStep
-        if issue == "graph":
-            trainer.engine.side = None  # single-stream capture (weight gradients inline)
         cap = CapturedTrainStep(trainer, x0, None if (is_dit or is_uncond) else text, empty, None if is_uncond else mask,
                                 B, generator=gen, drop_p=drop_p,
                                 mode=issue)
@@ -628,14 +628,19 @@ def main():
             a[2] += 1
             kern = kernel_name(tag, sp)
             split = int(re.search(r"splits=(\d+)", sp).group(1)) > 1
-            k = per_kernel.setdefault(kern, {"fl": 0.0, "ms": 0.0, "n": 0, "fl1": 0.0, "ms1": 0.0, "n1": 0, "mode": tag})
+            k = per_kernel.setdefault(kern, {"fl": 0.0, "ms": 0.0, "n": 0, "fl1": 0.0, "ms1": 0.0, "n1": 0, "mode": tag,
+                                             "by": 0.0, "by1": 0.0})
+            nb = re.search(r"bytes=(\d+)", sp)
+            nb = float(nb.group(1)) if nb else 0.0
             k["fl"] += fl
             k["ms"] += ms
             k["n"] += 1
+            k["by"] += nb
             if not split:  # the event brackets the kernel alone (split launches add a reducer launch)
                 k["fl1"] += fl
                 k["ms1"] += ms
                 k["n1"] += 1
+                k["by1"] += nb
         tot_fl = sum(v[0] for v in by.values())
         tot_ms = sum(v[1] for v in by.values())
         dname, d = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
@@ -643,13 +648,18 @@ def main():
         # otherwise (e.g. DiT weight gradients, whose few unsplit launches are the tiny t-emb GEMMs) all launches count,
         # each event then including its split-K reducer (a lower bound on the kernel's own rate)
         use1 = d["n1"] > 0 and d["fl1"] >= 0.5 * d["fl"]
-        dfl, dms, dn = (d["fl1"], d["ms1"], d["n1"]) if use1 else (d["fl"], d["ms"], d["n"])
+        dfl, dms, dn, dby = (d["fl1"], d["ms1"], d["n1"], d["by1"]) if use1 else (d["fl"], d["ms"], d["n"], d["by"])
         traffic, traffic_unit = pmc_traffic(dname, use1)
+        algo = dby / dn if dn else None  # algorithmic bytes per launch (sdmi.kernels.algo_bytes over the same launches)
         roof = {"bound": "mfma", "kernel": f"sdmi {dname} ({d['mode']}: implicit-GEMM conv fwd/dgrad)"
                 if d["mode"] == "gemm_a1b0" else f"sdmi {dname} ({d['mode']})",
                 "achieved": dfl / (dms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
                 "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic,
                 "traffic_unit": traffic_unit,
+                "algorithmic_bytes": algo,
+                "algorithmic_bytes_note": "per launch: unique operand bytes at their dtypes (conv im2col = the gathered "
+                                          "activation), output and fused epilogue reads, averaged over the same launches",
+                "traffic_ratio": traffic / algo if traffic and algo else None,
                 "launches": dn // PROF_STEPS,
                 "launches_note": f"unsplit launches of the kernel per step (HIP events on its stream, {PROF_STEPS} "
                                  "profiled steps averaged)" if use1 else "all launches (each includes its split-K reducer)",

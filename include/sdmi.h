@@ -111,6 +111,18 @@ typedef struct sdmi_gemm_desc {
    * latency-bound low-resolution GEMMs). Downgraded where the mode does not support it. Used with the measured
    * per-shape table of sdmi/tuned_gemm.json. */
   int variant_hint;
+  /* GroupNorm-backward statistics of the output (SDMI_GN_PART): the GEMM produces dy, the gradient of a
+   * [SiLU(]GroupNorm(x)[)] output (models/blocks.py:45-47, 64-66, 124-126, 137-139; unet_cond_base.py:179-180), and also
+   * writes, per segment of gn_rb rows (gn_rb in {16, 32, 64} divides gn_P, the rows per sample) and output column j,
+   * gn_part[2*(seg*n + j)] = sum dz, gn_part[2*(seg*n + j) + 1] = sum dz*xhat over the segment's rows, where
+   * dz = bf16(dy) [* SiLU'(x*a + s)], xhat = (x - mean)*rstd, x = gn_x[row*gn_ldx + j] (bf16) and {a, s, mean, rstd} =
+   * gn_tab[(row / gn_P)*n + j] (the float4 forward table of sdmi_gn_fwd). Unsplit launches need gn_rb | 64, split-K
+   * launches gn_rb % 8 == 0. Plain epilogue only (alpha; no bias / rowbias / resid / act / remap / perm / reductions;
+   * bf16 16-B aligned output). gn_part NULL = off. sdmi_gn_bwd_part consumes the partials. */
+  const void* gn_x; int gn_ldx;
+  const float* gn_tab;
+  float* gn_part;
+  int gn_P, gn_rb, gn_silu;
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */
@@ -175,6 +187,14 @@ int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const float* table, 
 int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
                 const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws, float* dgamma,
                 float* dbeta, const void* addend, int ldadd, sdmi_stream_t stream);
+/* GroupNorm (+SiLU) backward whose reductions were produced by the data-gradient GEMM that wrote dy
+ * (sdmi_gemm_desc::gn_part, rb rows per segment, part = float2 [B * P / rb][C]): one streaming launch per GroupNorm
+ * (dx = a*dz + q*x + o + addend; dgamma / dbeta) instead of the single-pass kernel's load / reduce / apply phases.
+ * ws: sdmi_chan_reduce_workspace. Same arithmetic as sdmi_gn_bwd up to the fp32 summation order of the partials. */
+int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                     const float* gamma, int B, int P, int C, int G, int silu, const float* part, int rb, float* ws,
+                     float* dgamma, float* dbeta, const void* addend, int ldadd, sdmi_stream_t stream);
+
 int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, float* ws, void* per_bc, int ld_bc, float* per_c,
                   float* per_c2, int c_store, sdmi_stream_t stream);
 
@@ -364,10 +384,8 @@ size_t sdmi_optim_workspace(void);
 int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws, int growth_interval,
                       int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
 int sdmi_loss_flag(const float* src, float* dst, int mode, sdmi_stream_t stream);
-/* The same norm in pieces (the trainer overlaps them with the backward): sdmi_sumsq_partials writes nblocks
- * sum-of-squares partials of grads[0 .. n) (16-B aligned) into partial[0 .. nblocks); sdmi_clip_finalize reduces the
- * first n partials (double accumulation, index order) and applies the clip / skip / scaler update above. */
-int sdmi_sumsq_partials(const float* grads, long long n, float* partial, int nblocks, sdmi_stream_t stream);
+/* sdmi_clip_finalize reduces the first n block partials (double accumulation, index order) and applies the clip /
+ * skip / scaler update above. */
 int sdmi_clip_finalize(const float* partial, int n, float max_norm, float* state, int growth_interval,
                        int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
 /* ema_alpha: the fp32 value of (1 - ema_decay) as the caller computes it (the reference passes alpha = 1 - 0.9999
@@ -407,10 +425,6 @@ int sdmi_modulate_bwd(const float* x, const float* dy, const float* s, int ls, f
 int sdmi_attn_map(const float* q, int ldq, const float* k, int ldk, int B, int H, int N, int S, int d, float scaling,
                   int average, float* out, sdmi_stream_t stream);
 
-/* Streams restricted to a share of the CUs (hipExtStreamCreateWithCUMask): keep_num of every keep_den CUs.
- * Used for the engine's weight-gradient side stream (SDMI_SIDE_CU=num/den), no reference counterpart. */
-int sdmi_stream_create_cu_share(int keep_num, int keep_den, sdmi_stream_t* out);
-int sdmi_stream_destroy(sdmi_stream_t s);
 
 /* ---------------------------------------------------------------------------------------------
  * Launch plans (host side of a training / sampling step, no reference counterpart: the reference issues every

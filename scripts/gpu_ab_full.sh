@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of the whole tree (python + libsdmi.so) against the copy in ab_old/ (a previous commit's package and
 # bench.py, library prebuilt): the GPU suite first, then the headline bench alternating old / new; AB_ENV_NEW adds env
-# settings to extra "new" arms, e.g. AB_ENV_NEW="SDMI_SHADOW=1".
+# settings to extra "new" arms, e.g. AB_ENV_NEW="SDMI_GRAD_WIRE=bf16".
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 if [ "${AB_TESTS:-1}" = 1 ]; then

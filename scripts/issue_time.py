@@ -66,7 +66,6 @@ def main():
             torch.cuda.synchronize()
         return 1e3 * sorted(ts)[2]
     print(f"single step from idle: eager enqueue {one(step):.2f} ms, native plan enqueue {one(plan.replay):.2f} ms")
-    os.environ["SDMI_WG_STREAM"] = "1"
     cap = CapturedTrainStep(tr, x0, text, empty, mask, B)
     for _ in range(3):
         cap.step()

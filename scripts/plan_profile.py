@@ -16,6 +16,11 @@ import bench  # noqa: E402
 from scripts.device_step import make  # noqa: E402
 
 
+# PLAN_PROFILE_ITERS="warm,iters" (default 2,10); "0,1" re-issues every launch exactly once, for rocprofv3 --pmc
+# passes whose per-dispatch counters are then each launch measured alone (scripts/gpu_pmc_isolated.sh)
+WARM, ITERS = (int(v) for v in os.environ.get("PLAN_PROFILE_ITERS", "2,10").split(","))
+
+
 def timeit(fn, iters=20):
     for _ in range(3):
         fn()
@@ -55,7 +60,7 @@ def main():
         if kind.value != 0:
             continue
         us = ctypes.c_float()
-        _lib.check(lib.sdmi_plan_time_op(plan.handle, i, 2, 10, ctypes.byref(us)), "time_op")
+        _lib.check(lib.sdmi_plan_time_op(plan.handle, i, WARM, ITERS, ctypes.byref(us)), "time_op")
         ops.append(dict(i=i, name=name.value.decode(errors="replace") if name.value else "?", grid=tuple(grid),
                         us=us.value))
     dem = subprocess.run(["c++filt"], input="\n".join(o["name"] for o in ops), capture_output=True, text=True).stdout
@@ -103,6 +108,8 @@ def main():
         aa, bb, m, nn, kk, conv, sp, tn, ph, gr = key
         print(f"  {t:8.1f} us {c:3d}x  a{aa}b{bb} {ph:>3s} M={m:6d} N={nn:5d} K={kk:6d} conv={conv} split={sp:2d} "
               f"tile={tn} grid={gr}  {fl * c / (t * 1e-6) / 1e12:6.1f} TF")
+    if os.environ.get("PLAN_PROFILE_NO_BLAS"):
+        return
     # vendor yardstick on the plain (non-conv) GEMM shapes
     print("--- hipBLASLt (torch.matmul, bf16) on the same plain shapes ---")
     seen = set()

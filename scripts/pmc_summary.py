@@ -9,7 +9,9 @@ import os
 import sys
 
 
-def load(d, counter):
+def load(d, counter, frac=1.0):
+    """per kernel name: counter values in dispatch order; frac < 1 keeps the last fraction of each kernel's dispatches
+    (isolated-plan passes, scripts/gpu_pmc_isolated.sh)"""
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     per = collections.defaultdict(list)
     for f in files:
@@ -17,8 +19,12 @@ def load(d, counter):
             if row.get("Counter_Name", counter) != counter:
                 continue
             name = row.get("Kernel_Name") or row.get("Kernel-Name") or "?"
-            per[name].append(float(row["Counter_Value"]))
-    return per
+            per[name].append((int(row.get("Dispatch_Id", 0)), float(row["Counter_Value"])))
+    out = {}
+    for k, v in per.items():
+        v = [x for _, x in sorted(v)]
+        out[k] = v[len(v) - int(round(len(v) * frac)):] if frac < 1.0 else v
+    return out
 
 
 def short(name):
@@ -28,7 +34,8 @@ def short(name):
 
 def main():
     fd, wd = sys.argv[1], sys.argv[2]
-    fetch, write = load(fd, "FETCH_SIZE"), load(wd, "WRITE_SIZE")
+    frac = float(sys.argv[sys.argv.index("--tail-frac") + 1]) if "--tail-frac" in sys.argv else 1.0
+    fetch, write = load(fd, "FETCH_SIZE", frac), load(wd, "WRITE_SIZE", frac)
     rows = []
     for k in set(fetch) | set(write):
         f = fetch.get(k, [])

@@ -5,7 +5,11 @@ reducer). From a --kernel-trace CSV (or a directory holding one): average durati
 dispatch's per-axis grid by Dispatch_Id): HBM bytes per unsplit launch (FETCH_SIZE x2, the gfx950 correction of
 MI355X_MICROARCH.md's HBM section; both counters in KiB).
 
-Usage: python scripts/roofline_evidence.py <kernel_trace.csv|dir> <fetch_dir> <write_dir> "<kernel>" [--json out]"""
+--tail-frac F keeps only the last fraction F of the kernel's dispatches in each file (the isolated-plan passes of
+scripts/gpu_pmc_isolated.sh: 3 step executions while the plan is recorded, then every launch re-issued alone once -> 0.25).
+
+Usage: python scripts/roofline_evidence.py <kernel_trace.csv|dir> <fetch_dir> <write_dir> "<kernel>" [--json out]
+       [--tail-frac F]"""
 import csv
 import glob
 import json
@@ -29,12 +33,17 @@ def _match(kernel, name):
     return kernel in name or (kernel.endswith(">") and kernel[:-1] + "," in name)
 
 
+def _tail(rows, frac):
+    return rows[len(rows) - int(round(len(rows) * frac)):] if frac < 1.0 else rows
+
+
 def main():
     trace, fdir, wdir, kernel = sys.argv[1:5]
+    frac = float(sys.argv[sys.argv.index("--tail-frac") + 1]) if "--tail-frac" in sys.argv else 1.0
     durs = []
-    for r in csv.DictReader(open(_trace_csv(trace))):
-        if not _match(kernel, r["Kernel_Name"]):
-            continue
+    rows = sorted((r for r in csv.DictReader(open(_trace_csv(trace))) if _match(kernel, r["Kernel_Name"])),
+                  key=lambda r: int(r["Dispatch_Id"]))
+    for r in _tail(rows, frac):
         if int(r["Grid_Size_Z"]) == 1:
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = {"kernel": kernel, "trace_unsplit_launches": len(durs),
@@ -43,8 +52,11 @@ def main():
         vals = []
         gz = _grid_z(d)
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-            for r in csv.DictReader(open(f)):
-                if r["Counter_Name"] == cname and _match(kernel, r["Kernel_Name"]) and gz.get(r["Dispatch_Id"]) == 1:
+            rows = sorted((r for r in csv.DictReader(open(f))
+                           if r["Counter_Name"] == cname and _match(kernel, r["Kernel_Name"])),
+                          key=lambda r: int(r["Dispatch_Id"]))
+            for r in _tail(rows, frac):
+                if gz.get(r["Dispatch_Id"]) == 1:
                     vals.append(float(r["Counter_Value"]) * 1024 * mul)
         out[cname.lower() + "_bytes_per_launch"] = sum(vals) / len(vals) if vals else None
         out[cname.lower() + "_launches"] = len(vals)

@@ -13,7 +13,6 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "stablediffusion-pytorch_amd"), REPO]
-os.environ["SDMI_WG_STREAM"] = "0"  # single stream (no side-stream optimizer chunks) for isolated timing
 import torch  # noqa: E402
 
 import bench  # noqa: E402
@@ -57,18 +56,19 @@ def main():
         for v in sd.values():
             if v.abs().max() == 0:
                 v.normal_(0, 0.02)
-        tr = DDPMTrainer(cfg, sd, dev, base="dit", lr=1e-4, ema_decay=None)
+        tr = DDPMTrainer(cfg, sd, dev, base="dit", lr=1e-4, ema_decay=None, single_stream=True)
         text = None
     elif args.workload == "uncond-unet":  # config/celebhq.yaml (bench.py --workload uncond-unet)
         import models.unet_base as mu
         cfg = bench.uncond_config()
         torch.manual_seed(0)
-        tr = DDPMTrainer(cfg, mu.Unet(4, cfg).state_dict(), dev, base="uncond", sched=(1000, 0.0015, 0.0195))
+        tr = DDPMTrainer(cfg, mu.Unet(4, cfg).state_dict(), dev, base="uncond", sched=(1000, 0.0015, 0.0195),
+                         single_stream=True)
         text = None
     else:
         cfg = bench.cond_config()
         torch.manual_seed(0)
-        tr = DDPMTrainer(cfg, mc.Unet(4, cfg).state_dict(), dev)
+        tr = DDPMTrainer(cfg, mc.Unet(4, cfg).state_dict(), dev, single_stream=True)
     x0, text_, empty, mask = bench.synthetic_batch(B, dev, 1)
     if args.workload == "uncond-unet":
         mask = None

@@ -190,29 +190,8 @@ using Ragged = std::true_type;
 // ONES (d % 16 == 8: the last output tile has free padded columns): column d of every valid V row is 1, so the
 // PV MFMA accumulates the softmax row sum into o[g][DT-1] (tile row 8: lane group 2, element 0) -- no per-score
 // VALU row-sum adds in the loop; the sum is of the bf16 P the MFMA consumes, i.e. exactly what O accumulated
-// LAZY (SDMI_ATTN_LAZY): no per-score scale / max subtraction on the VALU. The lane-resident q fragments are
-// pre-scaled by c = scale * log2(e) once, as a hi + lo bf16 pair (q c = hi + lo to ~2^-16 relative, so the scores keep
-// fp32-class accuracy for one extra MFMA per key block; the MFMA pipe is ~20 % busy here), and every score accumulator
-// starts at -m_ref, the lane's reference maximum: the MFMAs deliver s c - m_ref and P = exp2(acc) directly. m_ref only
-// moves (with the O / row-sum rescale) on the first key tile and when a tile's maximum exceeds it by more than
-// LAZY_TH (wave-uniform branch), so P <= 2^LAZY_TH; O / l and lse = m_ref + log2(l) are exact whatever m_ref is.
-constexpr float LAZY_TH = 8.f;
-
-__device__ __forceinline__ void split_scaled(const s16x8& q, float c, s16x8& hi, s16x8& lo) {
-  float x[8], h[8], l[8];
-  unpack8(__builtin_bit_cast(uint4, q), x);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float v = x[e] * c;
-    h[e] = bf2f(f2bf(v));
-    l[e] = v - h[e];
-  }
-  hi = __builtin_bit_cast(s16x8, pack8(h));
-  lo = __builtin_bit_cast(s16x8, pack8(l));
-}
-
-template <int DT, bool ONES, int OCC = 2, bool LAZY = false>
-__global__ __launch_bounds__(NT, OCC) void attn_fwd_kernel(AttnArgs a) {
+template <int DT, bool ONES>
+__global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -230,19 +209,11 @@ __global__ __launch_bounds__(NT, OCC) void attn_fwd_kernel(AttnArgs a) {
   for (int g = 0; g < 2; ++g) {
     myq[g] = blockIdx.x * ROWS + wave * 32 + g * 16 + (lane & 15);
     row_frags<DP>(qf[g], Q, a.ldq, myq[g], a.N, h * a.d, a.d, lane);
-    m[g] = LAZY ? 0.f : -INFINITY;
+    m[g] = -INFINITY;
     l[g] = 0.f;
 #pragma unroll
     for (int t = 0; t < DT; ++t) o[g][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  s16x8 qlo[2][KS];  // LAZY: qf becomes the hi part of q * c, qlo the lo part
-  if constexpr (LAZY) {
-#pragma unroll
-    for (int g = 0; g < 2; ++g)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) split_scaled(qf[g][ks], c, qf[g][ks], qlo[g][ks]);
-  }
-
   uint4 rk[Tile<DP>::CPT], rv[Tile<DP>::CPT];
   // ONES: the 8-column chunk of V starting at column d (all padding) becomes {1, 0, ..., 0} on valid key rows
   auto fetch_v = [&](int row0) __attribute__((always_inline)) {
@@ -273,21 +244,12 @@ __global__ __launch_bounds__(NT, OCC) void attn_fwd_kernel(AttnArgs a) {
     f32x4 s[2][4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      if constexpr (LAZY) {
-        s[0][kb] = (f32x4){-m[0], -m[0], -m[0], -m[0]};
-        s[1][kb] = (f32x4){-m[1], -m[1], -m[1], -m[1]};
-      } else {
-        s[0][kb] = s[1][kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      }
+      s[0][kb] = s[1][kb] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         s16x8 kf = frag_rows<DP>(sK, kb * 16, ks * 32, lane);
         s[0][kb] = mfma(kf, qf[0][ks], s[0][kb]);
         s[1][kb] = mfma(kf, qf[1][ks], s[1][kb]);
-        if constexpr (LAZY) {
-          s[0][kb] = mfma(kf, qlo[0][ks], s[0][kb]);
-          s[1][kb] = mfma(kf, qlo[1][ks], s[1][kb]);
-        }
       }
     }
     if constexpr (decltype(rag)::value) {  // last key tile of a ragged S (cross-attention S = 77): keys >= S out
@@ -306,38 +268,6 @@ __global__ __launch_bounds__(NT, OCC) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int j = 5; j < 16; j += 2) mx = fmaxf(fmaxf(mx, s[g][j >> 2][j & 3]), s[g][(j + 1) >> 2][(j + 1) & 3]);
       mx = xmax4(mx);
-      if constexpr (LAZY) {
-        // mx = this tile's max of s c - m_ref per query; rebase (wave-uniform) on the first tile or past LAZY_TH
-        if (k0 == 0 || __any(mx > LAZY_TH)) {
-          const float sh = k0 == 0 ? mx : fmaxf(mx, 0.f);
-          const float alpha = fast_exp2(-sh);
-          m[g] += sh;
-#pragma unroll
-          for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s[g][kb][i] = fast_exp2(s[g][kb][i] - sh);
-          if constexpr (!ONES) l[g] *= alpha;
-#pragma unroll
-          for (int t = 0; t < DT; ++t) scale4(o[g][t], alpha);
-        } else {
-#pragma unroll
-          for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s[g][kb][i] = fast_exp2(s[g][kb][i]);
-        }
-        if constexpr (!ONES) {
-          float ls0 = 0.f, ls1 = 0.f;
-#pragma unroll
-          for (int kb = 0; kb < 4; ++kb) {
-            ls0 += s[g][kb][0] + s[g][kb][1];
-            ls1 += s[g][kb][2] + s[g][kb][3];
-          }
-          l[g] += ls0 + ls1;
-        }
-        pf[g][0] = pack_acc(s[g][0], s[g][1]);
-        pf[g][1] = pack_acc(s[g][2], s[g][3]);
-        continue;
-      }
       const float mn = fmaxf(m[g], mx * c);
       const float alpha = fast_exp2(m[g] - mn);
       m[g] = mn;
@@ -403,10 +333,8 @@ __global__ __launch_bounds__(NT, OCC) void attn_fwd_kernel(AttnArgs a) {
 // =============================================================================================
 // G: 16-key groups per wave (2: 128 keys per workgroup; 4: 256, every staged Q / dO tile and LDS fragment serves twice
 // the keys). The query tile is consumed in two 32-query halves so the live P / dS accumulators stay at G x 2.
-// PS (SDMI_ATTN_LAZY & 2): the lane-resident operand of the score product (K here, Q in the dQ kernel) is pre-scaled by
-// c as a hi + lo bf16 pair and the score accumulators start at -lse, so P = exp2(acc) with no per-score FMA
-template <int DT, int OCC = 2, int G = 2, bool PS = false>
-__global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
+template <int DT, int G = 2>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][Q|dO]
   __shared__ __attribute__((aligned(16))) float sLD[2][2][64];               // [buf][-lse|-delta]
@@ -417,17 +345,13 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
   const bf16_t* dO = a.dout + (long long)b * a.N * a.lddo;
 
   int mykey[G];
-  s16x8 kf[G][KS], vf[G][KS], klo[G][KS];
+  s16x8 kf[G][KS], vf[G][KS];
   f32x4 dk[G][DT], dv[G][DT];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     mykey[g] = blockIdx.x * (64 * G) + wave * 16 * G + g * 16 + (lane & 15);
     row_frags<DP>(kf[g], a.k + (long long)b * a.S * a.ldk, a.ldk, mykey[g], a.S, h * a.d, a.d, lane);
     row_frags<DP>(vf[g], a.v + (long long)b * a.S * a.ldv, a.ldv, mykey[g], a.S, h * a.d, a.d, lane);
-    if constexpr (PS) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) split_scaled(kf[g][ks], c, kf[g][ks], klo[g][ks]);
-    }
 #pragma unroll
     for (int t = 0; t < DT; ++t) dk[g][t] = dv[g][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
@@ -471,7 +395,7 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
         // dP accumulates on top of -delta: the MFMA yields dP - delta directly (no per-element subtraction)
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-          p[g][h2] = PS ? nL : (f32x4){0.f, 0.f, 0.f, 0.f};
+          p[g][h2] = (f32x4){0.f, 0.f, 0.f, 0.f};
           ds[g][h2] = nD;
         }
 #pragma unroll
@@ -480,27 +404,12 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
           s16x8 oa = frag_rows<DP>(sO, qb * 16, ks * 32, lane);
 #pragma unroll
           for (int g = 0; g < G; ++g) p[g][h2] = mfma(qa, kf[g][ks], p[g][h2]);
-          if constexpr (PS) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) p[g][h2] = mfma(qa, klo[g][ks], p[g][h2]);
-          }
 #pragma unroll
           for (int g = 0; g < G; ++g) ds[g][h2] = mfma(oa, vf[g][ks], ds[g][h2]);
         }
         const float nl[4] = {nL[0], nL[1], nL[2], nL[3]};
-        if constexpr (PS) {
 #pragma unroll
-          for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float e = fast_exp2(p[g][h2][i]);
-              p[g][h2][i] = e;
-              ds[g][h2][i] = e * ds[g][h2][i];
-            }
-        } else {
-#pragma unroll
-          for (int g = 0; g < G; ++g) p_ds(p[g][h2], ds[g][h2], c, nl);
-        }
+        for (int g = 0; g < G; ++g) p_ds(p[g][h2], ds[g][h2], c, nl);
       }
       s16x8 pf[G], df[G];
 #pragma unroll
@@ -541,8 +450,8 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dkv_kernel(AttnArgs a) {
 // =============================================================================================
 // backward: dQ (queries on lanes, 64 * G queries per workgroup, key tiles streamed)
 // =============================================================================================
-template <int DT, int OCC = 2, int G = 2, bool PS = false>
-__global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
+template <int DT, int G = 2>
+__global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -584,14 +493,6 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < DT; ++t) dq[g][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  s16x8 qlo[G][KS];  // PS: qf becomes the hi part of q * c, qlo the lo part (after delta used the unscaled rows)
-  if constexpr (PS) {
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) split_scaled(qf[g][ks], c, qf[g][ks], qlo[g][ks]);
-  }
-
   uint4 rk[Tile<DP>::CPT], rv[Tile<DP>::CPT];
   tile_fetch<DP>(rk, K, a.ldk, 0, a.S, h * a.d, a.d);
   tile_fetch<DP>(rv, V, a.ldv, 0, a.S, h * a.d, a.d);
@@ -617,7 +518,7 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
         // dP accumulates on top of -delta (per query = per lane): the MFMA yields dP - delta directly
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-          sc[g] = PS ? (f32x4){nlse[g], nlse[g], nlse[g], nlse[g]} : (f32x4){0.f, 0.f, 0.f, 0.f};
+          sc[g] = (f32x4){0.f, 0.f, 0.f, 0.f};
           dp[g] = (f32x4){ndlt[g], ndlt[g], ndlt[g], ndlt[g]};
         }
 #pragma unroll
@@ -626,10 +527,6 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
           s16x8 va = frag_rows<DP>(sV, kb * 16, ks * 32, lane);
 #pragma unroll
           for (int g = 0; g < G; ++g) sc[g] = mfma(ka, qf[g][ks], sc[g]);
-          if constexpr (PS) {
-#pragma unroll
-            for (int g = 0; g < G; ++g) sc[g] = mfma(ka, qlo[g][ks], sc[g]);
-          }
 #pragma unroll
           for (int g = 0; g < G; ++g) dp[g] = mfma(va, of[g][ks], dp[g]);
         }
@@ -637,7 +534,7 @@ __global__ __launch_bounds__(NT, OCC) void attn_bwd_dq_kernel(AttnArgs a) {
         for (int g = 0; g < G; ++g) {
           float e[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) e[i] = PS ? fast_exp2(sc[g][i]) : fast_exp2(fmaf(sc[g][i], c, nlse[g]));
+          for (int i = 0; i < 4; ++i) e[i] = fast_exp2(fmaf(sc[g][i], c, nlse[g]));
           if constexpr (decltype(rag)::value) {  // keys >= S of the last ragged tile contribute nothing
             const int lim = a.S - k0 - kb * 16 - (lane >> 4) * 4;
 #pragma unroll
@@ -925,31 +822,6 @@ __global__ __launch_bounds__(NT) void attn_delta_kernel(AttnArgs a) {
 constexpr int ATTN_CTR_SLOTS = 4, ATTN_CTR_SLOT = 1 << 16;
 __device__ unsigned g_attn_counters[ATTN_CTR_SLOTS * ATTN_CTR_SLOT];
 
-// workgroups per CU the kernel is register-budgeted for (__launch_bounds__ minimum): kind 0 forward, 1 dQ, 2 dK/dV;
-// head dims <= 32 only (DT <= 2: the larger tiles spill at 3 / 4). SDMI_ATTN_OCC_FWD / _DQ / _DKV override (A/B
-// runs); default 2 (the round-2 measured setting)
-int attn_occ(int kind, int d) {
-  static int v[3] = {-1, -1, -1};
-  if (v[kind] < 0) {
-    const char* names[3] = {"SDMI_ATTN_OCC_FWD", "SDMI_ATTN_OCC_DQ", "SDMI_ATTN_OCC_DKV"};
-    const char* e = getenv(names[kind]);
-    v[kind] = e ? atoi(e) : 2;
-  }
-  (void)d;
-  return v[kind];
-}
-
-// SDMI_ATTN_LAZY bits: 1 = forward with the MFMA-side scale / max offset and lazy rebase (attn_fwd_kernel LAZY),
-// 2 = dQ / dK,dV kernels with the pre-scaled resident operand and -lse accumulator start (PS)
-int attn_lazy() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SDMI_ATTN_LAZY");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
 int check_args(const AttnArgs& a) {
   if (a.B <= 0 || a.H <= 0 || a.N <= 0 || a.S <= 0 || a.d <= 0) return -1;
   if (a.d % 8 || a.d > 64) return -2;
@@ -968,26 +840,11 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
   if (rc) return rc;
   dim3 grid((N + ROWS - 1) / ROWS, B * H);
   hipStream_t s = (hipStream_t)stream;
-  static int ones_ok = -1;  // SDMI_ATTN_ONES=0: VALU row sums for every head dim (A/B runs)
-  if (ones_ok < 0) {
-    const char* e = getenv("SDMI_ATTN_ONES");
-    ones_ok = e ? atoi(e) != 0 : 1;
-  }
-  const bool ones = ones_ok && d % 16 == 8;
-  const int occ = attn_occ(0, d);
-  const bool lazy = attn_lazy() & 1;
-#define SDMI_ATTN_FWD_OCC(DT, O)                                                                        \
-  if (lazy) {                                                                                           \
-    if (ones) sdmi_rt::launch(attn_fwd_kernel<DT, true, O, true>, grid, dim3(NT), 0, s, a);            \
-    else sdmi_rt::launch(attn_fwd_kernel<DT, false, O, true>, grid, dim3(NT), 0, s, a);                \
-  } else if (ones) sdmi_rt::launch(attn_fwd_kernel<DT, true, O>, grid, dim3(NT), 0, s, a);             \
-  else sdmi_rt::launch(attn_fwd_kernel<DT, false, O>, grid, dim3(NT), 0, s, a);
-#define SDMI_ATTN_FWD(DT)                                                \
-  if constexpr (DT <= 2) {                                               \
-    if (occ >= 4) { SDMI_ATTN_FWD_OCC(DT, 4) }                           \
-    else if (occ == 3) { SDMI_ATTN_FWD_OCC(DT, 3) }                      \
-    else { SDMI_ATTN_FWD_OCC(DT, 2) }                                    \
-  } else { SDMI_ATTN_FWD_OCC(DT, 2) }
+  // ONES: the softmax row sum through the PV MFMA where the padded head dim leaves a free column (d % 16 == 8)
+  const bool ones = d % 16 == 8;
+#define SDMI_ATTN_FWD(DT)                                                           \
+  if (ones) sdmi_rt::launch(attn_fwd_kernel<DT, true>, grid, dim3(NT), 0, s, a);    \
+  else sdmi_rt::launch(attn_fwd_kernel<DT, false>, grid, dim3(NT), 0, s, a);
   switch ((d + 15) / 16) {
     case 1: SDMI_ATTN_FWD(1) break;
     case 2: SDMI_ATTN_FWD(2) break;
@@ -995,7 +852,6 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
     default: SDMI_ATTN_FWD(4) break;
   }
 #undef SDMI_ATTN_FWD
-#undef SDMI_ATTN_FWD_OCC
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -1016,49 +872,25 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
   // the dQ kernel also produces delta = rowsum(dO * O) (written to delta_ws) for the dK/dV kernel after it.
   // 16-row groups per wave of both kernels (head dims <= 32): 4 (256 rows per workgroup) when N, S <= 256 -- measured
   // at B = 32, 16 heads: 16^2 d = 24 56.7 -> 48.6 us, d = 32 49.0 -> 44.2 us -- else 2 (128 rows; at 32^2 the two
-  // forms measured equal: 279 / 291 / 352 vs 270 / 292 / 348 us at d = 8 / 16 / 24). SDMI_ATTN_G=2 / 4 forces one.
-  static int G = -1;
-  if (G < 0) {
-    const char* e = getenv("SDMI_ATTN_G");
-    G = e ? atoi(e) : 0;
-  }
+  // forms measured equal: 279 / 291 / 352 vs 270 / 292 / 348 us at d = 8 / 16 / 24)
   // (and only while the 256-row grids keep >= 512 workgroups, two per CU: DiT-12L's 9-head 16^2 attention, 288
   // workgroups, measured 3.90 / 3.91 -> 3.92 / 3.92 ms per step with G = 4)
   const long long wg4 = (long long)B * H * ((std::min(N, S) + 255) / 256);
-  const int g4 = d <= 32 && (G == 4 || (G != 2 && N <= 256 && S <= 256 && wg4 >= 512));
+  const int g4 = d <= 32 && N <= 256 && S <= 256 && wg4 >= 512;
   const int rows = g4 ? 256 : ROWS;
   dim3 gk((S + rows - 1) / rows, B * H), gq((N + rows - 1) / rows, B * H);
-  const int oq = attn_occ(1, d), ok = attn_occ(2, d);
-  const bool ps = attn_lazy() & 2;
   switch ((d + 15) / 16) {
-#define SDMI_ATTN_BWD(DT)                                                                                  \
-  case DT:                                                                                                 \
-    if (ps) {                                                                                              \
-      if constexpr (DT <= 2) {                                                                             \
-        if (g4) {                                                                                          \
-          sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2, 4, true>, gq, dim3(NT), 0, s, a);                      \
-          sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2, 4, true>, gk, dim3(NT), 0, s, a);                     \
-          break;                                                                                           \
-        }                                                                                                  \
-      }                                                                                                    \
-      sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2, 2, true>, gq, dim3(NT), 0, s, a);                          \
-      sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2, 2, true>, gk, dim3(NT), 0, s, a);                         \
-      break;                                                                                               \
-    }                                                                                                      \
-    if constexpr (DT <= 2) {                                                                               \
-      if (g4) {                                                                                            \
-        sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2, 4>, gq, dim3(NT), 0, s, a);                              \
-        sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2, 4>, gk, dim3(NT), 0, s, a);                             \
-        break;                                                                                             \
-      }                                                                                                    \
-      if (oq >= 3) sdmi_rt::launch(attn_bwd_dq_kernel<DT, 3>, gq, dim3(NT), 0, s, a);                     \
-      else sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2>, gq, dim3(NT), 0, s, a);                              \
-      if (ok >= 3) sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 3>, gk, dim3(NT), 0, s, a);                    \
-      else sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2>, gk, dim3(NT), 0, s, a);                             \
-    } else {                                                                                               \
-      sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2>, gq, dim3(NT), 0, s, a);                                   \
-      sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2>, gk, dim3(NT), 0, s, a);                                  \
-    }                                                                                                      \
+#define SDMI_ATTN_BWD(DT)                                                               \
+  case DT:                                                                              \
+    if constexpr (DT <= 2) {                                                            \
+      if (g4) {                                                                         \
+        sdmi_rt::launch(attn_bwd_dq_kernel<DT, 4>, gq, dim3(NT), 0, s, a);              \
+        sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 4>, gk, dim3(NT), 0, s, a);             \
+        break;                                                                          \
+      }                                                                                 \
+    }                                                                                   \
+    sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2>, gq, dim3(NT), 0, s, a);                  \
+    sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2>, gk, dim3(NT), 0, s, a);                 \
     break;
     SDMI_ATTN_BWD(1)
     SDMI_ATTN_BWD(2)

@@ -38,7 +38,7 @@ struct LnFwdArgs {
   const bf16_t* shift; const bf16_t* scale; int ld_mod;
   bf16_t* y; int ldy;
   float* mean; float* rstd;
-  int rpw;  // rows per wave (SDMI_LN_FWD_RPW, default RPW)
+  int rpw;  // rows per wave (RPW)
   int rows, C, N;
   float eps;
 };
@@ -326,15 +326,9 @@ bool vec_ok(const void* p, int ld) { return p == nullptr || ((uintptr_t)p % 16 =
 
 // token rows per backward workgroup (= per shift/scale/gate partial chunk): the largest power of two <= the cap
 // dividing N. Each wave walks its rows serially (two dependent load round trips per row), so a smaller cap buys
-// workgroups: SDMI_LN_ROWS (default 8: 32 -> 8 measured -0.16 ms per DiT-12L step) for A/B runs.
+// workgroups: cap 8 (32 -> 8 measured -0.16 ms per DiT-12L step).
 extern "C" int sdmi_ln_chunk_rows(int N) {
-  static int cap = -1;
-  if (cap < 0) {
-    const char* e = getenv("SDMI_LN_ROWS");
-    cap = e ? atoi(e) : 8;
-    if (cap < 1 || cap > 32) cap = 8;
-  }
-  for (int r = cap; r > 1; r >>= 1)
+  for (int r = 8; r > 1; r >>= 1)
     if (N % r == 0) return r;
   return 1;
 }
@@ -352,14 +346,8 @@ extern "C" int sdmi_ln_mod_fwd(const void* x, int ldx, const void* v, int ldv, c
   a.xo = xo; a.ldxo = ldxo; a.shift = (const bf16_t*)shift; a.scale = (const bf16_t*)scale;
   a.ld_mod = ld_mod; a.y = (bf16_t*)y; a.ldy = ldy; a.mean = mean; a.rstd = rstd;
   a.rows = rows; a.C = C; a.N = N; a.eps = eps;
-  static int rpw = -1;
-  if (rpw < 0) {
-    const char* e = getenv("SDMI_LN_FWD_RPW");
-    rpw = e ? atoi(e) : RPW;
-    if (rpw < 1 || rpw > 64) rpw = RPW;
-  }
-  a.rpw = rpw;
-  const int per = WAVES * rpw;
+  a.rpw = RPW;
+  const int per = WAVES * RPW;
   if (x_f32)
     sdmi_rt::launch(ln_mod_fwd_kernel<true>, dim3((rows + per - 1) / per), dim3(NT), 0, (hipStream_t)stream, a);
   else

@@ -99,7 +99,6 @@ struct EpiArgs {
   int raw;  // 1: write raw fp32 partials (split-K) to ws, epilogue applied by the reducer
   int nsplit;
   const float* ws;  // split-K slabs [nsplit][M][N]
-  unsigned* counters;  // per-tile arrival counters: the last split of a tile reduces it (0: separate reducer)
   int vec;          // LDS-staged 16-B row stores (no column permute, 8-aligned columns/strides)
   int n8;           // N % 8 == 0: split-K slabs are written / read as 16-B rows even when !vec
   int rb_mod;       // rowbias row = (row / rb_div) % rb_mod when > 0 (per-token tables, e.g. position embedding)
@@ -112,12 +111,16 @@ struct EpiArgs {
   bf16_t* gsum;
   int n_gemm;  // columns the MFMA tiles produce (N, or N plus the synthesised reduction columns); with split-K the
                // slab row width N is n_gemm + 8 when the VALU row sums ride along in slab column n_x0 = n_gemm
-  // grouped launch: problem p stores to Cg[p] / sum_g[p], its split-K slabs start p * ws_gstride floats into ws and
-  // its arrival counters p * tiles after counters
+  // grouped launch: problem p stores to Cg[p] / sum_g[p], its split-K slabs start p * ws_gstride floats into ws
   void* Cg[SDMI_GEMM_GROUP_MAX];
   float* sum_g[SDMI_GEMM_GROUP_MAX];
   long long ws_gstride;
-  int ctr_gstride;
+  // GroupNorm-backward statistics (sdmi_gemm_desc::gn_part): per gn_rb-row segment and column, sum dz and dz*xhat
+  const bf16_t* gn_x; int gn_ldx;
+  const float4* gn_tab;
+  float* gn_part;
+  int gn_rb, gn_silu;
+  FastDiv gn_pd;  // rows per sample
 };
 
 // the epilogue arguments of problem p of a grouped launch (C / sum read from the kernel-argument segment)
@@ -125,7 +128,6 @@ __device__ __forceinline__ void group_epi(EpiArgs& e, void* C, float* sum, int p
   e.C = C;
   e.sum_out = sum;
   e.ws += (long long)p * e.ws_gstride;
-  if (e.counters) e.counters += (long long)p * e.ctr_gstride;
 }
 
 __device__ __forceinline__ long long rb_row(const EpiArgs& g, int row) {
@@ -281,6 +283,79 @@ struct Epi {
   }
 };
 
+// dz and dz * xhat of one 8-column chunk of one output row (GroupNorm backward, EpiArgs::gn_part): v = the stored bf16
+// dy values, x the GroupNorm input there, tb the forward table {a, s, mean, rstd} of the chunk's columns
+__device__ __forceinline__ void gn_accum(const EpiArgs& e, const float* v, const uint4 xr, const float4* tb, float* u,
+                                         float* w) {
+  float xv[8];
+  unpack8(xr, xv);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float dz = v[q];
+    if (e.gn_silu) dz *= silu_grad_f(fmaf(xv[q], tb[q].x, tb[q].y));
+    u[q] += dz;
+    w[q] = fmaf(dz, (xv[q] - tb[q].z) * tb[q].w, w[q]);
+  }
+}
+
+// The GroupNorm-backward statistics epilogue of one staged 64-row half (m0h = its first row): thread t owns column
+// chunk t % CH of rows t / CH + R k (R = NTH / CH row lanes); per gn_rb-row segment it stores bf16(alpha acc) with
+// 16-B stores, accumulates dz / dz * xhat over its rows, and the R row lanes are summed in a fixed order through LDS
+// (red: R x TBN x 2 floats) into the segment's column partials -- deterministic, no atomics.
+template <int TBN, int NTH>
+__device__ __forceinline__ void epi_gn_half(const EpiArgs& e, const float* st, float* red, int m0h, int n0) {
+  constexpr int SROW = TBN + 4, CH = TBN / 8, R = NTH / CH;
+  const int t = threadIdx.x, c8 = t % CH, rl0 = t / CH;
+  const int col = n0 + c8 * 8;
+  const bool on = rl0 < R && col < e.N;
+#pragma unroll 1
+  for (int s0 = 0; s0 < 64 && m0h + s0 < e.M; s0 += e.gn_rb) {
+    float u[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, w[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (on) {
+      const int b = (int)e.gn_pd.div((unsigned)(m0h + s0));  // a segment lies inside one sample (gn_rb | gn_P)
+      float4 tb[8];
+      const float4* tp = e.gn_tab + (long long)b * e.N + col;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) tb[q] = tp[q];
+#pragma unroll 1
+      for (int rl = s0 + rl0; rl < s0 + e.gn_rb; rl += R) {
+        const int row = m0h + rl;
+        if (row >= e.M) break;
+        const float4 lo = *(const float4*)(st + rl * SROW + c8 * 8), hi = *(const float4*)(st + rl * SROW + c8 * 8 + 4);
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const uint4 xr = *(const uint4*)(e.gn_x + (long long)row * e.gn_ldx + col);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] *= e.alpha;
+        const uint4 pk = pack8(v);
+        *(uint4*)((bf16_t*)e.C + (long long)row * e.ldc + col) = pk;
+        unpack8(pk, v);  // the statistics are of the stored bf16 dy, as the apply pass reads it
+        gn_accum(e, v, xr, tb, u, w);
+      }
+    }
+    if (rl0 < R) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        red[(rl0 * TBN + c8 * 8 + q) * 2] = u[q];
+        red[(rl0 * TBN + c8 * 8 + q) * 2 + 1] = w[q];
+      }
+    }
+    __syncthreads();
+    const long long seg = (m0h + s0) / e.gn_rb;
+#pragma unroll 1
+    for (int j = t; j < TBN; j += NTH) {
+      if (n0 + j >= e.N) continue;
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll 1
+      for (int r = 0; r < R; ++r) {
+        a1 += red[(r * TBN + j) * 2];
+        a2 += red[(r * TBN + j) * 2 + 1];
+      }
+      *(float2*)(e.gn_part + (seg * e.N + n0 + j) * 2) = make_float2(a1, a2);
+    }
+    __syncthreads();
+  }
+}
+
 // Shared epilogue of the GEMM kernels: acc = this wave's 64 x (NJ*16) sub-tile (4 x NJ MFMA tiles) at (wm, wn) of a
 // TBM x TBN workgroup tile computed by NT threads; smem >= 64 x (TBN + 4) fp32 of LDS that no wave reads any more (the
 // caller synchronises before).
@@ -307,6 +382,10 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
       }
     }
     __syncthreads();
+    if (e.gn_part && !e.raw) {  // GroupNorm-backward statistics path (plain epilogue, checked on the host)
+      epi_gn_half<TBN, NTH>(e, st, st + 64 * SROW, m0 + half * 64, n0);
+      continue;
+    }
 #pragma unroll 1
     for (int it = 0; it < 64 * TBN / 8 / NTH; ++it) {  // 64 rows x TBN/8 chunks of 8 columns
       const int ch = threadIdx.x + it * NTH;
@@ -386,70 +465,6 @@ __device__ __forceinline__ TileId tile_id() {
   t.m0 = mt * TBM;
   t.n0 = (t.tile - mt * gx) * TBN;
   return t;
-}
-
-// Split-K without a second launch: every split of a tile publishes its slab and bumps the tile's
-// arrival counter; the split that arrives last sums the slabs in fixed z order (deterministic) and
-// applies the epilogue, then re-arms the counter for the next launch (graph replays included).
-template <int TBN = BN, int TBM = BM, int NTH = NT>
-__device__ __forceinline__ void splitk_tail(const EpiArgs& e, char* smem, int m0, int n0, int tile) {
-  // Slabs were written with device-coherent (sc1) stores, so no L2 write-back fence is needed: wait
-  // for this block's stores to complete, then count the arrival with a relaxed device-scope atomic.
-  int* flag = (int*)smem;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned* ctr = e.counters + tile;
-    const unsigned prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == (unsigned)(e.nsplit - 1);
-    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  // acquire at agent scope before reading the other splits' slabs (they may sit in another XCD's L2 history)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)e.ws, (short)0, 0x7fffffff, 0x00020000);
-  const int zstride = (int)(e.split_stride * 4);
-  if (e.n8) {
-    // TBM x TBN/8 chunks of 8 columns; 4 splits (8 loads) in flight per thread
-#pragma unroll 1
-    for (int ch = threadIdx.x; ch < TBM * (TBN / 8); ch += NTH) {
-      const int rl = ch / (TBN / 8);
-      const int row = m0 + rl, col = n0 + (ch - rl * (TBN / 8)) * 8;
-      const bool xcol = e.n_x0 && col >= e.n_x0;
-      if (!xcol && (e.vec ? (row >= e.m_store || col >= e.n_store) : (row >= e.M || col >= e.N))) continue;
-      if (xcol && row >= e.M) continue;
-      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const int off = (row * e.N + col) * 4;
-#pragma unroll 4
-      for (int zz = 0; zz < e.nsplit; ++zz) {  // sc1 loads: read past a stale local L2
-        const int o = off + zz * zstride;
-        const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, o, 0, CPOL_SC1));
-        const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, o + 16, 0, CPOL_SC1));
-        v[0] += a[0]; v[1] += a[1]; v[2] += a[2]; v[3] += a[3]; v[4] += b[0]; v[5] += b[1]; v[6] += b[2]; v[7] += b[3];
-      }
-      if (xcol) {
-        Epi::extra(e, row, col, v, 8);
-      } else if (e.vec) {
-        Epi::finish8(e, row, col, v);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) Epi::store_final(e, row, col + q, v[q]);
-      }
-    }
-    return;
-  }
-#pragma unroll 1
-  for (int idx = threadIdx.x; idx < TBM * TBN; idx += NTH) {
-    const int row = m0 + idx / TBN, col = n0 + idx % TBN;
-    if (row >= e.M || col >= e.N) continue;
-    float acc = 0.f;
-    int off = (row * e.N + col) * 4;
-    for (int zz = 0; zz < e.nsplit; ++zz, off += zstride)
-      acc += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, off, 0, CPOL_SC1));
-    Epi::store_final(e, row, col, acc);
-  }
 }
 
 // RED (col-major A only): 0 plain GEMM, 1 + VALU row sums of A (bias gradient), 2 + synthesised reduction columns
@@ -712,7 +727,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
   }
 
   gemm_epilogue<BN, RED == 2>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
-  if (ep->raw && ep->counters) splitk_tail(*ep, smem, m0, n0, tl.tile);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1172,7 +1186,6 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
     }
   }
   gemm_epilogue<TBN, false, TBM, NJ, NTH>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
-  if (ep->raw && ep->counters) splitk_tail<TBN, TBM, NTH>(*ep, smem, m0, n0, tl.tile);
 }
 
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
@@ -1233,6 +1246,61 @@ __global__ __launch_bounds__(256) void splitk_reduce_n8_kernel(const EpiArgs g0)
   }
 }
 
+// Sum split-K slabs, store bf16(alpha * sum) and the GroupNorm-backward statistics (EpiArgs::gn_part): grid
+// (ceil(N / 256), M / gn_rb); 256 threads = 32 column chunks x 8 row lanes, the row lanes summed in LDS in a fixed
+// order into the segment's column partials (same arithmetic as epi_gn_half).
+__global__ __launch_bounds__(256) void splitk_reduce_gn_kernel(const EpiArgs e) {
+  __shared__ float red[8][256][2];
+  const int t = threadIdx.x, c8 = t & 31, rl0 = t >> 5;
+  const int col = blockIdx.x * 256 + c8 * 8;
+  const int r0 = blockIdx.y * e.gn_rb;
+  const bool on = col < e.N;
+  float u[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, w[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (on) {
+    const int b = (int)e.gn_pd.div((unsigned)r0);
+    float4 tb[8];
+    const float4* tp = e.gn_tab + (long long)b * e.N + col;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) tb[q] = tp[q];
+    const int zs = (int)e.split_stride;
+#pragma unroll 1
+    for (int rl = rl0; rl < e.gn_rb; rl += 8) {
+      const int row = r0 + rl;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+      const float* p = e.ws + (long long)row * e.N + col;
+#pragma unroll 4
+      for (int zz = 0; zz < e.nsplit; ++zz) {
+        const float4 x = *(const float4*)(p + (long long)zz * zs), y = *(const float4*)(p + (long long)zz * zs + 4);
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+        c.x += y.x; c.y += y.y; c.z += y.z; c.w += y.w;
+      }
+      float v[8] = {a.x * e.alpha, a.y * e.alpha, a.z * e.alpha, a.w * e.alpha,
+                    c.x * e.alpha, c.y * e.alpha, c.z * e.alpha, c.w * e.alpha};
+      const uint4 xr = *(const uint4*)(e.gn_x + (long long)row * e.gn_ldx + col);
+      const uint4 pk = pack8(v);
+      *(uint4*)((bf16_t*)e.C + (long long)row * e.ldc + col) = pk;
+      unpack8(pk, v);
+      gn_accum(e, v, xr, tb, u, w);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    red[rl0][c8 * 8 + q][0] = u[q];
+    red[rl0][c8 * 8 + q][1] = w[q];
+  }
+  __syncthreads();
+  const int j = blockIdx.x * 256 + t;
+  if (j < e.N) {
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      a1 += red[r][t][0];
+      a2 += red[r][t][1];
+    }
+    *(float2*)(e.gn_part + ((long long)blockIdx.y * e.N + j) * 2) = make_float2(a1, a2);
+  }
+}
+
 // Sum split-K slabs and apply the epilogue, general N (one element per thread).
 __global__ void splitk_reduce_kernel(const EpiArgs g0) {
   EpiArgs g = g0;  // grid.y = problem of a grouped launch
@@ -1249,6 +1317,11 @@ __global__ void splitk_reduce_kernel(const EpiArgs g0) {
 }
 
 hipError_t launch_reduce(const EpiArgs& red, hipStream_t s, int G = 1) {
+  if (red.gn_part) {
+    sdmi_rt::launch(splitk_reduce_gn_kernel, dim3((unsigned)((red.N + 255) / 256), (unsigned)(red.M / red.gn_rb)),
+                    dim3(256), 0, s, red);
+    return hipGetLastError();
+  }
   if (!red.n8) {
     const long long total = (long long)red.M * red.N;
     sdmi_rt::launch(splitk_reduce_kernel, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096), G), dim3(256),
@@ -1333,36 +1406,18 @@ int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total
 // Column-tile width: 192 (2-stage DMA, B_NK, N % 192 == 0) when it needs fewer rounds x columns of the
 // 512 workgroup slots (2 per CU) than 128 -- e.g. 32768 x 384: 768 tiles = 1.5 rounds at 128, 512 = 1 at 192.
 int pick_tbn(const sdmi_gemm_desc* d, int variant) {
-  static int force = -2;
-  if (force == -2) {
-    const char* s = getenv("SDMI_GEMM_TBN");
-    force = s ? atoi(s) : -1;
-  }
   if (variant == 4) return d->n % 384 == 0 ? 384 : 256;
   if (variant == 7) return 64;
   if (variant == 8 || variant == 6) return BN;
   if (variant == 5) return d->b_mode == SDMI_B_NK && d->n % 192 == 0 ? 192 : BN;
   if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR) return BN;
   // narrow outputs (N <= 64: the VQVAE's 64-channel convs at 256^2, 4-channel heads, DiT proj_out): a 128-column
-  // tile would spend half (or more) of its MFMAs on zero-padded columns. SDMI_GEMM_TBN64 = the largest N given
-  // 64-column tiles (default 64; 0 disables)
-  static int tbn64 = -1;
-  if (tbn64 < 0) {
-    const char* s = getenv("SDMI_GEMM_TBN64");
-    tbn64 = s ? atoi(s) : 64;
-    if (tbn64 < 0) tbn64 = 64;
-  }
-  if (d->n <= tbn64 && force != 128) return 64;
+  // tile would spend half (or more) of its MFMAs on zero-padded columns
+  if (d->n <= 64) return 64;
   // ragged N whose last 128-column tile would be at most half used (DiT hidden size 288: 3 x 128 = 384 columns,
-  // 25 % padding; 5 x 64 = 320, 10 %). SDMI_GEMM_TBN64_RAGGED=0 disables.
-  static int ragged = -1;
-  if (ragged < 0) {
-    const char* s = getenv("SDMI_GEMM_TBN64_RAGGED");
-    ragged = s ? atoi(s) : 1;
-  }
-  if (ragged && force != 128 && d->tile_n_hint != 128 && d->n % 128 && d->n % 128 <= 64 && d->n % 192) return 64;
+  // 25 % padding; 5 x 64 = 320, 10 %)
+  if (d->tile_n_hint != 128 && d->n % 128 && d->n % 128 <= 64 && d->n % 192) return 64;
   if (d->n % 192) return BN;
-  if (force == 128 || force == 192) return force;
   if (d->tile_n_hint == 128 || d->tile_n_hint == 192) return d->tile_n_hint;
   const long long mt = (d->m + BM - 1) / BM;
   const long long r128 = (mt * ((d->n + BN - 1) / BN) + 511) / 512, r192 = (mt * (d->n / 192) + 511) / 512;
@@ -1371,9 +1426,12 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
 
 template <int AM, int BMODE, int STAGES, int TBN, int TBM, int NWN, int RED, int KBK = BK>
 hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
+  constexpr int NTH = dma_threads<TBM, NWN>();
   constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * KBK * 2, epi = (size_t)64 * (TBN + 4) * 4;
-  sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid,
-                  dim3(dma_threads<TBM, NWN>()), ring > epi ? ring : epi, s, a, e);
+  // GroupNorm-backward statistics: the row-lane sums (NTH / (TBN / 8) x TBN x 2 floats) after the staged tile
+  const size_t epi_gn = epi + (size_t)(NTH / (TBN / 8)) * TBN * 2 * 4;
+  const size_t need = std::max(ring, e.gn_part ? epi_gn : epi);
+  sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid, dim3(NTH), need, s, a, e);
   return hipGetLastError();
 }
 
@@ -1426,35 +1484,6 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, i
     if (a.rowsum) return launch_dma_red<AM, BMODE, 1>(a, e, grid, s, v, tbn);
   }
   return launch_dma_red<AM, BMODE, 0>(a, e, grid, s, v, tbn);
-}
-
-// Split-K arrival counters: SK_SLOTS regions of SK_SLOT_TILES, one region per launch, round-robin, so split
-// GEMMs in flight at the same time on different streams never share a counter. Zero at load; the last arriver
-// of every tile re-arms its counter (plan / graph replays included).
-constexpr int SK_SLOTS = 64, SK_SLOT_TILES = 4096;
-__device__ unsigned g_splitk_counters[SK_SLOTS * SK_SLOT_TILES];
-
-// counter region for one launch of `tiles` output tiles split `splits` ways, or null (separate reducer launch).
-// The in-launch combine is used up to SDMI_SPLITK_FUSED splits (default 0 = never): its last arriver reads all of
-// the tile's slabs alone; measured slower than the reducer launch on the cond-UNet step even for 2-way splits
-// (+0.2 ms/step at <= 2, +0.5 at <= 4, +3.5 at any).
-unsigned* splitk_counters(long long tiles, int splits) {
-  static int fused_max = -1;
-  static unsigned* addr[64] = {};
-  static std::atomic<unsigned> next{0};
-  if (fused_max < 0) {
-    const char* s = getenv("SDMI_SPLITK_FUSED");
-    fused_max = s ? atoi(s) : 0;
-  }
-  if (splits > fused_max || tiles > SK_SLOT_TILES) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!addr[dev]) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_splitk_counters)) != hipSuccess) return nullptr;
-    addr[dev] = (unsigned*)p;
-  }
-  return addr[dev] + (size_t)(next.fetch_add(1) % SK_SLOTS) * SK_SLOT_TILES;
 }
 
 int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
@@ -1535,50 +1564,38 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
           (!d->bias2 || (uintptr_t)d->bias2 % 16 == 0) && (!d->resid || (uintptr_t)d->resid % 16 == 0) &&
           (!d->rowbias || (uintptr_t)d->rowbias % 16 == 0) &&
           (d->act != 3 || (d->ld_aux % 8 == 0 && (uintptr_t)d->aux % 16 == 0));
+  if (d->gn_part) {  // GroupNorm-backward statistics: plain bf16 epilogue, whole segments inside one sample
+    if (!d->gn_x || !d->gn_tab || d->gn_P <= 0 || d->m % d->gn_P || (d->gn_rb != 16 && d->gn_rb != 32 && d->gn_rb != 64) ||
+        d->gn_P % d->gn_rb || d->gn_P >= (1 << 24))
+      return -20;
+    if (d->bias || d->bias2 || d->rowbias || d->resid || d->act || d->remap || d->perm || has_reductions(d) ||
+        d->c_f32 || !e.vec || e.m_store != d->m || e.n_store != d->n || d->gn_ldx % 8 || (uintptr_t)d->gn_x % 16 ||
+        (uintptr_t)d->gn_part % 8 || (uintptr_t)d->gn_tab % 16)
+      return -21;
+    e.gn_x = (const bf16_t*)d->gn_x;
+    e.gn_ldx = d->gn_ldx;
+    e.gn_tab = (const float4*)d->gn_tab;
+    e.gn_part = d->gn_part;
+    e.gn_rb = d->gn_rb;
+    e.gn_silu = d->gn_silu;
+    e.gn_pd = FastDiv::make(d->gn_P);
+  }
   return 0;
 }
 
-int plan_splits_uncapped(const sdmi_gemm_desc* d, long long tiles, int nkt);
-
+// split-K slices: the measured per-shape count (splits_hint, sdmi/tuned_gemm.json) where there is one, else a shallow
+// default (>= 8 k-tiles per slice, at most 16 slices, until the grid has 384 tiles)
 int plan_splits(const sdmi_gemm_desc* d) {
   const int v = pick_variant(d), tbn = pick_tbn(d, v), tbm = tile_m(d, v);
-  long long tiles = (long long)((d->m + tbm - 1) / tbm) * ((n_grid(d, v) + tbn - 1) / tbn);
-  int nkt = (d->k + BK - 1) / BK;
-  static int cap = -1;  // SDMI_SPLIT_CAP: upper bound on the split count of col-major-A (weight-gradient) launches
-  if (cap < 0) {
-    const char* e = getenv("SDMI_SPLIT_CAP");
-    cap = e ? std::max(1, atoi(e)) : 1 << 30;
-  }
-  const int s = plan_splits_uncapped(d, tiles, nkt);
-  return d->a_mode == SDMI_A_COLMAJOR ? std::min(s, cap) : s;
-}
-
-int plan_splits_uncapped(const sdmi_gemm_desc* d, long long tiles, int nkt) {
+  const long long tiles = (long long)((d->m + tbm - 1) / tbm) * ((n_grid(d, v) + tbn - 1) / tbn);
+  const int nkt = (d->k + BK - 1) / BK;
   if (d->splits_hint > 0) {
     int s = std::min(d->splits_hint, nkt);
     while (s > 1 && (long long)s * d->m * slab_n(d) * 4 >= (1LL << 31)) s >>= 1;
     return std::max(s, 1);
   }
   int s = 1;
-  static int policy = -1;
-  if (policy < 0) {
-    const char* e = getenv("SDMI_SPLIT_POLICY");
-    policy = e ? atoi(e) : 0;
-  }
-  if (policy == 0) {  // shallow: >= 8 k-tiles per slice, at most 16 slices
-    while (tiles * s < 384 && nkt / (s * 2) >= 8 && s < 16) s *= 2;
-    return s;
-  }
-  if (policy == 2) return 1;
-  if (policy == 3) {  // only for grids far below the CU count, >= 16 k-tiles per slice
-    while (tiles * s < 128 && nkt / (s * 2) >= 16 && s < 32) s *= 2;
-    return s;
-  }
-  // fill the 256 CUs: deep split-K for the small-output / long-K weight gradients (a 128 x 128 dW over
-  // 32768 pixels is ONE tile), keeping >= 4 k-tiles per slice and the slabs within 32-bit offsets
-  while (tiles * s < 256 && nkt / (s * 2) >= 4 && s < 128 &&
-         (long long)(s * 2) * d->m * slab_n(d) * 4 < (1LL << 31))
-    s *= 2;
+  while (tiles * s < 384 && nkt / (s * 2) >= 8 && s < 16) s *= 2;
   return s;
 }
 
@@ -1661,10 +1678,6 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
     run.nsplit = splits;
     run.split_stride = slab;
     run.ws_gstride = (long long)splits * slab;
-    run.ctr_gstride = (int)(grid.x * grid.y);
-    // the in-launch combine reduces whole tiles only: the VALU row-sum chunk (outside every tile) needs the reducer
-    run.counters = (ns != nt || (variant != 0 && has_reductions(d)))
-                       ? nullptr : splitk_counters((long long)grid.x * grid.y * G, splits);
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
@@ -1677,7 +1690,7 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
     default: return -6;
   }
   if (err != hipSuccess) return (int)err;
-  if (splits > 1 && !run.counters) {
+  if (splits > 1) {
     EpiArgs red = e;
     red.raw = 0;
     red.nsplit = splits;

@@ -503,24 +503,3 @@ extern "C" int sdmi_pack_weights(const sdmi_pack_desc* descs_dev, const void* bm
   return 0;
 }
 
-// A stream whose dispatches may only use keep_num of every keep_den CUs (CU mask bit i set iff i % keep_den < keep_num,
-// so every XCD / shader engine keeps the same share whatever the bit -> CU interleave). The engine's weight-gradient
-// side stream runs on such a stream so its wide GEMMs can never occupy every CU while a small kernel of the
-// critical-path (data-gradient) chain waits for a slot.
-extern "C" int sdmi_stream_create_cu_share(int keep_num, int keep_den, sdmi_stream_t* out) {
-  if (!out || keep_den <= 0 || keep_num <= 0 || keep_num > keep_den) return -1;
-  int dev = 0, ncu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return -2;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) return -2;
-  const int words = (ncu + 31) / 32;
-  uint32_t mask[64] = {};
-  if (words > 64) return -3;
-  for (int i = 0; i < ncu; ++i)
-    if (i % keep_den < keep_num) mask[i / 32] |= 1u << (i % 32);
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess) return -4;
-  *out = (sdmi_stream_t)s;
-  return 0;
-}
-
-extern "C" int sdmi_stream_destroy(sdmi_stream_t s) { return hipStreamDestroy((hipStream_t)s) == hipSuccess ? 0 : -1; }

@@ -384,41 +384,6 @@ __host__ __device__ constexpr int small_it(int nth) { return nth == 1024 ? 8 : 1
 
 __host__ __device__ __forceinline__ int small_rows(int cw, int nth = NT) { return nth / (cw >> 3); }
 
-// host: single-pass kernels enabled (SDMI_GN_SMALL=0 disables them for A/B runs; =1 keeps only the 256-thread one)
-int gn_small_mode() {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("SDMI_GN_SMALL");
-    mode = e ? atoi(e) : 2;
-  }
-  return mode;
-}
-
-// threads per workgroup of the single-pass kernels for a P x cw slab, or 0 (multi-pass path)
-int gn_pass_threads(int P, int cw) {
-  const int mode = gn_small_mode();
-  if (mode >= 1 && cw <= NT && P <= small_it(256) * small_rows(cw, 256)) return 256;
-  if (mode >= 2 && cw <= NT && P <= small_it(1024) * small_rows(cw, 1024)) return 1024;
-  return 0;
-}
-
-// the 1024-thread single pass puts one workgroup on a CU per (strip, batch row): below SDMI_GN_PASS_MIN_WG such
-// workgroups (narrow C at B = 32: C = 128 -> 64 workgroups) the chip is mostly idle and the two-pass path
-// (pixel-split reductions, >= 512 workgroups) is used instead. 0 (default) keeps the single pass everywhere.
-int gn_pass_min_wg() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("SDMI_GN_PASS_MIN_WG");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-int gn_pass_threads_for(int P, int cw, int nch, int B) {
-  const int nth = gn_pass_threads(P, cw);
-  return (nth == 1024 && (long long)nch * B < gn_pass_min_wg()) ? 0 : nth;
-}
-
 // per-channel sums of u (and v) over the workgroup's rows -> s1/s2[cw] in LDS (red: [NTH][17] scratch), in two
 // fixed-order stages so no thread sums more than ~8 + NTH / cw partials: (1) thread j sums a contiguous segment of
 // ~8 rows of channel j % cw (segment j / cw), (2) one thread per channel sums the segments
@@ -670,29 +635,14 @@ struct PassCfg {
   int cw, nth, it;
 };
 
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
-// Occupancy-first choice: the widest strip that still gives >= SDMI_GN_MIN_WG workgroups (default 512 = 2 per CU, measured best of 512 / 1024 / 2048;
-// narrow strips share 128-B lines with their neighbours, which strip_block() keeps on one XCD), else the narrowest
-// strip; per strip the fewest threads with <= 4 pixel rows each (loads in flight per thread), else <= 8.
-// SDMI_GN_LEGACY=1: the round-1 shape (>= 64-channel strips, 256 threads x 10 rows or 1024 x 8).
+// Occupancy-first choice: the widest strip that still gives >= 512 workgroups (2 per CU, measured best of 512 / 1024 /
+// 2048; narrow strips share 128-B lines with their neighbours, which strip_block() keeps on one XCD), else the
+// narrowest strip; per strip the fewest threads with <= 4 pixel rows each (loads in flight per thread), else <= 8.
 bool pick_pass(int B, int P, int C, int G, PassCfg& pc) {
-  if (gn_small_mode() == 0) return false;
   const int Cg = C / G;
   // 32x32 and larger images (P >= 1024): 256 workgroups of wider strips measured better in isolation (32^2 C=384
   // fwd 19.7 -> 15.2 us, bwd 35.1 -> 33.7 us; C=128 bwd 18.2 -> 16.6 us; others equal), smaller images keep 512
-  static const int legacy = env_int("SDMI_GN_LEGACY", 0), target_small = env_int("SDMI_GN_MIN_WG", 512),
-                   target_big = env_int("SDMI_GN_MIN_WG_32", 256);
-  const int target = P >= 1024 ? target_big : target_small;
-  if (legacy) {
-    pc.cw = strip_width(C, Cg);
-    pc.nth = gn_pass_threads_for(P, pc.cw, (C + pc.cw - 1) / pc.cw, B);
-    pc.it = pc.nth == 256 ? 10 : 8;
-    return pc.nth != 0;
-  }
+  const int target = P >= 1024 ? 256 : 512;
   int u = Cg;
   while (u % 8) u += Cg;
   static const int NTHS[] = {64, 256, 512, 1024};
@@ -841,6 +791,98 @@ __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
   }
 }
 
+// GroupNorm (+SiLU) backward from the producing GEMM's statistics (sdmi_gemm_desc::gn_part): grid (strips of whole
+// groups, B, pixel splits). Every workgroup sums the P / rb segment partials of its (batch row, strip) in segment order
+// (fp32, fixed order: deterministic), forms the group coefficients exactly as gn_bwd_pass_kernel does, and streams
+// dx = a*dz + q*x + o (+ addend) over its pixel range -- one read of x, dy and the addend, one write of dx, no
+// reduction phase. dgamma / dbeta: the pixel-split-0 workgroups publish their (b, c) sums and the last of the B
+// arrivals per strip sums them (batch_tail).
+__global__ __launch_bounds__(NT) void gn_bwd_part_kernel(StripArgs a, const float2* part, int rb, bf16_t* dx, int lddx,
+                                                         const bf16_t* add, int ldadd) {
+  __shared__ float s1[NT], s2[NT];
+  __shared__ float2 grp[NT];
+  __shared__ float4 stb[NT];
+  const int strip = blockIdx.x, b = blockIdx.y;
+  const int c0 = strip * a.CW, cw = min(a.CW, a.C - c0);
+  const int t = threadIdx.x, Cg = a.C / a.G;
+  const int nseg = a.P / rb;
+  for (int ch = t; ch < cw; ch += NT) {
+    stb[ch] = a.tab[(long long)b * a.C + c0 + ch];
+    const float2* pp = part + (long long)b * nseg * a.C + c0 + ch;
+    float x1 = 0.f, x2 = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < nseg; ++j) {
+      const float2 v = pp[(long long)j * a.C];
+      x1 += v.x;
+      x2 += v.y;
+    }
+    s1[ch] = x1;
+    s2[ch] = x2;
+  }
+  __syncthreads();
+  const int ng = cw / Cg;
+  const float inv_n = 1.0f / ((float)a.P * Cg);
+  for (int gi = t; gi < ng; gi += NT) {
+    float A = 0.f, Bc = 0.f;
+    for (int ch = gi * Cg; ch < (gi + 1) * Cg; ++ch) {
+      A += a.gamma[c0 + ch] * s1[ch];
+      Bc += a.gamma[c0 + ch] * s2[ch];
+    }
+    const float4 tt = stb[gi * Cg];
+    const float rs = tt.w, mu = tt.z;
+    grp[gi] = make_float2(-rs * rs * Bc * inv_n, rs * rs * mu * Bc * inv_n - rs * A * inv_n);
+  }
+  const bool publish = a.sum1 && blockIdx.z == 0;
+  if (publish) {
+    for (int ch = t; ch < cw; ch += NT) {
+      float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
+      st_coherent(rp, s1[ch]);
+      st_coherent(rp + 1, s2[ch]);
+    }
+  }
+  __syncthreads();
+  const int L = cw >> 3, R = NT / L, lane = t % L, r = t / L;
+  if (r < R) {
+    const int cc = c0 + lane * 8;
+    float ta[8], tsv[8], tq[8], to[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float4 tb = stb[lane * 8 + e];
+      const float2 qo = grp[(lane * 8 + e) / Cg];
+      ta[e] = tb.x;
+      tsv[e] = tb.y;
+      tq[e] = qo.x;
+      to[e] = qo.y;
+    }
+    const int per = (a.P + gridDim.z - 1) / gridDim.z;
+    const int p0 = blockIdx.z * per, p1 = min(a.P, p0 + per);
+    const long long rbase = (long long)b * a.P;
+#pragma unroll 2
+    for (int p = p0 + r; p < p1; p += R) {
+      const long long row = rbase + p;
+      float xv[8], gv[8], av[8], ov[8];
+      unpack8(*(const uint4*)(a.x + row * a.ldx + cc), xv);
+      unpack8(*(const uint4*)(a.dy + row * a.ldy + cc), gv);
+      if (add) {
+        unpack8(*(const uint4*)(add + row * ldadd + cc), av);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) av[e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float dz = gv[e];
+        if (a.silu) dz *= silu_grad_f(fmaf(xv[e], ta[e], tsv[e]));
+        ov[e] = av[e] + fmaf(ta[e], dz, fmaf(tq[e], xv[e], to[e]));
+      }
+      *(uint4*)(dx + row * lddx + cc) = pack8(ov);
+    }
+  }
+  if (!publish) return;
+  if (!arrive_last(a.ctr + BATCH_CTR + strip, a.nb)) return;
+  batch_tail(a, c0, cw, a.sum1, a.sum2, a.C);
+}
+
 // grid of an elementwise pass: C/64 strips x B x pixel splits, >= ~2048 workgroups, >= 64 pixels each
 dim3 apply_grid(int B, int P, int C) {
   const int strips = (C + APPLY_CW - 1) / APPLY_CW;
@@ -971,6 +1013,31 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   a.tab = (const float4*)table2_ws; a.add = (const bf16_t*)addend; a.ldadd = ldadd;
   a.B = B; a.P = P; a.C = C; a.silu = silu;
   sdmi_rt::launch(gn_bwd_apply_kernel, apply_grid(B, P, C), dim3(NT), 0, s, a);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// GroupNorm backward from the dgrad GEMM's segment partials (sdmi_gemm_desc::gn_part, rb rows per segment)
+extern "C" int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                                const float* gamma, int B, int P, int C, int G, int silu, const float* part, int rb,
+                                float* ws, float* dgamma, float* dbeta, const void* addend, int ldadd,
+                                sdmi_stream_t stream) {
+  if (C % 8 || G <= 0 || C % G || B <= 0 || P <= 0 || rb <= 0 || P % rb || !part) return -1;
+  if ((dgamma == nullptr) != (dbeta == nullptr)) return -3;
+  if (ldx % 8 || lddy % 8 || lddx % 8 || (addend && ldadd % 8)) return -5;
+  StripArgs r = {};
+  r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy; r.tab = (const float4*)table;
+  r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.gamma = gamma;
+  r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
+  r.CW = strip_width(C, C / G);
+  const int nch = (C + r.CW - 1) / r.CW;
+  if (r.CW > NT || nch > BATCH_CTR) return -2;
+  if (dgamma && !(r.ctr = counter_slot())) return -4;
+  // pixel splits: >= 1024 workgroups while every split keeps >= 64 pixels
+  int ps = 1;
+  while ((long long)nch * B * ps < 1024 && P / (ps * 2) >= 64) ps *= 2;
+  sdmi_rt::launch(gn_bwd_part_kernel, dim3(nch, B, ps), dim3(NT), 0, (hipStream_t)stream, r, (const float2*)part, rb,
+                  (bf16_t*)dx, lddx, (const bf16_t*)addend, ldadd);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -13,15 +13,53 @@ namespace {
 constexpr int NT = 256;
 constexpr int NORM_BLOCKS = 2048;
 
-__global__ void sumsq_kernel(const float* g, long long n, float* partial) {
+// Gradient sum of squares in FIXED blocks of NORM_BLK elements at absolute flat offsets: block b of a range that starts
+// on a block boundary is summed by workgroup b alone, in a fixed order (per-thread float4 strides, then the wave tree,
+// then the four waves in order), into partial[b]. The partial of a block depends only on that block's data, so the
+// whole-buffer norm (sdmi_clip_unscale), the pieces overlapped with the backward (sdmi_sumsq_blocks on watermark
+// ranges rounded down to block boundaries) and the per-bucket pieces after each data-parallel all-reduce all produce
+// the same partial array -- and norm_finalize_kernel sums it in index order: bitwise the same norm for any split.
+constexpr long long NORM_BLK = 1 << 17;
+
+__global__ __launch_bounds__(NT) void sumsq_block_kernel(const float* g, long long n, float* partial) {
+  const long long b0 = (long long)blockIdx.x * NORM_BLK;
+  const long long e = n - b0 < NORM_BLK ? n - b0 : NORM_BLK;
+  const float* gb = g + b0;
   float acc = 0.f;
-  const long long n4 = n / 4;
-  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n4; i += (long long)gridDim.x * NT) {
-    float4 v = ((const float4*)g)[i];
+  const long long e4 = e / 4;
+  for (long long i = threadIdx.x; i < e4; i += NT) {
+    const float4 v = ((const float4*)gb)[i];
     acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
-  if (blockIdx.x == 0)
-    for (long long i = n4 * 4 + threadIdx.x; i < n; i += NT) acc += g[i] * g[i];
+  for (long long i = e4 * 4 + threadIdx.x; i < e; i += NT) acc += gb[i] * gb[i];
+  __shared__ float red[NT / 64];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// the bf16 gradient wire: dst[i] = float(src[i]) (exact) and, when partial != null, the block sums of squares of dst
+__global__ __launch_bounds__(NT) void widen_sumsq_kernel(const bf16_t* src, float* dst, long long n, float* partial) {
+  const long long b0 = (long long)blockIdx.x * NORM_BLK;
+  const long long e = n - b0 < NORM_BLK ? n - b0 : NORM_BLK;
+  const bf16_t* sb = src + b0;
+  float* db = dst + b0;
+  float acc = 0.f;
+  const long long e4 = e / 4;
+  for (long long i = threadIdx.x; i < e4; i += NT) {
+    const uint2 u = ((const uint2*)sb)[i];
+    const float4 v = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                 __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+    ((float4*)db)[i] = v;
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  for (long long i = e4 * 4 + threadIdx.x; i < e; i += NT) {
+    const float v = bf2f(sb[i]);
+    db[i] = v;
+    acc += v * v;
+  }
+  if (!partial) return;
   __shared__ float red[NT / 64];
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -156,24 +194,37 @@ __global__ void cast_bf16_kernel(const float* p, bf16_t* pb, long long n) {
 
 extern "C" size_t sdmi_optim_workspace(void) { return NORM_BLOCKS * sizeof(float); }
 
+extern "C" long long sdmi_norm_block(void) { return NORM_BLK; }
+
 // state: device float[8], initialise to {0, 0, init_scale, 0, 0, 0, 0, 0}
 extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws,
                                  int growth_interval, int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream) {
+  if (!grads || !state || !ws || n <= 0 || ((uintptr_t)grads & 15)) return -1;
+  const long long nb = (n + NORM_BLK - 1) / NORM_BLK;
+  if (nb > NORM_BLOCKS) return -3;  // > 268 M parameters: sdmi_sumsq_blocks into a larger partial array instead
   hipStream_t s = (hipStream_t)stream;
-  sdmi_rt::launch(sumsq_kernel, dim3(NORM_BLOCKS), dim3(NT), 0, s, grads, n, ws);
+  sdmi_rt::launch(sumsq_block_kernel, dim3((unsigned)nb), dim3(NT), 0, s, grads, n, ws);
   SDMI_CHECK_LAUNCH();
-  sdmi_rt::launch(norm_finalize_kernel, dim3(1), dim3(NT), 0, s, ws, NORM_BLOCKS, max_norm, state, growth_interval,
+  sdmi_rt::launch(norm_finalize_kernel, dim3(1), dim3(NT), 0, s, ws, (int)nb, max_norm, state, growth_interval,
                      skip_if_loss_nonfinite, grad_div);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
 
-// Gradient norm in pieces: sum-of-squares partials of one range of the flat gradient buffer (nblocks partials into
-// partial[0 .. nblocks)), issued while the backward is still producing later ranges; sdmi_clip_finalize then reduces
-// every partial written (in index order, double accumulation) exactly as sdmi_clip_unscale's second kernel does.
-extern "C" int sdmi_sumsq_partials(const float* grads, long long n, float* partial, int nblocks, sdmi_stream_t stream) {
-  if (!grads || !partial || n < 0 || nblocks <= 0 || ((uintptr_t)grads & 15)) return -1;
-  sdmi_rt::launch(sumsq_kernel, dim3(nblocks), dim3(NT), 0, (hipStream_t)stream, grads, n, partial);
+extern "C" int sdmi_sumsq_blocks(const float* grads, long long n, float* partial, sdmi_stream_t stream) {
+  if (!grads || !partial || n < 0 || ((uintptr_t)grads & 15)) return -1;
+  if (n == 0) return 0;
+  sdmi_rt::launch(sumsq_block_kernel, dim3((unsigned)((n + NORM_BLK - 1) / NORM_BLK)), dim3(NT), 0,
+                  (hipStream_t)stream, grads, n, partial);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_widen_bf16_sumsq(const void* src, float* dst, long long n, float* partial, sdmi_stream_t stream) {
+  if (!src || !dst || n < 0 || ((uintptr_t)src & 7) || ((uintptr_t)dst & 15)) return -1;
+  if (n == 0) return 0;
+  sdmi_rt::launch(widen_sumsq_kernel, dim3((unsigned)((n + NORM_BLK - 1) / NORM_BLK)), dim3(NT), 0,
+                  (hipStream_t)stream, (const bf16_t*)src, dst, n, partial);
   SDMI_CHECK_LAUNCH();
   return 0;
 }
@@ -213,21 +264,10 @@ extern "C" int sdmi_cast_bf16(const float* src, void* dst, long long n, sdmi_str
 extern "C" int sdmi_adam_ema_bf16(float* params, const float* grads, float* m, float* v, float* ema, long long n,
                                   const float* state, float lr, float b1, float b2, float eps, float ema_decay,
                                   float ema_alpha, void* params_bf16, sdmi_stream_t stream) {
-  static long long max_blocks = -1;  // grid cap (SDMI_ADAM_BLOCKS): a narrower grid leaves CUs to concurrent work
-  if (max_blocks < 0) {
-    const char* e = getenv("SDMI_ADAM_BLOCKS");
-    max_blocks = e ? atoll(e) : 8192;
-    if (max_blocks < 1) max_blocks = 8192;
-  }
-  static int allow_vec = -1;  // SDMI_ADAM_VEC=0: scalar streams (A/B runs)
-  if (allow_vec < 0) {
-    const char* e = getenv("SDMI_ADAM_VEC");
-    allow_vec = e ? atoi(e) != 0 : 1;
-  }
-  const bool vec = allow_vec && ((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)m | (uintptr_t)v | (uintptr_t)ema) & 15) == 0) &&
+  const bool vec = ((((uintptr_t)params | (uintptr_t)grads | (uintptr_t)m | (uintptr_t)v | (uintptr_t)ema) & 15) == 0) &&
                    ((uintptr_t)params_bf16 & 7) == 0;
   long long blocks = (n / (vec ? 4 : 1) + NT - 1) / NT;
-  if (blocks > max_blocks) blocks = max_blocks;
+  if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   if (vec)
     sdmi_rt::launch(adam_ema_kernel<4>, dim3((unsigned)blocks), dim3(NT), 0, (hipStream_t)stream, params, grads, m, v,

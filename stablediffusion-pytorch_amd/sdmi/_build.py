@@ -11,17 +11,16 @@ PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 REPO = os.path.dirname(PKG)
 LIB = os.path.join(HERE, "libsdmi.so")
-ARCH = os.environ.get("SDMI_ARCH", "gfx950")
+ARCH = "gfx950"
 # per-source extra flags. attention.hip: softmax maxima are taken straight from MFMA accumulators; in the default
 # IEEE mode every fmaxf input would first be quieted by a canonicalising v_max_f32 (one extra VALU op per score).
 # The kernels never produce or consume NaNs (masked scores are -inf), so IEEE mode is switched off there.
 # -fno-slp-vectorize: the softmax VALU is written as scalar f32 ops; SLP would re-pack adjacent ones into
 # v_pk_{fma,mul,add}_f32, which beside MFMAs cost about three times two scalar ops (MI355X guide, 'price of one
-# filler beside MFMAs'). SDMI_ATTN_SLP=1 builds the file with SLP on (A/B).
-EXTRA_FLAGS = {"attention.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]
-               + ([] if os.environ.get("SDMI_ATTN_SLP", "0") == "1" else ["-fno-slp-vectorize"]),
+# filler beside MFMAs').
+EXTRA_FLAGS = {"attention.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee", "-fno-slp-vectorize"],
                # gemm.hip: the VALU bias row sums of the weight-gradient mainloop run beside the MFMAs (same reason)
-               "gemm.hip": [] if os.environ.get("SDMI_GEMM_SLP", "0") == "1" else ["-fno-slp-vectorize"]}
+               "gemm.hip": ["-fno-slp-vectorize"]}
 
 
 def sources():

@@ -45,6 +45,10 @@ class GemmDesc(ctypes.Structure):
         ("sum_out", ctypes.c_void_p), ("sum_out2", ctypes.c_void_p), ("gsum_out", ctypes.c_void_p),
         ("gsum_ld", ctypes.c_int), ("sum_group", ctypes.c_int),
         ("variant_hint", ctypes.c_int),
+        ("gn_x", ctypes.c_void_p), ("gn_ldx", ctypes.c_int),
+        ("gn_tab", ctypes.c_void_p),
+        ("gn_part", ctypes.c_void_p),
+        ("gn_P", ctypes.c_int), ("gn_rb", ctypes.c_int), ("gn_silu", ctypes.c_int),
     ]
 
 
@@ -87,11 +91,10 @@ SIGNATURES = {
     "sdmi_gn_apply": ([_P, _I, _P, _I, _P, _I, _I, _I, _I, _P], _I),
     "sdmi_gn_fwd": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _P, _P], _I),
     "sdmi_gn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P], _I),
+    "sdmi_gn_bwd_part": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P], _I),
     "sdmi_chan_sum": ([_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _I, _P], _I),
     "sdmi_prep_input": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),
     "sdmi_cond_wgrad": ([_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P], _I),
-    "sdmi_stream_create_cu_share": ([_I, _I, ctypes.POINTER(ctypes.c_void_p)], _I),
-    "sdmi_stream_destroy": ([_P], _I),
     "sdmi_prep_input_cmap": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),
     "sdmi_cond_wgrad_cmap": ([_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P], _I),
     "sdmi_nhwc_to_nchw": ([_P, _I, _I, _I, _I, _I, _P, _P], _I),
@@ -108,8 +111,10 @@ SIGNATURES = {
     "sdmi_optim_workspace": ([], _SZ),
     "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
     "sdmi_loss_flag": ([_P, _P, _I, _P], _I),
-    "sdmi_sumsq_partials": ([_P, _L, _P, _I, _P], _I),
     "sdmi_clip_finalize": ([_P, _I, _F, _P, _I, _I, _F, _P], _I),
+    "sdmi_norm_block": ([], _L),
+    "sdmi_sumsq_blocks": ([_P, _L, _P, _P], _I),
+    "sdmi_widen_bf16_sumsq": ([_P, _P, _L, _P, _P], _I),
     "sdmi_adam_ema": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _F, _P], _I),
     "sdmi_adam_ema_bf16": ([_P, _P, _P, _P, _P, _L, _P, _F, _F, _F, _F, _F, _F, _P, _P], _I),
     "sdmi_cast_bf16": ([_P, _P, _L, _P], _I),

@@ -14,7 +14,6 @@ HIP kernels of libsdmi.so, planned for MI355X:
 Parameters are referenced by the reference's state-dict keys; gradients go to caller-owned fp32 views.
 """
 import contextlib
-import os
 
 import torch
 
@@ -84,7 +83,7 @@ def position_embedding(D, gh, gw):
 class DiTEngine:
     EPS = 1e-6  # nn.LayerNorm(..., eps=1E-6), transformer_layer.py:27,30; transformer.py:137
 
-    def __init__(self, cfg, params, grads=None, im_channels=4, shadow=None):
+    def __init__(self, cfg, params, grads=None, im_channels=4, single_stream=False):
         self.cfg = cfg
         self.L = dit_layout(cfg, im_channels)
         L = self.L
@@ -101,29 +100,26 @@ class DiTEngine:
         # the chunk's parameters or packed weights (same protocol as the UNet engine)
         self._pending = {}
         self._key_chunk = {}
-        self.shadow = shadow  # (flat fp32 parameters, bf16 image): see PackPlan
         self.P = _WaitingParams(params, self)
         self.Gd = grads
         self.im_channels = im_channels
         self.device = next(iter(params.values())).device
         # weight-gradient GEMMs of the backward run round-robin on side streams, overlapped with the data-gradient
-        # chain on the current stream (SDMI_WG_STREAM=0: inline; SDMI_DIT_WG_STREAMS streams, default 1: measured 0 / 1 / 2 / 3 -> 4.47 / 4.00 / 4.08 / 4.11 ms/step)
-        use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
-        nside = int(os.environ.get("SDMI_DIT_WG_STREAMS", "1")) if use_side else 0
-        self.sides = [torch.cuda.Stream(device=self.device) for _ in range(nside)]
+        # chain on the current stream: one side stream (measured 0 / 1 / 2 / 3 streams -> 4.47 / 4.00 / 4.08 / 4.11 ms/step)
+        self.sides = [torch.cuda.Stream(device=self.device)] if self.device.type == "cuda" and not single_stream else []
         self.side = self.sides[0] if self.sides else None
         self._wg_next = 0
         self._keep = []
         self.cpad = (L["patch_in"] + 7) // 8 * 8
         self._pos = {}
-        self.dgrad_t = os.environ.get("SDMI_DGRAD_T", "1") != "0"  # linear data gradients from transposed packs
+        self.dgrad_t = True  # linear data gradients from transposed packs (3.5 % faster step)
         self._build_pack()
 
     # ------------------------------------------------------------------------------------------
     def _build_pack(self):
         P, L = self.P, self.L
         D, p = L["D"], L["p"]
-        pk = PackPlan(self.device, self.shadow)
+        pk = PackPlan(self.device)
 
         def lin(key, name=None, t=False):
             w = P[key]
@@ -389,7 +385,7 @@ class DiTEngine:
         """Weight-gradient work on the next side stream, after everything issued so far on the current stream;
         `keep` pins its operands until the backward's final join (the allocator must not hand their memory to the
         current stream while a side stream still reads it)."""
-        if self.side is None or not self.sides:  # inline (SDMI_WG_STREAM=0, or single-stream graph capture)
+        if self.side is None or not self.sides:  # inline (single-stream graph capture)
             yield
             return
         self._keep.extend(keep)
@@ -399,10 +395,9 @@ class DiTEngine:
         with torch.cuda.stream(side):
             yield
 
-    # SDMI_DIT_WG_GROUP = n: the projections' weight gradients of n consecutive layers go out as one launch per shape
-    # (1: every weight gradient its own launch, issued where it becomes computable). Measured DiT-12L step, same box:
-    # 1 -> 4.44 / 4.43 ms, 3 -> 4.11 / 4.13, 6 -> 4.04 / 4.05
-    _dit_group = max(1, int(os.environ.get("SDMI_DIT_WG_GROUP", "6")))
+    # the projections' weight gradients of 6 consecutive layers go out as one launch per shape. Measured DiT-12L step,
+    # same box, layers per group: 1 -> 4.44 / 4.43 ms, 3 -> 4.11 / 4.13, 6 -> 4.04 / 4.05
+    _dit_group = 6
     _pending_wg = {}
 
     def _wgrad_linear(self, dy, x, gW, gb=None):
@@ -524,7 +519,7 @@ class DiTEngine:
                          psc=mcol(ws, i, 1), gate=mcol(mod, i - 1, 5) if prev else None,
                          v=prev["v2"] if prev else None, dv=dv2, pg=mcol(ws, i - 1, 5) if prev else None, dx16=dtok,
                          N=N)
-            # grouped weight gradients: issued every SDMI_DIT_WG_GROUP layers (same-shape projections of those
+            # grouped weight gradients: issued every _dit_group layers (same-shape projections of those
             # layers in one launch each); the layers are reported final only once their gradients are issued
             if self._pending_wg and ((L["n_layers"] - i) % self._dit_group == 0 or i == 0):
                 self._flush_wg()

@@ -8,13 +8,9 @@ mode "graph": one hipGraph (torch.cuda.CUDAGraph); single-stream only (a two-str
 same host cost as eager issue on this ROCm) and N == 1 only.
 Per-step randomness (noise, t, cond-drop) is drawn into static buffers before each replay, as the reference draws it
 per step (one fused HIP launch, sdmi_step_draw)."""
-import os
-
 import torch
 
 from .plan import StepPlan
-
-_TORCH_DRAW = os.environ.get("SDMI_TORCH_DRAW", "0") == "1"
 
 
 class CapturedTrainStep:
@@ -69,31 +65,20 @@ class CapturedTrainStep:
         self.tr.step(self.x0, self.noise, self.t, self.txt, self.mask, mask_keep=self.keep)
 
     def _draw(self):
-        """One launch (sdmi_step_draw: Philox keyed by the generator's seed, a host draw counter as the offset) instead
-        of torch's five RNG calls + where (≈ 0.13 ms of the step on the compute stream); SDMI_TORCH_DRAW=1 keeps the
-        torch draws (A/B)."""
-        if not _TORCH_DRAW:
-            from . import _lib
-            txt = self.txt
-            if txt is not None:
-                assert self.text.is_contiguous() and self.empty.is_contiguous() and txt.is_contiguous()
-                assert self.text.dtype == torch.float32 and self.empty.numel() * self.B == self.text.numel()
-            _lib.check(_lib.lib().sdmi_step_draw(
-                self.noise.data_ptr(), self.noise.numel(), self.t.data_ptr(), self.B, self.tr.num_timesteps,
-                self.text.data_ptr() if txt is not None else None, self.empty.data_ptr() if txt is not None else None,
-                txt.data_ptr() if txt is not None else None, self.empty.numel() if txt is not None else 0,
-                self.text_drop_p, self.keep.data_ptr() if self.mask is not None else None, self.drop_p, self.seed,
-                self.draws, torch.cuda.current_stream(self.t.device).cuda_stream), "sdmi_step_draw")
-            self.draws += 1
-            return
-        g = self.gen
-        self.noise.normal_(generator=g)
-        self.t.random_(0, self.tr.num_timesteps, generator=g)
-        if self.txt is not None:
-            drop = torch.rand(self.B, device=self.t.device, generator=g) < self.text_drop_p  # diffusion_utils.py:21-28
-            torch.where(drop[:, None, None], self.empty, self.text, out=self.txt)
-        if self.mask is not None:
-            self.keep.copy_((torch.rand(self.B, device=self.t.device, generator=g) > self.drop_p).float())
+        """One launch (sdmi_step_draw: Philox keyed by the step's seed, a host draw counter as the offset) instead of
+        torch's five RNG calls + where (~0.13 ms of the step on the compute stream)."""
+        from . import _lib
+        txt = self.txt
+        if txt is not None:
+            assert self.text.is_contiguous() and self.empty.is_contiguous() and txt.is_contiguous()
+            assert self.text.dtype == torch.float32 and self.empty.numel() * self.B == self.text.numel()
+        _lib.check(_lib.lib().sdmi_step_draw(
+            self.noise.data_ptr(), self.noise.numel(), self.t.data_ptr(), self.B, self.tr.num_timesteps,
+            self.text.data_ptr() if txt is not None else None, self.empty.data_ptr() if txt is not None else None,
+            txt.data_ptr() if txt is not None else None, self.empty.numel() if txt is not None else 0,
+            self.text_drop_p, self.keep.data_ptr() if self.mask is not None else None, self.drop_p, self.seed,
+            self.draws, torch.cuda.current_stream(self.t.device).cuda_stream), "sdmi_step_draw")
+        self.draws += 1
 
     def step(self):
         self._draw()

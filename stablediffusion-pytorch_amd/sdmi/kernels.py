@@ -33,7 +33,7 @@ PHASE = ""  # label prefixed to profiled launches ("fwd" / "bwd" / "wg" ...; set
 # phases whose GEMMs may take the 192-column tile (measured per phase: faster in fwd / bwd; in the weight-gradient
 # phase its 80 KiB of LDS per workgroup crowds out the concurrent streams and the step ran 0.4 ms slower)
 # elsewhere the 128-column tile is requested
-TILE192_PHASES = set(os.environ.get("SDMI_TILE192_PHASES", "fwd,bwd").split(","))
+TILE192_PHASES = {"fwd", "bwd"}
 
 # measured split-K slice counts (or [splits, mainloop variant]) per GEMM shape (scripts/tune_gemm.py ->
 # sdmi/tuned_gemm.json); None = not loaded
@@ -74,28 +74,39 @@ class _Prof:
             PROFILE.append((self.tag, self.flops, self.e0, self.e1, f"[{PHASE}] {self.info}" if PHASE else self.info))
 
 
-# split-K cap for the weight-gradient GEMMs currently issued (set per backward block by the UNet engine, 0 = none):
-# weight gradients that overlap the rest of the backward need not fill the chip, and fewer slices write and re-read
-# fewer fp32 slabs; the last blocks' weight gradients (the step's tail) keep their measured split counts
-WG_CAP = 0
-
-# SDMI_DIAG_SKIP (diagnostics only -- the step then trains wrongly): "wg" leaves out every weight-gradient GEMM,
-# "opt" the optimizer + weight packing, to attribute the overlapped step's time (scripts/gpu_diag.sh)
-DIAG_SKIP = set(filter(None, os.environ.get("SDMI_DIAG_SKIP", "").split(",")))
-
-
 # running total of the GEMM FLOPs issued (the UNet engine balances its weight-gradient side streams by it)
 FLOPS_ISSUED = 0.0
+
+
+def algo_bytes(d):
+    """Algorithmic HBM bytes of one GEMM launch: every operand's UNIQUE bytes at its dtype, read or written once (an
+    implicit-GEMM conv's im2col operand counts the activation it gathers from, not the k x taps expansion), plus the
+    fused epilogue's addend / mask / second-source reads. The roofline's traffic / algorithmic ratio then shows what a
+    kernel re-reads beyond that (split-K slabs, halo and cross-tile re-reads that miss L2)."""
+    def conv_src(g, pixels):
+        return (pixels // max(1, g.oh * g.ow)) * g.ih * g.iw * g.cin * 2
+    m, n, k = d.m, d.n, d.k
+    if d.a_mode == _lib.A_CONV:
+        ka = d.k_split if d.a2 else k
+        a = conv_src(d.geom, m) if ka else 0
+        a += m * (k - d.k_split) * 2 if d.a2 else 0
+    else:
+        a = m * k * 2
+    b = conv_src(d.geom, k) if d.b_mode == _lib.B_KN_CONV else n * k * 2
+    ms, ns = (d.m_store or m), (d.n_store or n)
+    out = ms * ns * (4 if d.c_f32 else 2)
+    extra = (ms * ns * 2 if d.resid else 0) + (ms * ns * 2 if d.aux else 0)
+    return a + b + out + extra
 
 
 def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=None, rowbias=None,
          rb_ld=0, rb_div=0, resid=None, ldr=0, alpha=1.0, act=0, remap=None, perm=None, m_store=0, n_store=0,
          a2=None, lda2=0, k_split=0, bias2=None, rb_mod=0, aux=None, ld_aux=0, sum_out=None, sum_out2=None,
-         gsum=None, sum_group=0):
+         gsum=None, sum_group=0, gn=None):
     """C[m][n] = epi(sum_k A[m][k] B[k][n]).  a/b/c/resid/rowbias are tensors (pointer = data_ptr,
-    offsets already applied by slicing); see include/sdmi.h for the operand modes."""
-    if "wg" in DIAG_SKIP and PHASE == "wg":
-        return c
+    offsets already applied by slicing); see include/sdmi.h for the operand modes.
+    gn (gn_request): C is the data gradient of a [SiLU(]GroupNorm(x)[)] output; the launch also writes the
+    GroupNorm-backward segment statistics (sdmi_gemm_desc::gn_part) into gn["part"] (rows per segment gn["rb"])."""
     global FLOPS_ISSUED
     FLOPS_ISSUED += 2.0 * m * n * k
     L = _lib.lib()
@@ -136,6 +147,12 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
         if gsum is not None:
             d.gsum_out, d.gsum_ld, d.sum_group = gsum.data_ptr(), ld_of(gsum), sum_group
     d.tile_n_hint = 0 if (not PHASE or PHASE in TILE192_PHASES) else 128
+    if gn is not None:
+        d.gn_x, d.gn_ldx = gn["x"].data_ptr(), ld_of(gn["x"])
+        d.gn_tab = gn["tab"].data_ptr()
+        d.gn_P, d.gn_silu = gn["P"], 1 if gn["silu"] else 0
+        d.gn_rb = gn_rb(gn["P"], 64)
+        d.gn_part = 8  # validated by the plan; the real buffer once the split count (and so the segment) is known
     tuned = _tuned()
     if tuned:
         e = tuned.get(gemm_key(d), 0)  # splits, or [splits, mainloop variant]
@@ -143,14 +160,16 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
             d.splits_hint, d.variant_hint = e[0], e[1]
         else:
             d.splits_hint = e
-    if GEMM_CAPTURE is not None:
-        GEMM_CAPTURE.append(GemmDesc.from_buffer_copy(d))
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
-    if WG_CAP and PHASE == "wg" and splits.value > WG_CAP:  # see WG_CAP
-        d.splits_hint = WG_CAP
-        check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
+    if gn is not None:
+        rb = gn_rb(gn["P"], 64 if splits.value == 1 else 16)
+        part = torch.empty(m // rb * n * 2, dtype=torch.float32, device=c.device)
+        d.gn_rb, d.gn_part = rb, part.data_ptr()
+        gn["part"], gn["rb"] = part, rb
+    if GEMM_CAPTURE is not None:
+        GEMM_CAPTURE.append(GemmDesc.from_buffer_copy(d))
     ws = None
     if ws_bytes.value:
         ws = torch.empty(ws_bytes.value // 4, dtype=torch.float32, device=c.device)
@@ -165,6 +184,7 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
         var, tn = ctypes.c_int(0), ctypes.c_int(0)
         check(L.sdmi_gemm_kernel_info(ctypes.byref(d), ctypes.byref(var), ctypes.byref(tn)), "sdmi_gemm_kernel_info")
         info = f" variant={var.value} tile_n={tn.value}"
+        info += f" bytes={algo_bytes(d)}"
     with _Prof(f"gemm_a{a_mode}b{b_mode}", 2.0 * m * n * k, f"M={m} N={n} K={k} splits={splits.value}{info}"):
         check(L.sdmi_gemm(ctypes.byref(d), ws.data_ptr() if ws is not None else None, ws_bytes.value, _stream()),
               "sdmi_gemm")
@@ -183,7 +203,7 @@ def conv_geom(ih, iw, cin, ldx, kh, kw, oh, ow, sy, sx, oy0, ox0):
 
 
 def conv_fwd(x, B, H, W, cin, ldx, wpk, cout, kh, kw, stride, pad, out, ldo, *, bias=None, rowbias=None,
-             rb_ld=0, resid=None, ldr=0, act=0, n_store=0, x2=None, cin2=0, bias2=None, ldw=0):
+             rb_ld=0, resid=None, ldr=0, act=0, n_store=0, x2=None, cin2=0, bias2=None, ldw=0, gn=None):
     """y[b,oy,ox,co] = sum_{ty,tx,ci} x[b, oy*s+ty-pad, ox*s+tx-pad, ci] * wpk[co, (ty*kw+tx)*cin + ci].
     x: NHWC bf16 buffer (row stride ldx), wpk: bf16 [cout][kh*kw*cin]."""
     OH = (H + 2 * pad - kh) // stride + 1
@@ -195,7 +215,7 @@ def conv_fwd(x, B, H, W, cin, ldx, wpk, cout, kh, kw, stride, pad, out, ldo, *, 
     return gemm(B * OH * OW, cout, K1 + cin2, x, _lib.A_CONV, 0, wpk, _lib.B_NK, ldw or (K1 + cin2), out, ldo,
                 geom=g, bias=bias, rowbias=rowbias, rb_ld=(rb_ld or cout) if rowbias is not None else 0,
                 rb_div=OH * OW, resid=resid, ldr=ldr, act=act, n_store=n_store,
-                a2=x2, lda2=ld_of(x2) if x2 is not None else 0, k_split=K1, bias2=bias2)
+                a2=x2, lda2=ld_of(x2) if x2 is not None else 0, k_split=K1, bias2=bias2, gn=gn)
 
 
 def conv_wgrad(dy, ldy, x, B, H, W, cin, ldx, cout, kh, kw, stride, pad, out, OH, OW, *, perm=True, cvalid=0,
@@ -257,22 +277,22 @@ def linear(x, w, out, *, bias=None, resid=None, act=0, alpha=1.0, n_store=0, row
                 rowbias=rowbias, rb_ld=ld_of(rowbias) if rowbias is not None else 0, rb_mod=rb_mod)
 
 
-def linear_dgrad(dy, w, out, *, resid=None, relu_of=None):
+def linear_dgrad(dy, w, out, *, resid=None, relu_of=None, gn=None):
     """out[m][k] = sum_n dy[m][n] w[n][k] (+ resid), times (relu_of[m][k] > 0) when relu_of (the saved ReLU
     output) is given;  w [N,K] bf16 used as B[k=n][n=k] (row-major)."""
     M, N = dy.shape
     K = w.shape[1]
     return gemm(M, K, N, dy, _lib.A_ROWMAJOR, ld_of(dy), w, _lib.B_KN, w.stride(0), out, ld_of(out), resid=resid,
-                ldr=ld_of(resid) if resid is not None else 0, act=3 if relu_of is not None else 0, aux=relu_of)
+                ldr=ld_of(resid) if resid is not None else 0, act=3 if relu_of is not None else 0, aux=relu_of, gn=gn)
 
 
-def linear_dgrad_t(dy, wt, out, *, resid=None, relu_of=None):
+def linear_dgrad_t(dy, wt, out, *, resid=None, relu_of=None, gn=None):
     """linear_dgrad from the transposed weight: out[m][k] = sum_n dy[m][n] wt[k][n] (+ resid, ReLU mask as
     linear_dgrad); wt [K,N] bf16 rows (B_NK), which takes the wider N tiles of the forward GEMM."""
     M, N = dy.shape
     K = wt.shape[0]
     return gemm(M, K, N, dy, _lib.A_ROWMAJOR, ld_of(dy), wt, _lib.B_NK, ld_of(wt), out, ld_of(out), resid=resid,
-                ldr=ld_of(resid) if resid is not None else 0, act=3 if relu_of is not None else 0, aux=relu_of)
+                ldr=ld_of(resid) if resid is not None else 0, act=3 if relu_of is not None else 0, aux=relu_of, gn=gn)
 
 
 def linear_wgrad(dy, x, out, *, bias_grad=None, bias_grad2=None, group_sums=None, group=0, m_store=0):
@@ -288,8 +308,6 @@ def linear_wgrad_grouped(items):
     """linear_wgrad of several same-shape problems in ONE launch (sdmi_gemm_grouped): items = [(dy, x, out,
     bias_grad or None)], all dy / x of one shape and row stride, all bias_grad present or all None. The split count is
     the single problem's tuned one shared out over the group."""
-    if "wg" in DIAG_SKIP and PHASE == "wg":
-        return
     global FLOPS_ISSUED
     G = len(items)
     if G == 1:
@@ -332,7 +350,7 @@ def linear_wgrad_grouped(items):
     if PROFILE is not None:
         var, tn = ctypes.c_int(0), ctypes.c_int(0)
         check(L.sdmi_gemm_kernel_info(ctypes.byref(descs[0]), ctypes.byref(var), ctypes.byref(tn)), "kernel_info")
-        info = f" variant={var.value} tile_n={tn.value}"
+        info = f" variant={var.value} tile_n={tn.value} bytes={sum(algo_bytes(x) for x in descs[:G])}"
     with _Prof(f"gemm_a{_lib.A_COLMAJOR}b{_lib.B_KN}", 2.0 * M * N * K * G,
                f"M={N} N={K} K={M} splits={splits.value} groups={G}{info}"):
         check(L.sdmi_gemm_grouped(descs, G, ws.data_ptr() if ws is not None else None, ws_bytes.value, _stream()),
@@ -368,9 +386,35 @@ def gn_apply(x, tab, B, P, C, silu, out):
     return out
 
 
-def gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, silu, dgamma, dbeta, addend=None):
+def gn_rb(P, cap):
+    """rows per GroupNorm-backward statistics segment: the largest of 64 / 32 / 16 (<= cap) dividing P, else 0"""
+    for rb in (64, 32, 16):
+        if rb <= cap and P % rb == 0:
+            return rb
+    return 0
+
+
+def gn_request(x, tab, P, C, silu):
+    """GroupNorm-backward statistics request for the GEMM producing the GroupNorm output gradient (gemm(gn=...)), or
+    None where the fused path does not apply (P % 16 != 0: e.g. MNIST's 7 x 7 level; C % 8 != 0)."""
+    if P % 16 or C % 8 or ld_of(x) % 8:
+        return None
+    return dict(x=x, tab=tab, P=P, silu=silu)
+
+
+def gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, silu, dgamma, dbeta, addend=None, gn=None):
+    """GroupNorm(+SiLU) backward; with gn (the request whose GEMM produced dy) from its segment statistics in one
+    streaming launch (sdmi_gn_bwd_part), else the self-contained sdmi_gn_bwd."""
     L = _lib.lib()
     ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=x.device)
+    if gn is not None:
+        assert gn.get("part") is not None, "the producing GEMM did not run with this GroupNorm request"
+        with _Prof("gn_bwd", 0, f"B={B} P={P} C={C} part"):
+            check(L.sdmi_gn_bwd_part(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma), B, P, C,
+                                     G, 1 if silu else 0, _p(gn["part"]), gn["rb"], _p(ws), _p(dgamma), _p(dbeta),
+                                     _p(addend), ld_of(addend) if addend is not None else 0, _stream()),
+                  "sdmi_gn_bwd_part")
+        return dx
     tab2 = torch.empty(B * C * 4, dtype=torch.float32, device=x.device)
     with _Prof("gn_bwd", 0, f"B={B} P={P} C={C}"):
         check(L.sdmi_gn_bwd(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma), B, P, C, G,

@@ -7,57 +7,174 @@ all-reduced (SUM) on a dedicated stream while the backward continues. The averag
 folded into the optimizer's unscale/clip coefficient, so no extra pass touches the gradients.
 On ROCm the "nccl" backend is RCCL over xGMI; the same class runs with gloo on CPU for tests.
 
+Gradient norm (clip_grad_norm_, :362-365) in the exchange: with `norm` (a NormBlocks), each bucket's block sums of
+squares run on the reducer stream as soon as ITS all-reduce has completed -- while the next bucket is on the wire --
+so after the last bucket only the last bucket's pieces and the finalisation remain. Buckets are whole numbers of norm
+blocks, and a block's partial depends only on its own (all-reduced) data, so the norm is bitwise the whole-buffer norm
+(csrc/optim.hip sumsq_block_kernel).
+
 wire="bf16" (off by default; SDMI_GRAD_WIRE=bf16 in the trainer) sends each bucket as bf16: half the bytes on the
 xGMI links, at the cost of bf16 rounding of every rank's gradient and of the ring's partial sums (the reference's DDP
-averages fp32 gradients). The fp32 buffer is rounded into a bf16 staging copy on the reducer stream, all-reduced,
-and widened back once the collective has completed."""
+averages fp32 gradients). The fp32 bucket is rounded into a persistent bf16 staging buffer by a HIP kernel on the
+reducer stream (sdmi_cast_bf16), all-reduced, and widened back by a HIP kernel that also produces the bucket's norm
+blocks (sdmi_widen_bf16_sumsq): no aten kernel on the exchange path."""
+import math
+
 import torch
 import torch.distributed as dist
 
 from . import plan
 
+CPU_NORM_BLOCK = 1 << 17  # CPU (gloo test) tensors: the same block size as csrc/optim.hip NORM_BLK
+
+
+class NormBlocks:
+    """Partial slots of the gradient sum of squares, one per block of `blk` elements at absolute flat offsets
+    [0, numel). launch(g, lo, hi) fills the slots of [lo, hi) (lo on a block boundary; hi on one or == numel)."""
+
+    def __init__(self, numel, device):
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        if self.cuda:
+            from . import _lib
+            self.blk = int(_lib.lib().sdmi_norm_block())
+        else:
+            self.blk = CPU_NORM_BLOCK
+        self.numel = numel
+        self.n = max(1, math.ceil(numel / self.blk))
+        self.partials = torch.zeros(self.n, dtype=torch.float32, device=self.device)
+
+    def floor(self, off):
+        return off // self.blk * self.blk
+
+    def _check_range(self, lo, hi):
+        hi = min(hi, self.numel)
+        assert lo % self.blk == 0 and (hi == self.numel or hi % self.blk == 0), (lo, hi)
+        return hi
+
+    def launch(self, g, lo, hi, stream=None):
+        hi = self._check_range(lo, hi)
+        if hi <= lo:
+            return
+        dst = self.partials[lo // self.blk:]
+        if self.cuda:
+            from . import _lib
+            _lib.check(_lib.lib().sdmi_sumsq_blocks(g[lo:hi].data_ptr(), hi - lo, dst.data_ptr(),
+                                                    (stream or torch.cuda.current_stream(self.device)).cuda_stream),
+                       "sdmi_sumsq_blocks")
+        else:
+            self._cpu_blocks(g[lo:hi], dst)
+
+    def widen(self, wire, g, lo, hi, stream):
+        """g[lo:hi] = float(wire[lo:hi]) with the norm blocks of [lo, min(hi, numel)) (bf16 wire, reducer stream)."""
+        nh = self._check_range(lo, hi)
+        if self.cuda:
+            from . import _lib
+            L = _lib.lib()
+            if nh > lo:
+                _lib.check(L.sdmi_widen_bf16_sumsq(wire[lo:nh].data_ptr(), g[lo:nh].data_ptr(), nh - lo,
+                                                   self.partials[lo // self.blk:].data_ptr(), stream.cuda_stream),
+                           "sdmi_widen_bf16_sumsq")
+            if hi > nh:  # the flag tail past numel (not part of the norm)
+                _lib.check(L.sdmi_widen_bf16_sumsq(wire[nh:hi].data_ptr(), g[nh:hi].data_ptr(), hi - nh, None,
+                                                   stream.cuda_stream), "sdmi_widen_bf16_sumsq")
+        else:
+            g[lo:hi].copy_(wire[lo:hi])
+            if nh > lo:
+                self._cpu_blocks(g[lo:nh], self.partials[lo // self.blk:])
+
+    def _cpu_blocks(self, x, dst):
+        for b in range(math.ceil(x.numel() / self.blk)):
+            v = x[b * self.blk:(b + 1) * self.blk].double()
+            dst[b] = float((v * v).sum())
+
+    def whole(self, g):
+        """Every block of g[0:numel) at once (the unsplit reference of the pieces)."""
+        self.launch(g, 0, self.numel)
+
 
 class BucketReducer:
-    def __init__(self, flat, group=None, bucket_bytes=64 << 20, wire="fp32"):
+    def __init__(self, flat, group=None, bucket_bytes=64 << 20, wire="fp32", norm=None):
         if wire not in ("fp32", "bf16"):
             raise ValueError(f"gradient wire format {wire!r}: fp32 or bf16")
         self.flat = flat
         self.group = group
         self.wire = wire
+        self.norm = norm
         self.bucket = max(1, bucket_bytes // flat.element_size())
+        if norm is not None:  # whole norm blocks per bucket
+            self.bucket = max(norm.blk, (self.bucket + norm.blk - 1) // norm.blk * norm.blk)
         self.total = flat.numel()
         self.cuda = flat.is_cuda
         self.stream = torch.cuda.Stream(device=flat.device) if self.cuda else None
+        self.wire_buf = torch.empty(self.total, dtype=torch.bfloat16, device=flat.device) if wire == "bf16" else None
         self.producers = []  # extra streams that write gradients (the engine's weight-gradient stream)
         self.reset()
 
     def reset(self):
         self.launched = 0
-        self.works = []
+        self.works = {}    # bucket index -> (work, lo, hi), issued and not yet waited for
+        self.pending = []  # bucket indices in issue order whose completion work is not yet queued
+        self.nb = 0
 
-    def _issue(self, view):
-        """all-reduce on the reducer stream (also the unit a recorded StepPlan re-issues)."""
+    def _issue(self, i, lo, hi):
+        """all-reduce of bucket i on the reducer stream (the unit a recorded StepPlan re-issues as a callout)."""
         if self.cuda:
             with torch.cuda.stream(self.stream):
-                self._issue_on(view)
+                self._issue_on(i, lo, hi)
         else:
-            self._issue_on(view)
+            self._issue_on(i, lo, hi)
 
-    def _issue_on(self, view):
-        if self.wire == "bf16":
-            wire = view.to(torch.bfloat16)
-            self.works.append((dist.all_reduce(wire, group=self.group, async_op=True), wire, view))
+    def _issue_on(self, i, lo, hi):
+        buf = self.wire_buf[lo:hi] if self.wire == "bf16" else self.flat[lo:hi]
+        self.works[i] = (dist.all_reduce(buf, group=self.group, async_op=True), lo, hi)
+
+    def _wait(self, i):
+        """the reducer stream waits for bucket i's collective (NCCL/RCCL: a stream wait, no host sync)."""
+        w = self.works.pop(i)[0]
+        if self.cuda:
+            with torch.cuda.stream(self.stream):
+                w.wait()
         else:
-            self.works.append((dist.all_reduce(view, group=self.group, async_op=True), None, None))
+            w.wait()
+
+    def _complete(self, i, lo, hi):
+        """after bucket i's all-reduce: widen (bf16 wire) and the bucket's norm blocks, on the reducer stream."""
+        plan.record(self._wait, i)
+        if self.wire == "bf16":
+            if self.norm is not None:
+                self.norm.widen(self.wire_buf, self.flat, lo, hi, self.stream)
+            elif self.cuda:
+                from . import _lib
+                _lib.check(_lib.lib().sdmi_widen_bf16_sumsq(self.wire_buf[lo:hi].data_ptr(), self.flat[lo:hi].data_ptr(),
+                                                            hi - lo, None, self.stream.cuda_stream),
+                           "sdmi_widen_bf16_sumsq")
+            else:
+                self.flat[lo:hi].copy_(self.wire_buf[lo:hi])
+        elif self.norm is not None:
+            self.norm.launch(self.flat, lo, hi, self.stream)
 
     def _launch(self, lo, hi):
-        view = self.flat[lo:hi]
         if self.cuda:
             for st in [torch.cuda.current_stream(self.flat.device)] + list(self.producers):
                 ev = torch.cuda.Event()
                 plan.record_event(ev, st)
                 plan.wait_event(self.stream, ev)
-        plan.record(self._issue, view)
+        if self.wire == "bf16":  # round the final fp32 bucket into the staging buffer on the reducer stream
+            if self.cuda:
+                from . import _lib
+                _lib.check(_lib.lib().sdmi_cast_bf16(self.flat[lo:hi].data_ptr(), self.wire_buf[lo:hi].data_ptr(),
+                                                     hi - lo, self.stream.cuda_stream), "sdmi_cast_bf16")
+            else:
+                self.wire_buf[lo:hi].copy_(self.flat[lo:hi])
+        i = self.nb
+        self.nb += 1
+        plan.record(self._issue, i, lo, hi)
+        # the previous bucket completes behind this one's issue, so its widening / norm overlaps this collective
+        while self.pending:
+            j, jlo, jhi = self.pending.pop(0)
+            self._complete(j, jlo, jhi)
+        self.pending.append((i, lo, hi))
 
     def ready(self, upto):
         """Gradients at flat offsets < upto are final."""
@@ -69,16 +186,11 @@ class BucketReducer:
             self._launch(self.launched, self.total)
             self.launched = self.total
 
-    def _drain(self):
-        for w, wire, view in self.works:
-            w.wait()  # NCCL/RCCL: makes the current stream wait for the collective (no host sync)
-            if wire is not None:
-                view.copy_(wire)  # widen the summed bf16 bucket back into the fp32 gradients (current stream)
-        self.works = []
-
     def finish(self):
         if self.launched < self.total:
             self.ready(self.total)
-        plan.record(self._drain)
+        while self.pending:
+            j, jlo, jhi = self.pending.pop(0)
+            self._complete(j, jlo, jhi)
         if self.cuda:
             plan.wait_stream(torch.cuda.current_stream(self.flat.device), self.stream)

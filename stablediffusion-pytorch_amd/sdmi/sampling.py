@@ -24,8 +24,6 @@ from . import kernels as K
 from .module_glue import engine_path_ok
 from .plan import StepPlan
 
-_CTX_CACHE = os.environ.get("SDMI_SAMPLE_CTX_CACHE", "1") != "0"  # 0: the context branch recomputed every step (A/B)
-
 
 class _Loop:
     """Shared state of a captured loop: the model binding (fused engine, or a stepwise model call), x_t / noise /
@@ -79,7 +77,7 @@ class _Loop:
                 self._drop_recording()
             # the context branch (text -> context_proj -> every cross-attention's k|v) is the same for every step of
             # the loop: computed once per run into fixed buffers (UNetEngine.context_cache) instead of per step
-            if self.text is not None and hasattr(self.eng, "context_cache") and _CTX_CACHE:
+            if self.text is not None and hasattr(self.eng, "context_cache"):
                 self.ctx_cache = self.eng.context_cache(self.text, self.ctx_cache)
 
     def _drop_recording(self):

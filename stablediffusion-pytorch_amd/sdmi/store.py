@@ -89,8 +89,7 @@ class FlatStore:
             for s in shapes[k]:
                 n *= s
             self.offsets[k] = (off, n)
-            # 32-B aligned starts: 16-B vector loads of fp32 biases, and 16-B aligned rows of the trainer's bf16
-            # image of this buffer (weights read from it directly, PackPlan shadow)
+            # 32-B aligned starts: 16-B vector loads of fp32 biases
             off += (n + 7) // 8 * 8
         self.numel = off
         self.params = torch.zeros(off, dtype=torch.float32, device=device)

@@ -18,7 +18,7 @@ import torch.distributed as dist
 from . import _lib
 from . import kernels as K
 from . import plan
-from .reducer import BucketReducer
+from .reducer import BucketReducer, NormBlocks
 from .store import FlatStore, param_label, unet_gemm_natural
 from .unet_engine import UNetEngine
 from .dit_engine import DiTEngine, dit_flat_order
@@ -37,56 +37,49 @@ def scheduler_tables(num_timesteps, beta_start, beta_end):
 class NormParts:
     """clip_grad_norm_'s sum of squares in pieces overlapped with the backward (one GPU): as soon as the backward has
     finalised a >= `chunk` slice of the flat gradient buffer (the same watermarks the data-parallel reducer uses), its
-    partial sums run on a stream of their own behind every gradient producer; the last slice and the finalisation run
-    on the compute stream, so the step boundary (backward end -> norm -> first optimizer chunk -> next forward) no
-    longer waits for a full pass over the 474 MB of gradients. Partials land in fixed slots and are reduced in slot
-    order: deterministic, eager and plan-replayed steps identical."""
-
-    MAX_PARTIALS = 8192
+    block partials (NormBlocks: fixed blocks at absolute flat offsets, the watermark rounded down to a block boundary)
+    run on a stream of their own behind every gradient producer; the last slice and the finalisation run on the compute
+    stream, so the step boundary (backward end -> norm -> first optimizer chunk -> next forward) no longer waits for a
+    full pass over the 474 MB of gradients. Every block's partial depends only on its data and the finalisation sums
+    them in block order: bitwise the norm of one whole-buffer pass (sdmi_clip_unscale) and of the data-parallel
+    reducer's per-bucket pieces."""
 
     def __init__(self, grads, numel, producers=(), chunk_elems=16 << 20):
         self.g, self.numel = grads, numel
         self.chunk = chunk_elems
         self.producers = list(producers)
         self.stream = torch.cuda.Stream(device=grads.device)
-        self.partials = torch.zeros(self.MAX_PARTIALS, dtype=torch.float32, device=grads.device)
+        self.blocks = NormBlocks(numel, grads.device)
         self.reset()
 
     def reset(self):
         self.launched = 0
-        self.used = 0
-
-    @staticmethod
-    def _blocks(n):
-        return max(16, min(1024, n // (256 * 4 * 16)))
-
-    def _launch(self, lo, hi, stream):
-        nb = self._blocks(hi - lo)
-        assert self.used + nb <= self.MAX_PARTIALS
-        _lib.check(_lib.lib().sdmi_sumsq_partials(self.g[lo:hi].data_ptr(), hi - lo, self.partials[self.used:].data_ptr(),
-                                                  nb, stream.cuda_stream), "sdmi_sumsq_partials")
-        self.used += nb
 
     def ready(self, upto):
         """Gradients at flat offsets < upto are final (called during the backward)."""
-        upto = min(upto, self.numel)
+        upto = self.blocks.floor(min(upto, self.numel))
         if upto - self.launched < self.chunk:
             return
         for st in [torch.cuda.current_stream(self.g.device)] + self.producers:
             ev = torch.cuda.Event()
             plan.record_event(ev, st)
             plan.wait_event(self.stream, ev)
-        self._launch(self.launched, upto, self.stream)
+        self.blocks.launch(self.g, self.launched, upto, self.stream)
         self.launched = upto
 
     def finish(self, max_norm, state, growth, skip_mode, grad_div):
         """After the backward (side streams joined into the current stream): the rest, then clip / skip / scaler."""
         cur = torch.cuda.current_stream(self.g.device)
         if self.launched < self.numel:
-            self._launch(self.launched, self.numel, cur)
+            self.blocks.launch(self.g, self.launched, self.numel, cur)
         plan.wait_stream(cur, self.stream)
-        _lib.check(_lib.lib().sdmi_clip_finalize(self.partials.data_ptr(), self.used, max_norm, state.data_ptr(), growth,
-                                                 skip_mode, grad_div, K._stream()), "sdmi_clip_finalize")
+        finalize_norm(self.blocks, max_norm, state, growth, skip_mode, grad_div)
+
+
+def finalize_norm(blocks, max_norm, state, growth, skip_mode, grad_div):
+    """clip / skip / GradScaler update from a complete NormBlocks partial array (current stream)."""
+    _lib.check(_lib.lib().sdmi_clip_finalize(blocks.partials.data_ptr(), blocks.n, max_norm, state.data_ptr(), growth,
+                                             skip_mode, grad_div, K._stream()), "sdmi_clip_finalize")
 
 
 class DDPMTrainer:
@@ -96,7 +89,9 @@ class DDPMTrainer:
     def __init__(self, cfg, state_dict, device, *, base="cond", lr=1e-5, betas=(0.9, 0.999), eps=1e-8,
                  max_grad_norm=1.0, ema_decay=0.9999, init_scale=65536.0, growth_interval=2000,
                  sched=(1000, 0.00085, 0.012), group=None, bucket_bytes=64 << 20, force_reducer=False,
-                 grad_wire=None):
+                 grad_wire=None, single_stream=False):
+        """single_stream: every kernel on the current stream (no weight-gradient / context / optimizer side streams:
+        single-stream hipGraph capture, isolated GEMM timing)."""
         self.cfg = cfg
         self.base = base
         self.device = torch.device(device)
@@ -105,9 +100,8 @@ class DDPMTrainer:
         self.group = group
         self.world = dist.get_world_size(group) if (group is not None or dist.is_initialized()) else 1
         # N > 1: one fp32 slot after the gradients carries this rank's non-finite-loss flag through the all-reduce
-        # UNet: 3x3 / down-sampling conv weights in GEMM-natural (co, kh, kw, ci) order (store.unet_gemm_natural;
-        # SDMI_NATURAL=0 keeps torch order everywhere)
-        nat = unet_gemm_natural if base != "dit" and os.environ.get("SDMI_NATURAL", "1") != "0" else None
+        # UNet: 3x3 / down-sampling conv weights in GEMM-natural (co, kh, kw, ci) order (store.unet_gemm_natural)
+        nat = unet_gemm_natural if base != "dit" else None
         self.store = FlatStore(shapes, cfg, self.device, order=order, grad_tail=4 if self.world > 1 else 0, natural=nat)
         self.store.load(state_dict)
         if self.world > 1:
@@ -123,50 +117,40 @@ class DDPMTrainer:
         self.state = torch.tensor([0, 0, init_scale, 0, 0, 0, 0, 0], dtype=torch.float32, device=self.device)
         self.hp = dict(lr=lr, b1=betas[0], b2=betas[1], eps=eps, clip=max_grad_norm, ema=ema_decay,
                        growth=growth_interval)
-        # SDMI_SHADOW=1: a bf16 image of the flat parameters written by the optimizer pass itself
-        # (sdmi_adam_ema_bf16); the GEMM weights whose packed layout is their flat layout are read from it and only
-        # the others are repacked. Off by default: measured +0.2 ms/step on the cond-UNet (the sixth stream slows the
-        # chunked Adam in-step by ~15 %, more than the repack it saves) and neutral on DiT (same-box A/B)
-        self.shadow = None
-        if self.device.type == "cuda" and os.environ.get("SDMI_SHADOW", "0") == "1":
-            self.shadow = torch.empty(self.store.numel, dtype=torch.bfloat16, device=self.device)
-        sh = (self.store.params, self.shadow) if self.shadow is not None else None
         if base == "dit":
-            self.engine = DiTEngine(cfg, self.store.p, self.store.g, shadow=sh)
+            self.engine = DiTEngine(cfg, self.store.p, self.store.g, single_stream=single_stream)
         else:
             # latent channels from the state dict (4 for CelebHQ, the VQVAE's z_channels in general: 3 for MNIST)
             self.engine = UNetEngine(cfg, self.store.p, self.store.g, base=base,
-                                     im_channels=shapes["conv_out.weight"][0], shadow=sh)
+                                     im_channels=shapes["conv_out.weight"][0], single_stream=single_stream)
         self.num_timesteps = sched[0]
         sa, s1a = scheduler_tables(*sched)
         self.sqrt_abar, self.sqrt_1m_abar = sa.to(self.device), s1a.to(self.device)
         # force_reducer: run the bucketed all-reduce even at world size 1 (exercises RCCL + plan replay on one GPU)
         # gradient wire format of the all-reduce: fp32 (the reference's DDP) unless grad_wire / SDMI_GRAD_WIRE = bf16
         self.grad_wire = grad_wire or os.environ.get("SDMI_GRAD_WIRE", "fp32")
-        self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes, wire=self.grad_wire)
+        # the reducer also produces the gradient norm: each bucket's block partials right after its all-reduce
+        self.red_norm = (NormBlocks(self.store.numel, self.device)
+                         if (self.world > 1 or force_reducer) and self.device.type == "cuda" else None)
+        self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes, wire=self.grad_wire, norm=self.red_norm)
                         if self.world > 1 or force_reducer else None)
         self.tail_events = None  # (after backward, after the all-reduce drain): set by measure_exchange_tail()
-        # one GPU: the gradient norm in pieces overlapped with the backward (SDMI_NORM_PARTS=0: one pass afterwards).
-        # With N > 1 the norm needs the all-reduced gradients, so it stays one pass after the exchange.
+        # one GPU: the gradient norm in pieces overlapped with the backward.
+        # With N > 1 the norm needs the all-reduced gradients: the reducer computes it bucket by bucket.
         self.norm_parts = None
-        if (self.world == 1 and self.reducer is None and self.device.type == "cuda"
-                and os.environ.get("SDMI_NORM_PARTS", "1") != "0"):
+        if self.world == 1 and self.reducer is None and self.device.type == "cuda":
             self.norm_parts = NormParts(self.store.grads, self.store.numel,
                                         getattr(self.engine, "sides", None) or [])
         if self.reducer is not None and getattr(self.engine, "side", None) is not None:
             self.reducer.producers.extend(getattr(self.engine, "sides", None) or [self.engine.side])
         self._progress = None
-        self.main_stream = None
-        if self.device.type == "cuda" and os.environ.get("SDMI_MAIN_PRIORITY", "0") == "1":
-            lo, hi = torch.cuda.Stream.priority_range()
-            self.main_stream = torch.cuda.Stream(device=self.device, priority=hi)
         # Optimizer + weight packing pipelined against the next step's forward: the flat buffer is cut into
         # forward-ordered chunks; after the (global) clip, Adam + EMA + packing run chunk by chunk on the engine's
         # side stream, each chunk ending in an event that the engine waits for only where the forward first reads
-        # one of that chunk's parameters or packed weights (UNet engine; SDMI_OPT_CHUNKS=1 disables it).
+        # one of that chunk's parameters or packed weights (UNet engine, 6 chunks).
         # DiT: the forward's first GEMM (every layer's adaLN table) needs the largest chunk at once, so pipelining
-        # measured no gain there (4.00 ms/step unchunked vs 4.04-4.07 at 6 chunks): SDMI_DIT_OPT_CHUNKS, default 1
-        nchunks = int(os.environ.get("SDMI_DIT_OPT_CHUNKS", "1") if base == "dit" else os.environ.get("SDMI_OPT_CHUNKS", "6"))
+        # measured no gain there (4.00 ms/step unchunked vs 4.04-4.07 at 6 chunks): one chunk
+        nchunks = 1 if base == "dit" else 6
         self.opt_ranges = None
         if nchunks > 1 and getattr(self.engine, "side", None) is not None:
             self.opt_ranges, key_chunk = self.store.forward_chunks(nchunks)
@@ -220,17 +204,8 @@ class DDPMTrainer:
     # ------------------------------------------------------------------------------------------
     def step(self, x0, noise, t, text=None, mask=None, mask_keep=None, klass=None):
         """One training step on device tensors: x0/noise (B,4,H,W) fp32, t (B,) int64, text (B,S,C) fp32,
-        mask (B,18,MH,MW) fp32 (one-hot), mask_keep (B,) fp32 cond-drop multipliers or None.
-        With SDMI_MAIN_PRIORITY=1 the step's critical path (forward + data-gradient chain + optimizer) runs on a
-        high-priority stream, so the overlapped weight-gradient stream yields to it under contention."""
-        if self.main_stream is None:
-            return self._step(x0, noise, t, text, mask, mask_keep, klass)
-        caller = torch.cuda.current_stream(self.device)
-        plan.wait_stream(self.main_stream, caller)
-        with torch.cuda.stream(self.main_stream):
-            r = self._step(x0, noise, t, text, mask, mask_keep, klass)
-        plan.wait_stream(caller, self.main_stream)
-        return r
+        mask (B,18,MH,MW) fp32 (one-hot), mask_keep (B,) fp32 cond-drop multipliers or None."""
+        return self._step(x0, noise, t, text, mask, mask_keep, klass)
 
     def _step(self, x0, noise, t, text, mask, mask_keep, klass=None):
         eng, st = self.engine, self.store
@@ -279,6 +254,9 @@ class DDPMTrainer:
                                         K._stream()), "sdmi_loss_flag")
         if self.norm_parts is not None:
             self.norm_parts.finish(hp["clip"], self.state, hp["growth"], 1, 1.0)
+        elif self.red_norm is not None:  # the reducer's per-bucket pieces (all-reduced sums: grad_div = world)
+            finalize_norm(self.red_norm, hp["clip"], self.state, hp["growth"], 1 if self.world == 1 else 2,
+                          float(self.world))
         else:
             _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(),
                                            ws.data_ptr(), hp["growth"], 1 if self.world == 1 else 2, float(self.world),
@@ -288,19 +266,18 @@ class DDPMTrainer:
             _lib.check(L.sdmi_adam_ema_bf16(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(),
                                             self.v.data_ptr(), K._p(self.ema), st.numel, self.state.data_ptr(), hp["lr"],
                                             hp["b1"], hp["b2"], hp["eps"], ema_decay, 1.0 - ema_decay,
-                                            K._p(self.shadow), K._stream()), "sdmi_adam_ema")
-            eng.refresh_weights(cast=False)  # the optimizer pass wrote the bf16 image
+                                            None, K._stream()), "sdmi_adam_ema")
+            eng.refresh_weights()
             return self.state
         side = eng.side
         plan.wait_stream(side, torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
-            for c, (lo, hi) in enumerate(self.opt_ranges if "opt" not in K.DIAG_SKIP else ()):
+            for c, (lo, hi) in enumerate(self.opt_ranges):
                 e = self.ema[lo:hi] if self.ema is not None else None
-                sh = self.shadow[lo:hi] if self.shadow is not None else None
                 _lib.check(L.sdmi_adam_ema_bf16(st.params[lo:hi].data_ptr(), st.grads[lo:hi].data_ptr(),
                                                 self.m[lo:hi].data_ptr(), self.v[lo:hi].data_ptr(), K._p(e), hi - lo,
                                                 self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"], hp["eps"],
-                                                ema_decay, 1.0 - ema_decay, K._p(sh), K._stream()), "sdmi_adam_ema")
+                                                ema_decay, 1.0 - ema_decay, None, K._stream()), "sdmi_adam_ema")
                 eng.pack.run_chunk(c)
                 plan.record_event(self.opt_events[c], side)
             late = eng.pack.late_chunk

@@ -17,8 +17,6 @@ for MI355X:
 Parameters are referenced by the reference's state-dict keys.
 """
 import contextlib
-import math
-import os
 
 import torch
 
@@ -83,17 +81,12 @@ def cross_list(L):
 class PackPlan:
     """bf16 GEMM-layout copies of the fp32 weights, refreshed by one batched pack launch."""
 
-    def __init__(self, device, shadow=None):
-        """shadow: (flat fp32 parameter buffer, its bf16 image) kept current by the trainer's optimizer
-        (sdmi_adam_ema_bf16): a view whose packed layout IS its source's flat layout (linears, GEMM-natural conv
-        weights, concatenations of consecutive flat runs) then aliases the bf16 image instead of being packed."""
+    def __init__(self, device):
         self.device = device
         self.items = []  # (name, src tensor, dims, shape of packed view)
         self.titems = []  # layouts derived from packed views by per-tap transposes (add_transpose)
         self.total = 0
         self.views = {}
-        self.shadow = shadow
-        self.alias = {}  # view name -> element offset of its first row in the bf16 image
 
     def add(self, name, src, O, I, Ipad, KH, KW, so, si, skh, skw, kh_off=0, kh_mul=1, kw_off=0, kw_mul=1,
             rows=None, into=None, row0=0, col0=0):
@@ -144,22 +137,6 @@ class PackPlan:
         self.n_declared = n
         self.finalize()
 
-    def _flat_elem(self, it):
-        """Element offset of item `it`'s source in the shadow's flat buffer when the item is a plain copy of
-        consecutive flat elements into consecutive packed elements (identity layout), else None."""
-        if self.shadow is None or it["dst_ld"] or it["Ipad"] != it["I"]:
-            return None
-        if (it["kh_off"], it["kh_mul"], it["kw_off"], it["kw_mul"]) != (0, 1, 0, 1) or it["si"] != 1:
-            return None
-        I, KH, KW = it["I"], it["KH"], it["KW"]
-        if (KW > 1 and it["skw"] != I) or (KH > 1 and it["skh"] != KW * I) or (it["O"] > 1 and it["so"] != KH * KW * I):
-            return None
-        flat = self.shadow[0]
-        nb = it["src"].data_ptr() - flat.data_ptr()
-        if nb < 0 or nb % 4 or nb // 4 + it["O"] * KH * KW * I > flat.numel():
-            return None
-        return nb // 4
-
     def finalize(self):
         self.buf = torch.zeros(max(self.total, 64), dtype=torch.bfloat16, device=self.device)
         chunk = _lib.lib().sdmi_pack_chunk()
@@ -175,22 +152,6 @@ class PackPlan:
                     break
                 name = nm
             return name
-
-        # views that alias the bf16 parameter image: every item writing the view is an identity copy, all at the
-        # same (flat element - packed element) distance, together covering the whole view, 16-B aligned rows
-        self.alias, by_view = {}, {}
-        for j, it in enumerate(self.items):
-            by_view.setdefault(view_of(it["dst_off"]), []).append(j)
-        for nm, js in by_view.items():
-            base, rows, width = self.views[nm]
-            fe = [self._flat_elem(self.items[j]) for j in js]
-            if any(e is None for e in fe):
-                continue
-            delta = {e - self.items[j]["dst_off"] for e, j in zip(fe, js)}
-            size = sum(self.items[j]["O"] * self.items[j]["KH"] * self.items[j]["KW"] * self.items[j]["I"] for j in js)
-            if len(delta) == 1 and size == rows * width and (base + delta.pop()) % 8 == 0 and width % 8 == 0:
-                self.alias[nm] = base + (fe[0] - self.items[js[0]]["dst_off"])
-        aliased = {j for nm in self.alias for j in by_view[nm]}
 
         for j, it in enumerate(self.items):  # a view is complete after the latest chunk of the items writing it
             nm = view_of(it["dst_off"])
@@ -216,8 +177,6 @@ class PackPlan:
         descs = (_lib.PackDesc * len(self.items))()
         bmaps = [[] for _ in range(self.nchunks)]
         for j, it in enumerate(self.items):
-            if j in aliased:
-                continue
             d = descs[j]
             d.src = it["src"].data_ptr()
             d.dst = self.buf.data_ptr() + 2 * it["dst_off"]
@@ -236,10 +195,7 @@ class PackPlan:
         for j, it in enumerate(self.titems):
             d = tdescs[j]
             sbase, _, swidth = self.views[it["src_view"]]
-            if it["src_view"] in self.alias:
-                d.src = self.shadow[1].data_ptr() + 2 * (self.alias[it["src_view"]] + it["src_col0"])
-            else:
-                d.src = self.buf.data_ptr() + 2 * (sbase + it["src_col0"])
+            d.src = self.buf.data_ptr() + 2 * (sbase + it["src_col0"])
             d.dst = self.buf.data_ptr() + 2 * it["dst_off"]
             d.O, d.I, d.taps = it["O"], it["I"], it["taps"]
             d.src_ld, d.src_tap, d.dst_ld, d.dst_tap = swidth, it["src_tap"], it["dst_ld"], it["dst_tap"]
@@ -255,17 +211,10 @@ class PackPlan:
 
     def view(self, name):
         off, rows, width = self.views[name]
-        if name in self.alias:
-            a = self.alias[name]
-            return self.shadow[1][a:a + rows * width].view(rows, width)
         return self.buf[off:off + rows * width].view(rows, width)
 
-    def run(self, cast=True):
-        """Refresh every packed view; cast=False when the bf16 image is already current (the optimizer wrote it)."""
-        if self.shadow is not None and cast:
-            flat, img = self.shadow
-            _lib.check(_lib.lib().sdmi_cast_bf16(flat.data_ptr(), img.data_ptr(), flat.numel(), K._stream()),
-                       "sdmi_cast_bf16")
+    def run(self):
+        """Refresh every packed view."""
         for c in range(self.nchunks):
             self.run_chunk(c)
 
@@ -329,33 +278,11 @@ class Tape(list):
         super().append(item)
 
 
-_SIDE_STREAMS = {}
-
-
-def side_stream(device):
-    """The weight-gradient side stream. SDMI_SIDE_CU=num/den restricts it to num of every den CUs
-    (sdmi_stream_create_cu_share) so its wide GEMMs leave CUs free for the critical-path data-gradient chain;
-    unset: an ordinary stream."""
-    share = os.environ.get("SDMI_SIDE_CU", "")
-    if not share:
-        return torch.cuda.Stream(device=device)
-    num, den = (int(v) for v in share.split("/"))
-    key = (str(device), num, den)
-    if key not in _SIDE_STREAMS:  # one per process and device (never destroyed: streams live as long as the engine)
-        import ctypes
-        with torch.cuda.device(device):
-            h = ctypes.c_void_p()
-            _lib.check(_lib.lib().sdmi_stream_create_cu_share(num, den, ctypes.byref(h)), "sdmi_stream_create_cu_share")
-            _SIDE_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=device)
-    return _SIDE_STREAMS[key]
-
-
 class UNetEngine:
-    def __init__(self, cfg, params, grads=None, base=None, im_channels=4, shadow=None):
-        """params / grads: {state-dict key: fp32 CUDA tensor}; grads may be None (inference). shadow: (flat fp32
-        parameter buffer holding every params view, its bf16 image) -- see PackPlan."""
+    def __init__(self, cfg, params, grads=None, base=None, im_channels=4, single_stream=False):
+        """params / grads: {state-dict key: fp32 CUDA tensor}; grads may be None (inference). single_stream: no side
+        streams (weight gradients and the context branch inline)."""
         self.cfg = cfg
-        self.shadow = shadow
         self.L = layout(cfg)
         self.base = base or ("cond" if cfg.get("condition_config") else "uncond")
         self.P = _WaitingParams(params, self)
@@ -387,28 +314,26 @@ class UNetEngine:
         self.ctx_total = off
         # weight-gradient work (wgrad GEMMs, bias sums) runs on a side stream, overlapped with the
         # data-gradient chain of the backward on the current stream
-        use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
-        self.side = side_stream(self.device) if use_side else None
-        # SDMI_WG_STREAMS = n > 1: the weight-gradient blocks go round-robin over n side streams (the first is
-        # self.side, which also runs the optimizer chunks), so independent small weight-gradient GEMMs overlap
-        # each other as well as the data-gradient chain
-        nside = int(os.environ.get("SDMI_WG_STREAMS", "2")) if use_side else 0  # measured: 1: 15.3-15.7, 2: 15.04-15.09, 3: 15.2, 4: 15.1-15.2 ms/step
-        self.sides = [self.side] + [torch.cuda.Stream(device=self.device) for _ in range(nside - 1)] if use_side else []
+        use_side = self.device.type == "cuda" and not single_stream
+        self.side = torch.cuda.Stream(device=self.device) if use_side else None
+        # the weight-gradient blocks go round-robin over two side streams (the first is self.side, which also runs the
+        # optimizer chunks), so independent small weight-gradient GEMMs overlap each other as well as the
+        # data-gradient chain (measured 1 / 2 / 3 / 4 streams: 15.3-15.7 / 15.04-15.09 / 15.2 / 15.1-15.2 ms/step)
+        self.sides = [self.side, torch.cuda.Stream(device=self.device)] if use_side else []
         self._wg_next = 0
-        # the cross-attention context branch runs ahead of the forward on a stream of its own (SDMI_CTX_STREAM=0: inline)
-        use_ctx = self.device.type == "cuda" and os.environ.get("SDMI_CTX_STREAM", "1") != "0"
-        self.ctx_stream = torch.cuda.Stream(device=self.device) if use_ctx else None
+        # the cross-attention context branch runs ahead of the forward on a stream of its own
+        self.ctx_stream = torch.cuda.Stream(device=self.device) if use_side else None
         self._keep = []
         # linear data gradients from transposed packed weights (B_NK: the forward GEMM's wider tiles). Off by
         # default here: the data-gradient GEMMs gain 0.2 ms in isolation but the overlapped step measures
         # +0.04 ms (same-box A/B); the DiT engine, without a weight-gradient stream, gains 3.5 %.
-        self.dgrad_t = os.environ.get("SDMI_DGRAD_T", "0") != "0"
+        self.dgrad_t = False
         self._build_pack()
 
     # ------------------------------------------------------------------------------------------
     def _build_pack(self):
         P, L = self.P, self.L
-        pk = PackPlan(self.device, self.shadow)
+        pk = PackPlan(self.device)
         conv, lin = self._pk_conv, self._pk_lin
 
         cin_img = self.im_channels + (L["im_out"] if L["image"] else 0)
@@ -553,10 +478,10 @@ class UNetEngine:
         for c in sorted(self._pending):
             self._need(c)
 
-    def refresh_weights(self, cast=True):
+    def refresh_weights(self):
         if self.pack.stale():
             self.pack.finalize()
-        self.pack.run(cast=cast)
+        self.pack.run()
 
     # ------------------------------------------------------------------------------------------
     def _new(self, rows, C, dtype=torch.bfloat16):
@@ -899,14 +824,16 @@ class UNetEngine:
                          bias_grad2=self.g(rc + ".bias"))
         self._wgrad_linear(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
         dh2 = self._new(B * Pn, cout)
-        K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout)
+        # the GroupNorm backward's reductions come out of the data-gradient GEMM that produces its input gradient
+        g2 = K.gn_request(c["h1"], c["t2"], Pn, cout, True)
+        K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout, gn=g2)
         dx, fresh = grads.get(c["xn"])
         if self.dgrad_t:
             K.linear_dgrad_t(dy, self.W(f"{p}.res{l}#t"), dx, resid=None if fresh else dx)
         else:
             K.linear_dgrad(dy, self.W(f"{p}.res{l}#cat")[:, 9 * cout:], dx, resid=None if fresh else dx)
         K.gn_bwd(c["h1"], dh2, dh2, c["t2"], P[b + ".0.weight"], B, Pn, cout, G, True,
-                 self.g(b + ".0.weight"), self.g(b + ".0.bias"))
+                 self.g(b + ".0.weight"), self.g(b + ".0.bias"), gn=g2)
         off = self.temb_off.get((p, l))
         with self._wg(dh2):
             # conv1 bias, t_emb_layers bias and the per-sample time-embedding gradient (blocks.py:117-118) are
@@ -916,9 +843,10 @@ class UNetEngine:
                          bias_grad2=self.g(f"{p}.t_emb_layers.{l}.1.bias") if off is not None else None,
                          group_sums=self.dtemb_all[:, off:off + cout] if off is not None else None)
         dh0 = self._new(B * Pn, cin)
-        K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin)
+        g1 = K.gn_request(c["x"], c["t1"], Pn, cin, True)
+        K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin, gn=g1)
         K.gn_bwd(c["x"], dh0, dx, c["t1"], P[a + ".0.weight"], B, Pn, cin, G, True,
-                 self.g(a + ".0.weight"), self.g(a + ".0.bias"), addend=dx)
+                 self.g(a + ".0.weight"), self.g(a + ".0.bias"), addend=dx, gn=g1)
 
     # ---- self / cross attention --------------------------------------------------------------------
     def _attn_fwd(self, p, l, C, x, xname, out, oname, B, h, w, st, tape, cross):
@@ -978,6 +906,7 @@ class UNetEngine:
         gW = self.g(mk + ".in_proj_weight")
         gb = self.g(mk + ".in_proj_bias")
         da = self._new(B * N, C)
+        ga = K.gn_request(c["x"], c["tab"], N, C, False)
         if not c["cross"]:
             qkv = c["qkv"]
             dqkv = self._new(B * N, 3 * C)
@@ -985,9 +914,9 @@ class UNetEngine:
                        dqkv[:, C:2 * C], dqkv[:, 2 * C:], B, Hh, N, N, d)
             self._wgrad_linear(dqkv, c["a"], gW, gb)
             if WinT is not None:
-                K.linear_dgrad_t(dqkv, WinT, da)
+                K.linear_dgrad_t(dqkv, WinT, da, gn=ga)
             else:
-                K.linear_dgrad(dqkv, Win, da)
+                K.linear_dgrad(dqkv, Win, da, gn=ga)
         else:
             S, kv = c["S"], c["kv"]
             dq = self._new(B * N, C)
@@ -1007,9 +936,9 @@ class UNetEngine:
                 else:
                     K.linear_dgrad(dkv, Win[C:], dcp)
             if WinT is not None:
-                K.linear_dgrad_t(dq, WinT[:, :C], da)
+                K.linear_dgrad_t(dq, WinT[:, :C], da, gn=ga)
             else:
-                K.linear_dgrad(dq, Win[:C], da)
+                K.linear_dgrad(dq, Win[:C], da, gn=ga)
         # x receives dy (residual) + GroupNorm-branch gradient
         key, off, _ = grads.groups[c["xn"]]
         # (no alias while weight gradients are grouped: the deferred out_proj gradient still has to read dy)
@@ -1027,7 +956,7 @@ class UNetEngine:
             else:
                 addend = dy
         K.gn_bwd(c["x"], da, dx, c["tab"], P[nk + ".weight"], B, N, C, G, False,
-                 self.g(nk + ".weight"), self.g(nk + ".bias"), addend=addend)
+                 self.g(nk + ".weight"), self.g(nk + ".bias"), addend=addend, gn=ga)
 
     # ---- down / up sampling convs --------------------------------------------------------------------
     def _down_fwd(self, p, C, x, xname, out, oname, B, h, w, tape):
@@ -1088,10 +1017,11 @@ class UNetEngine:
             K.conv_wgrad(dpred, 8, c["hs"], B, H, W, C, C, 8, 3, 3, 1, 1, self.g("conv_out.weight"), H, W,
                          m_store=self.im_channels, bias_grad=self.g("conv_out.bias"))
         dhs = self._new(B * Pn, C)
-        K.conv_fwd(dpred, B, H, W, 8, 8, self.W("conv_out#d"), C, 3, 3, 1, 1, dhs, C)
+        gh = K.gn_request(c["x"], c["tab"], Pn, C, True)
+        K.conv_fwd(dpred, B, H, W, 8, 8, self.W("conv_out#d"), C, 3, 3, 1, 1, dhs, C, gn=gh)
         dx, fresh = grads.get(c["xn"])
         K.gn_bwd(c["x"], dhs, dx, c["tab"], P["norm_out.weight"], B, Pn, C, G, True,
-                 self.g("norm_out.weight"), self.g("norm_out.bias"), addend=None if fresh else dx)
+                 self.g("norm_out.weight"), self.g("norm_out.bias"), addend=None if fresh else dx, gn=gh)
 
     def _bwd_input(self, c, grads):
         L = self.L
@@ -1173,32 +1103,20 @@ class UNetEngine:
                 K.PHASE = prev
             return
         self._keep.extend(keep)
-        if self._wg_balance:  # the side stream with the fewest weight-gradient FLOPs issued so far this backward
-            si = min(range(len(self.sides)), key=lambda j: (self._wg_flops[j], j))
-        else:  # round-robin
-            si = self._wg_next % len(self.sides)
+        si = self._wg_next % len(self.sides)  # round-robin (FLOP-balanced measured no better)
         side = self.sides[si]
         self._wg_next += 1
         plan.wait_stream(side, torch.cuda.current_stream(self.device))
-        f0 = K.FLOPS_ISSUED
         try:
             with torch.cuda.stream(side):
                 yield
         finally:
             K.PHASE = prev
-        self._wg_flops[si] += K.FLOPS_ISSUED - f0
         self.wg_event = torch.cuda.Event()
         plan.record_event(self.wg_event, side)
 
-    # SDMI_WG_GROUP=0: every linear weight gradient its own launch, issued where it becomes computable
-    _group_wg = os.environ.get("SDMI_WG_GROUP", "1") != "0"
-    # SDMI_WG_BALANCE=1: a weight-gradient block goes to the side stream with the fewest FLOPs issued so far (else
-    # round-robin)
-    _wg_balance = os.environ.get("SDMI_WG_BALANCE", "0") == "1"
-    _wg_flops = [0.0] * 8
-
     def _grouping(self):
-        return self._group_wg and self.side is not None
+        return self.side is not None
 
     def _wgrad_linear(self, dy, x, gW, gb=None):
         """A linear / 1x1-conv weight gradient (dW = dy^T x, db = column sums of dy) on the side stream. Grouped
@@ -1226,7 +1144,7 @@ class UNetEngine:
 
     def _join(self):
         """The current stream waits for all weight-gradient work issued so far."""
-        if self.side is None:  # inline weight gradients (SDMI_WG_STREAM=0, or single-stream graph capture)
+        if self.side is None:  # inline weight gradients (single-stream graph capture)
             return
         for side in self.sides:
             plan.wait_stream(torch.cuda.current_stream(self.device), side)
@@ -1252,12 +1170,8 @@ class UNetEngine:
         self._wg_next = 0  # same side-stream assignment every step
         K.PHASE = "bwd"
         self._pending_wg = {}
-        self._wg_flops = [0.0] * max(1, len(self.sides))
         for k in range(len(tape) - 1, -1, -1):
             fn, c = tape[k]
-            # SDMI_WG_CAP_EARLY = n: weight gradients of every block but the tail ones (the first down level, the
-            # input / time-embedding ends) split at most n ways (kernels.WG_CAP)
-            K.WG_CAP = 0 if c.get("label") in self._tail_labels else self._wg_cap_early
             fn(c, grads)
             if self._pending_wg and (k == 0 or tape[k - 1][1].get("label") != c.get("label")):
                 self._flush_wg()  # the block's grouped weight gradients, before its gradients are reported final
@@ -1268,13 +1182,10 @@ class UNetEngine:
         self._keep = []
         self.dpred = None
         K.PHASE = ""
-        K.WG_CAP = 0
 
-    # SDMI_DY_ALIAS=1: an attention block's input gradient reuses its output-gradient buffer (the GroupNorm backward
-    # then rewrites dy in place, so the main stream first waits for the side-stream weight gradient reading dy)
-    _dy_alias = os.environ.get("SDMI_DY_ALIAS", "1") != "0"
-    _wg_cap_early = int(os.environ.get("SDMI_WG_CAP_EARLY", "0"))
-    _tail_labels = set(os.environ.get("SDMI_WG_TAIL", "downs.0,input,time").split(","))
+    # an attention block's input gradient reuses its output-gradient buffer (the GroupNorm backward then rewrites dy in
+    # place, so the main stream first waits for the side-stream weight gradient reading dy)
+    _dy_alias = True
 
     def _ctx_grad_view(self):
         """The context_proj weight gradients are one contiguous [sum C][ctx_dim] region of the flat store."""

@@ -19,7 +19,7 @@ from . import _lib
 from . import kernels as K
 from . import plan
 from .store import FlatStore
-from .unet_engine import Grads, PackPlan, Tape, UNetEngine, side_stream
+from .unet_engine import Grads, PackPlan, Tape, UNetEngine
 from .vqvae_engine import vqvae_layout
 
 S_NORM, S_COEF, S_SCALE, S_GROWTH, S_STEP, S_SKIP, S_LOSS = range(7)
@@ -49,8 +49,7 @@ class VQVAETrainEngine(UNetEngine):
         self.cin_pad = (im_channels + 7) // 8 * 8
         self.temb_off = {}  # no time embedding anywhere (blocks built with t_emb_dim=None)
         self.temb_total = 0
-        use_side = self.device.type == "cuda" and os.environ.get("SDMI_WG_STREAM", "1") != "0"
-        self.side = side_stream(self.device) if use_side else None
+        self.side = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
         self.sides = [self.side] if self.side is not None else []  # the UNet engine's _wg / _join round-robin
         self._wg_next = 0
         self._keep = []

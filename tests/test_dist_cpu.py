@@ -121,3 +121,39 @@ def test_bf16_gradient_wire_tracks_fp32_after_three_steps():
     d32, d16 = out[("fp32", 0)] - init, out[("bf16", 0)] - init
     rel = ((d16 - d32).norm() / d32.norm()).item()
     assert 0 < rel <= 2e-2, rel
+
+
+def _norm_worker(rank, world, port, wire, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sdmi.reducer import BucketReducer, NormBlocks, CPU_NORM_BLOCK
+    numel = 5 * CPU_NORM_BLOCK + 1234
+    flat = torch.randn(numel + 4, generator=torch.Generator().manual_seed(300 + rank))  # + the trainer's flag tail
+    norm = NormBlocks(numel, "cpu")
+    red = BucketReducer(flat, None, bucket_bytes=4, wire=wire, norm=norm)  # rounded up to one norm block per bucket
+    assert red.bucket == CPU_NORM_BLOCK
+    red.reset()
+    for m in (1000, CPU_NORM_BLOCK + 7, 3 * CPU_NORM_BLOCK, numel, numel + 4):
+        red.ready(m)
+    red.finish()
+    whole = NormBlocks(numel, "cpu")
+    whole.whole(flat)  # one pass over the all-reduced buffer
+    out[rank] = (red.nb, torch.equal(norm.partials, whole.partials), norm.partials.clone())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_reducer_norm_pieces_equal_whole_buffer_norm(wire):
+    """N > 1 gradient norm (train_ddpm_cond_celebhq_multi_gpu.py:362-365 on the DDP-averaged gradients): the reducer
+    computes each bucket's norm blocks right after its all-reduce (buckets are whole blocks), and the block partials
+    -- hence the finalised norm, summed in block order -- equal one whole-buffer pass over the all-reduced gradients
+    bitwise, on both ranks, for the fp32 and the bf16 wire (where the blocks are of the widened values)."""
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_norm_worker, args=(world, _free_port(), wire, out), nprocs=world, join=True)
+    for r in range(world):
+        nb, same, _ = out[r]
+        assert nb == 6 and same, (r, nb, same)
+    assert torch.equal(out[0][2], out[1][2])

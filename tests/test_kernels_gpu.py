@@ -72,6 +72,74 @@ def test_groupnorm_fwd_bwd(B, H, C, G, silu):
     assert relerr(buf.view(B, P, C).permute(0, 2, 1), xg + add.float().view(B, P, C).permute(0, 2, 1)) < 2e-2
 
 
+class _AllSplit(dict):
+    """tuned-table stand-in: every GEMM launch asks for `n` split-K slices"""
+
+    def __init__(self, n):
+        super().__init__()
+        self.n = n
+
+    def get(self, key, default=0):
+        return self.n
+
+
+# B, P (pixels per sample), C, producer ("conv": 3x3 implicit-GEMM data gradient, "linear": in-projection data gradient),
+# silu; the cond-UNet's GroupNorm inputs: 32^2 / 16^2 / 8^2 / 4^2 levels
+@pytest.mark.parametrize("B,H,C,prod,silu", [(4, 32, 384, "conv", True), (4, 16, 512, "linear", False),
+                                             (8, 8, 768, "conv", True), (32, 4, 512, "conv", True),
+                                             (32, 4, 512, "linear", False), (3, 16, 96, "conv", True)])
+@pytest.mark.parametrize("splits", [1, 4])
+def test_groupnorm_bwd_from_gemm_statistics(B, H, C, prod, silu, splits, monkeypatch):
+    """GroupNorm backward whose Σdz / Σdz·x̂ come out of the producing data-gradient GEMM (sdmi_gemm_desc::gn_part:
+    the unsplit epilogue and the split-K reducer) followed by the streaming sdmi_gn_bwd_part, against the
+    self-contained sdmi_gn_bwd on the same dy: the GEMM output is bitwise unchanged, dx / dgamma / dbeta agree to fp32
+    summation order (the partials are summed per segment, then over segments)."""
+    k = K()
+    monkeypatch.setattr(k, "TUNED", _AllSplit(splits))
+    torch.manual_seed(1)
+    P, G = H * H, 32
+    M = B * P
+    x = bf(torch.randn(M, C, device="cuda") * 2 + 0.5)
+    gamma = torch.randn(C, device="cuda") * 0.1 + 1
+    beta = torch.randn(C, device="cuda") * 0.1
+    y = torch.empty_like(x)
+    tab = k.gn_fwd(x, B, P, C, G, gamma, beta, silu, y)
+    if prod == "conv":  # dy = conv3x3 data gradient of an upstream gradient (cout = 256) through packed weights
+        cu = 256
+        g_up = bf(torch.randn(M, cu, device="cuda"))
+        wd = bf(torch.randn(C, 9 * cu, device="cuda") * 0.02)
+        run = lambda out, gn: k.conv_fwd(g_up, B, H, H, cu, cu, wd, C, 3, 3, 1, 1, out, C, gn=gn)  # noqa: E731
+    else:
+        n3 = 3 * C
+        g_up = bf(torch.randn(M, n3, device="cuda"))
+        w = bf(torch.randn(n3, C, device="cuda") * 0.05)
+        run = lambda out, gn: k.linear_dgrad(g_up, w, out, gn=gn)  # noqa: E731
+    dy_ref = torch.empty(M, C, dtype=torch.bfloat16, device="cuda")
+    run(dy_ref, None)
+    dy = torch.empty_like(dy_ref)
+    req = k.gn_request(x, tab, P, C, silu)
+    assert req is not None
+    run(dy, req)
+    torch.cuda.synchronize()
+    assert torch.equal(dy, dy_ref)
+    assert req["rb"] == (16 if splits > 1 else min(64, P))
+    add = bf(torch.randn(M, C, device="cuda"))
+    dx_ref, dx = torch.empty_like(x), torch.empty_like(x)
+    dg_ref, db_ref, dg, db = (torch.empty(C, device="cuda") for _ in range(4))
+    k.gn_bwd(x, dy_ref, dx_ref, tab, gamma, B, P, C, G, silu, dg_ref, db_ref, addend=add)
+    k.gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, silu, dg, db, addend=add, gn=req)
+    torch.cuda.synchronize()
+    assert relerr(dx, dx_ref) < 2e-3, relerr(dx, dx_ref)
+    assert relerr(dg, dg_ref) < 1e-4 and relerr(db, db_ref) < 1e-4, (relerr(dg, dg_ref), relerr(db, db_ref))
+    # deterministic: the same launches again give the same bits
+    dx2 = torch.empty_like(x)
+    req2 = k.gn_request(x, tab, P, C, silu)
+    run(dy, req2)
+    k.gn_bwd(x, dy, dx2, tab, gamma, B, P, C, G, silu, dg, db, addend=add, gn=req2)
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dx)
+
+
 # d = 8, 24, 40 take the forward's ones-column row sum (d % 16 == 8), incl. ragged N and S = 77
 @pytest.mark.parametrize("B,Hh,N,S,d", [(2, 16, 64, 64, 8), (2, 16, 256, 256, 24), (1, 16, 16, 77, 32),
                                         (2, 4, 1024, 1024, 16), (2, 16, 64, 77, 48), (1, 8, 100, 100, 64),
