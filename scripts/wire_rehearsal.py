@@ -37,7 +37,7 @@ def worker(rank, world, port, steps, wire):
     t = torch.randint(0, 1000, (B,), generator=g).cuda()
     text = torch.randn(B, 77, 64, generator=g).cuda()
     mask = torch.nn.functional.one_hot(torch.randint(0, 19, (B, 64, 64), generator=g), 19).movedim(-1, 1)[:, 1:]
-    mask = mask.float().cuda()
+    mask = mask.float().contiguous().cuda()
     torch.cuda.synchronize()
     for _ in range(steps):
         tr.step(x0, noise, t, text, mask)

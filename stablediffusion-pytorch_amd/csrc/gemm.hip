@@ -119,8 +119,9 @@ struct EpiArgs {
   const bf16_t* gn_x; int gn_ldx;
   const float4* gn_tab;
   float* gn_part;
-  int gn_rb, gn_silu;
+  int gn_rb, gn_silu, gn_fwd;
   FastDiv gn_pd;  // rows per sample
+  int gn_sl;      // split-K reducer: slab lanes of splitk_reduce_n8_kernel for the same launch (same summation order)
 };
 
 // the epilogue arguments of problem p of a grouped launch (C / sum read from the kernel-argument segment)
@@ -283,6 +284,33 @@ struct Epi {
   }
 };
 
+// the epilogue values of 8 consecutive columns of one row before the bf16 store: alpha * acc + bias + bias2 + rowbias
+// + resid (the GroupNorm-forward statistics path: no remap / column permute / activation)
+__device__ __forceinline__ void values8(const EpiArgs& g, int row, int col, float* v) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] *= g.alpha;
+  if (g.bias) {
+    const float4 b0 = *(const float4*)(g.bias + col), b1 = *(const float4*)(g.bias + col + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if (g.bias2) {
+    const float4 b0 = *(const float4*)(g.bias2 + col), b1 = *(const float4*)(g.bias2 + col + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if (g.rowbias) {
+    float t[8];
+    unpack8(*(const uint4*)(g.rowbias + rb_row(g, row) * g.rb_ld + col), t);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += t[q];
+  }
+  if (g.resid) {
+    float t[8];
+    unpack8(*(const uint4*)(g.resid + (long long)row * g.ldr + col), t);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] += t[q];
+  }
+}
+
 // dz and dz * xhat of one 8-column chunk of one output row (GroupNorm backward, EpiArgs::gn_part): v = the stored bf16
 // dy values, x the GroupNorm input there, tb the forward table {a, s, mean, rstd} of the chunk's columns
 __device__ __forceinline__ void gn_accum(const EpiArgs& e, const float* v, const uint4 xr, const float4* tb, float* u,
@@ -316,13 +344,25 @@ __device__ __forceinline__ void epi_gn_half(const EpiArgs& e, const float* st, f
       float4 tb[8];
       const float4* tp = e.gn_tab + (long long)b * e.N + col;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) tb[q] = tp[q];
+      for (int q = 0; q < 8; ++q) tb[q] = e.gn_fwd ? make_float4(0.f, 0.f, 0.f, 0.f) : tp[q];
 #pragma unroll 1
       for (int rl = s0 + rl0; rl < s0 + e.gn_rb; rl += R) {
         const int row = m0h + rl;
         if (row >= e.M) break;
         const float4 lo = *(const float4*)(st + rl * SROW + c8 * 8), hi = *(const float4*)(st + rl * SROW + c8 * 8 + 4);
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        if (e.gn_fwd) {  // forward statistics of the stored outputs: sum v, sum v^2
+          values8(e, row, col, v);
+          const uint4 pk = pack8(v);
+          *(uint4*)((bf16_t*)e.C + (long long)row * e.ldc + col) = pk;
+          unpack8(pk, v);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            u[q] += v[q];
+            w[q] = fmaf(v[q], v[q], w[q]);
+          }
+          continue;
+        }
         const uint4 xr = *(const uint4*)(e.gn_x + (long long)row * e.gn_ldx + col);
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] *= e.alpha;
@@ -1261,21 +1301,47 @@ __global__ __launch_bounds__(256) void splitk_reduce_gn_kernel(const EpiArgs e) 
     float4 tb[8];
     const float4* tp = e.gn_tab + (long long)b * e.N + col;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) tb[q] = tp[q];
+    for (int q = 0; q < 8; ++q) tb[q] = e.gn_fwd ? make_float4(0.f, 0.f, 0.f, 0.f) : tp[q];
     const int zs = (int)e.split_stride;
 #pragma unroll 1
     for (int rl = rl0; rl < e.gn_rb; rl += 8) {
       const int row = r0 + rl;
+      // the slab sum in splitk_reduce_n8_kernel<gn_sl>'s order: lane l sums slabs l, l + SL, ... in order, then the
+      // lanes are added in lane order -- so the stored dy is bitwise the reducer's without the statistics
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
       const float* p = e.ws + (long long)row * e.N + col;
+#pragma unroll 1
+      for (int l = 0; l < e.gn_sl; ++l) {
+        float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pc = pa;
 #pragma unroll 4
-      for (int zz = 0; zz < e.nsplit; ++zz) {
-        const float4 x = *(const float4*)(p + (long long)zz * zs), y = *(const float4*)(p + (long long)zz * zs + 4);
-        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
-        c.x += y.x; c.y += y.y; c.z += y.z; c.w += y.w;
+        for (int zz = l; zz < e.nsplit; zz += e.gn_sl) {
+          const float4 x = *(const float4*)(p + (long long)zz * zs), y = *(const float4*)(p + (long long)zz * zs + 4);
+          pa.x += x.x; pa.y += x.y; pa.z += x.z; pa.w += x.w;
+          pc.x += y.x; pc.y += y.y; pc.z += y.z; pc.w += y.w;
+        }
+        if (l == 0) {
+          a = pa;
+          c = pc;
+        } else {
+          a.x += pa.x; a.y += pa.y; a.z += pa.z; a.w += pa.w;
+          c.x += pc.x; c.y += pc.y; c.z += pc.z; c.w += pc.w;
+        }
       }
-      float v[8] = {a.x * e.alpha, a.y * e.alpha, a.z * e.alpha, a.w * e.alpha,
-                    c.x * e.alpha, c.y * e.alpha, c.z * e.alpha, c.w * e.alpha};
+      float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      if (e.gn_fwd) {
+        values8(e, row, col, v);
+        const uint4 pk = pack8(v);
+        *(uint4*)((bf16_t*)e.C + (long long)row * e.ldc + col) = pk;
+        unpack8(pk, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          u[q] += v[q];
+          w[q] = fmaf(v[q], v[q], w[q]);
+        }
+        continue;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= e.alpha;
       const uint4 xr = *(const uint4*)(e.gn_x + (long long)row * e.gn_ldx + col);
       const uint4 pk = pack8(v);
       *(uint4*)((bf16_t*)e.C + (long long)row * e.ldc + col) = pk;
@@ -1316,10 +1382,20 @@ __global__ void splitk_reduce_kernel(const EpiArgs g0) {
   }
 }
 
+// slab lanes of the n8 reducer: aim for >= 1024 workgroups
+int reduce_lanes(const EpiArgs& red) {
+  const long long items = (long long)red.M * (red.N / 8);
+  int sl = 1;
+  while (sl < 32 && sl * 2 <= red.nsplit && items * sl / 256 < 1024) sl *= 2;
+  return sl;
+}
+
 hipError_t launch_reduce(const EpiArgs& red, hipStream_t s, int G = 1) {
   if (red.gn_part) {
+    EpiArgs r = red;
+    r.gn_sl = reduce_lanes(red);
     sdmi_rt::launch(splitk_reduce_gn_kernel, dim3((unsigned)((red.N + 255) / 256), (unsigned)(red.M / red.gn_rb)),
-                    dim3(256), 0, s, red);
+                    dim3(256), 0, s, r);
     return hipGetLastError();
   }
   if (!red.n8) {
@@ -1329,8 +1405,7 @@ hipError_t launch_reduce(const EpiArgs& red, hipStream_t s, int G = 1) {
     return hipGetLastError();
   }
   const long long items = (long long)red.M * (red.N / 8);
-  int sl = 1;  // slab lanes: aim for >= 1024 workgroups
-  while (sl < 32 && sl * 2 <= red.nsplit && items * sl / 256 < 1024) sl *= 2;
+  const int sl = reduce_lanes(red);
   const unsigned blocks = (unsigned)std::min<long long>((items * sl + 255) / 256, 8192);
   const dim3 grid(blocks, G);  // y: problem of a grouped launch
   switch (sl) {
@@ -1430,7 +1505,7 @@ hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s)
   constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * KBK * 2, epi = (size_t)64 * (TBN + 4) * 4;
   // GroupNorm-backward statistics: the row-lane sums (NTH / (TBN / 8) x TBN x 2 floats) after the staged tile
   const size_t epi_gn = epi + (size_t)(NTH / (TBN / 8)) * TBN * 2 * 4;
-  const size_t need = std::max(ring, e.gn_part ? epi_gn : epi);
+  const size_t need = std::max(ring, (e.gn_part && !e.raw) ? epi_gn : epi);
   sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid, dim3(NTH), need, s, a, e);
   return hipGetLastError();
 }
@@ -1564,13 +1639,14 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
           (!d->bias2 || (uintptr_t)d->bias2 % 16 == 0) && (!d->resid || (uintptr_t)d->resid % 16 == 0) &&
           (!d->rowbias || (uintptr_t)d->rowbias % 16 == 0) &&
           (d->act != 3 || (d->ld_aux % 8 == 0 && (uintptr_t)d->aux % 16 == 0));
-  if (d->gn_part) {  // GroupNorm-backward statistics: plain bf16 epilogue, whole segments inside one sample
-    if (!d->gn_x || !d->gn_tab || d->gn_P <= 0 || d->m % d->gn_P || (d->gn_rb != 16 && d->gn_rb != 32 && d->gn_rb != 64) ||
-        d->gn_P % d->gn_rb || d->gn_P >= (1 << 24))
+  if (d->gn_part) {  // GroupNorm statistics: bf16 epilogue, whole segments inside one sample
+    if ((!d->gn_fwd && (!d->gn_x || !d->gn_tab)) || d->gn_P <= 0 || d->m % d->gn_P ||
+        (d->gn_rb != 16 && d->gn_rb != 32 && d->gn_rb != 64) || d->gn_P % d->gn_rb || d->gn_P >= (1 << 24))
       return -20;
-    if (d->bias || d->bias2 || d->rowbias || d->resid || d->act || d->remap || d->perm || has_reductions(d) ||
-        d->c_f32 || !e.vec || e.m_store != d->m || e.n_store != d->n || d->gn_ldx % 8 || (uintptr_t)d->gn_x % 16 ||
-        (uintptr_t)d->gn_part % 8 || (uintptr_t)d->gn_tab % 16)
+    // backward statistics: plain epilogue; forward statistics: bias / bias2 / rowbias / resid allowed
+    if ((!d->gn_fwd && (d->bias || d->bias2 || d->rowbias || d->resid)) || d->act || d->remap || d->perm ||
+        has_reductions(d) || d->c_f32 || !e.vec || e.m_store != d->m || e.n_store != d->n || (uintptr_t)d->gn_part % 8 ||
+        (!d->gn_fwd && (d->gn_ldx % 8 || (uintptr_t)d->gn_x % 16 || (uintptr_t)d->gn_tab % 16)))
       return -21;
     e.gn_x = (const bf16_t*)d->gn_x;
     e.gn_ldx = d->gn_ldx;
@@ -1578,6 +1654,7 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
     e.gn_part = d->gn_part;
     e.gn_rb = d->gn_rb;
     e.gn_silu = d->gn_silu;
+    e.gn_fwd = d->gn_fwd;
     e.gn_pd = FastDiv::make(d->gn_P);
   }
   return 0;

@@ -791,6 +791,74 @@ __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
   }
 }
 
+// GroupNorm (+SiLU) forward from the producing GEMM's statistics (sdmi_gemm_desc::gn_part with gn_fwd): grid (strips
+// of whole groups, B, pixel splits). Every workgroup sums the P / rb segment partials {sum x, sum x^2} of its (batch
+// row, strip) in segment order, merges each group in double exactly as gn_fwd_pass_kernel does, and streams
+// y = act(x * a + s) over its pixel range; the pixel-split-0 workgroups write the forward table {a, s, mean, rstd}.
+__global__ __launch_bounds__(NT) void gn_fwd_part_kernel(StripArgs a, const float2* part, int rb, bf16_t* y, int ldy) {
+  __shared__ float s1[NT], s2[NT];
+  __shared__ float2 grp[NT];
+  const int strip = blockIdx.x, b = blockIdx.y;
+  const int c0 = strip * a.CW, cw = min(a.CW, a.C - c0);
+  const int t = threadIdx.x, Cg = a.C / a.G;
+  const int nseg = a.P / rb;
+  for (int ch = t; ch < cw; ch += NT) {
+    const float2* pp = part + (long long)b * nseg * a.C + c0 + ch;
+    float x1 = 0.f, x2 = 0.f;
+#pragma unroll 8
+    for (int j = 0; j < nseg; ++j) {
+      const float2 v = pp[(long long)j * a.C];
+      x1 += v.x;
+      x2 += v.y;
+    }
+    s1[ch] = x1;
+    s2[ch] = x2;
+  }
+  __syncthreads();
+  const int ng = cw / Cg;
+  for (int gi = t; gi < ng; gi += NT) {
+    double m1 = 0, m2 = 0;
+    for (int c = gi * Cg; c < (gi + 1) * Cg; ++c) { m1 += s1[c]; m2 += s2[c]; }
+    const double n = (double)a.P * Cg, mu = m1 / n;
+    double var = m2 / n - mu * mu;
+    if (var < 0) var = 0;
+    grp[gi] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)a.eps)));
+  }
+  __syncthreads();
+  if (blockIdx.z == 0) {
+    for (int ch = t; ch < cw; ch += NT) {
+      const int c = c0 + ch;
+      const float2 mr = grp[ch / Cg];
+      const float sc = mr.y * a.gamma[c];
+      a.out_tab[(long long)b * a.C + c] = make_float4(sc, a.beta[c] - mr.x * sc, mr.x, mr.y);
+    }
+  }
+  const int L = cw >> 3, R = NT / L, lane = t % L, r = t / L;
+  if (r >= R) return;
+  const int cc = c0 + lane * 8;
+  float ta[8], ts[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float2 mr = grp[(lane * 8 + e) / Cg];
+    ta[e] = mr.y * a.gamma[cc + e];
+    ts[e] = a.beta[cc + e] - mr.x * ta[e];
+  }
+  const int per = (a.P + gridDim.z - 1) / gridDim.z;
+  const int p0 = blockIdx.z * per, p1 = min(a.P, p0 + per);
+  const long long rbase = (long long)b * a.P;
+#pragma unroll 4
+  for (int p = p0 + r; p < p1; p += R) {
+    float xv[8], o[8];
+    unpack8(*(const uint4*)(a.x + (rbase + p) * a.ldx + cc), xv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float z = fmaf(xv[e], ta[e], ts[e]);
+      o[e] = a.silu ? silu_f(z) : z;
+    }
+    *(uint4*)(y + (rbase + p) * ldy + cc) = pack8(o);
+  }
+}
+
 // GroupNorm (+SiLU) backward from the producing GEMM's statistics (sdmi_gemm_desc::gn_part): grid (strips of whole
 // groups, B, pixel splits). Every workgroup sums the P / rb segment partials of its (batch row, strip) in segment order
 // (fp32, fixed order: deterministic), forms the group coefficients exactly as gn_bwd_pass_kernel does, and streams
@@ -1013,6 +1081,25 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   a.tab = (const float4*)table2_ws; a.add = (const bf16_t*)addend; a.ldadd = ldadd;
   a.B = B; a.P = P; a.C = C; a.silu = silu;
   sdmi_rt::launch(gn_bwd_apply_kernel, apply_grid(B, P, C), dim3(NT), 0, s, a);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// GroupNorm (+SiLU) forward from the producing GEMM's segment statistics (sdmi_gemm_desc::gn_part, gn_fwd = 1)
+extern "C" int sdmi_gn_fwd_part(const void* x, int ldx, void* y, int ldy, int B, int P, int C, int G, float eps,
+                                const float* gamma, const float* beta, int silu, const float* part, int rb,
+                                float* table, sdmi_stream_t stream) {
+  if (C % 8 || G <= 0 || C % G || B <= 0 || P <= 0 || rb <= 0 || P % rb || !part || ldx % 8 || ldy % 8) return -1;
+  StripArgs a = {};
+  a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.eps = eps; a.silu = silu;
+  a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table;
+  a.CW = strip_width(C, C / G);
+  const int nch = (C + a.CW - 1) / a.CW;
+  if (a.CW > NT) return -2;
+  int ps = 1;
+  while ((long long)nch * B * ps < 1024 && P / (ps * 2) >= 64) ps *= 2;
+  sdmi_rt::launch(gn_fwd_part_kernel, dim3(nch, B, ps), dim3(NT), 0, (hipStream_t)stream, a, (const float2*)part, rb,
+                  (bf16_t*)y, ldy);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -509,6 +509,7 @@ class UNetEngine:
         K.PHASE = "fwd"
         tape = Tape()
         st = dict(B=B, H=H, W=W)
+        self._fstats = {}
         grads = Grads(dev)
         self._grads = grads
         x = plan.as_operand(x)
@@ -679,7 +680,8 @@ class UNetEngine:
         C = L["conv_out"]
         Pn = H * W
         hs = self._new(B * Pn, C)
-        tab = K.gn_fwd(cur, B, Pn, C, G, P["norm_out.weight"], P["norm_out.bias"], True, hs)
+        tab = K.gn_fwd(cur, B, Pn, C, G, P["norm_out.weight"], P["norm_out.bias"], True, hs, gn=self._fstat_take(cur))
+        self._fstats = {}
         pred = self._new(B * Pn, 8, torch.float32)
         K.conv_fwd(hs, B, H, W, C, C, self.W("conv_out#f"), 8, 3, 3, 1, 1, pred, 8, bias=P["conv_out.bias"],
                    n_store=self.im_channels)
@@ -787,24 +789,39 @@ class UNetEngine:
             grads.declare(oname, y.shape[0], y.shape[1])
         return y, oname
 
+    # ---- GroupNorm-forward statistics from the producing GEMMs ------------------------------------------
+    # A module output y that the next module normalises gets its {sum x, sum x^2} segment statistics from the GEMM
+    # that writes it (kernels.gn_request_fwd); the consuming GroupNorm then runs as one streaming pass. The registry
+    # holds the tensor itself and matches by identity, so a statistic is never applied to other data.
+    def _fstat_req(self, y, P, C):
+        r = K.gn_request_fwd(P, C) if y.shape[1] == C else None
+        if r is not None:
+            self.__dict__.setdefault("_fstats", {})[id(y)] = (y, r)
+        return r
+
+    def _fstat_take(self, x):
+        e = self.__dict__.setdefault("_fstats", {}).pop(id(x), None)
+        return e[1] if e is not None and e[0] is x else None
+
     # ---- resnet ----------------------------------------------------------------------------------
     def _resnet_fwd(self, p, l, cin, cout, x, xname, out, oname, B, h, w, st, tape):
         P, G = self.P, self.L["G"]
         Pn = h * w
         a, b = f"{p}.resnet_conv_first.{l}", f"{p}.resnet_conv_second.{l}"
         h0 = self._new(B * Pn, cin)
-        t1 = K.gn_fwd(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"], True, h0)
+        t1 = K.gn_fwd(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"], True, h0, gn=self._fstat_take(x))
         h1 = self._new(B * Pn, cout)
         off = self.temb_off.get((p, l))  # None: no time embedding (the VQVAE's blocks, t_emb_dim=None)
+        g2 = K.gn_request_fwd(Pn, cout)  # the second GroupNorm's statistics from the first conv's epilogue
         K.conv_fwd(h0, B, h, w, cin, cin, self.W(a + ".2#f"), cout, 3, 3, 1, 1, h1, cout, bias=P[a + ".2.bias"],
-                   rowbias=st["temb_all"][:, off:] if off is not None else None, rb_ld=self.temb_total)
+                   rowbias=st["temb_all"][:, off:] if off is not None else None, rb_ld=self.temb_total, gn=g2)
         h2 = self._new(B * Pn, cout)
-        t2 = K.gn_fwd(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"], True, h2)
+        t2 = K.gn_fwd(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"], True, h2, gn=g2)
         rc = f"{p}.residual_input_conv.{l}"
         y = out if out is not None else self._new(B * Pn, cout)
         # conv2(h2) + residual 1x1(x) in ONE GEMM: A = [im2col(h2) | x], B = [W2 | Wr]
         K.conv_fwd(h2, B, h, w, cout, cout, self.W(f"{p}.res{l}#cat"), cout, 3, 3, 1, 1, y, K.ld_of(y),
-                   bias=P[b + ".2.bias"], x2=x, cin2=cin, bias2=P[rc + ".bias"])
+                   bias=P[b + ".2.bias"], x2=x, cin2=cin, bias2=P[rc + ".bias"], gn=self._fstat_req(y, Pn, cout))
         tape.append((self._resnet_bwd, dict(p=p, l=l, cin=cin, cout=cout, x=x, xn=xname, yn=oname, h0=h0, h1=h1, h2=h2,
                                             t1=t1, t2=t2, B=B, h=h, w=w)))
         return y
@@ -855,7 +872,7 @@ class UNetEngine:
         nk = f"{p}.cross_attention_norms.{l}" if cross else f"{p}.attention_norms.{l}"
         mk = f"{p}.cross_attentions.{l}" if cross else f"{p}.attentions.{l}"
         a = self._new(B * N, C)
-        tab = K.gn_fwd(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"], False, a)
+        tab = K.gn_fwd(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"], False, a, gn=self._fstat_take(x))
         Win = self.W(mk + ".in_proj_weight#f")
         bin_ = P[mk + ".in_proj_bias"]
         d = C // Hh
@@ -888,7 +905,7 @@ class UNetEngine:
             c["lse"] = K.attn_fwd(q, kv[:, :C], kv[:, C:], o, B, Hh, N, S, d)
             c.update(q=q, cp=cp, kv=kv, S=S, ctx=ctx, ck=ck)
         y = out if out is not None else self._new(B * N, C)
-        K.linear(o, self.W(mk + ".out_proj#f"), y, bias=P[mk + ".out_proj.bias"], resid=x)
+        K.linear(o, self.W(mk + ".out_proj#f"), y, bias=P[mk + ".out_proj.bias"], resid=x, gn=self._fstat_req(y, N, C))
         tape.append((self._attn_bwd, c))
         return y
 
@@ -963,7 +980,7 @@ class UNetEngine:
         key = f"{p}.down_sample_conv"
         y = out if out is not None else self._new(B * (h // 2) * (w // 2), C)
         K.conv_fwd(x, B, h, w, C, K.ld_of(x), self.W(key + "#f"), C, 4, 4, 2, 1, y, K.ld_of(y),
-                   bias=self.P[key + ".bias"])
+                   bias=self.P[key + ".bias"], gn=self._fstat_req(y, (h // 2) * (w // 2), C))
         tape.append((self._down_bwd, dict(key=key, C=C, x=x, xn=xname, yn=oname, B=B, h=h, w=w)))
         return y
 
@@ -1115,8 +1132,10 @@ class UNetEngine:
         self.wg_event = torch.cuda.Event()
         plan.record_event(self.wg_event, side)
 
+    _group_wg = True  # engines whose backward loop does not flush per block (VQVAETrainEngine) set False
+
     def _grouping(self):
-        return self.side is not None
+        return self._group_wg and self.side is not None
 
     def _wgrad_linear(self, dy, x, gW, gb=None):
         """A linear / 1x1-conv weight gradient (dW = dy^T x, db = column sums of dy) on the side stream. Grouped
