@@ -118,14 +118,11 @@ typedef struct sdmi_gemm_desc {
    * dz = bf16(dy) [* SiLU'(x*a + s)], xhat = (x - mean)*rstd, x = gn_x[row*gn_ldx + j] (bf16) and {a, s, mean, rstd} =
    * gn_tab[(row / gn_P)*n + j] (the float4 forward table of sdmi_gn_fwd). Unsplit launches need gn_rb | 64, split-K
    * launches gn_rb % 8 == 0. Plain epilogue only (alpha; no bias / rowbias / resid / act / remap / perm / reductions;
-   * bf16 16-B aligned output). gn_part NULL = off. sdmi_gn_bwd_part consumes the partials.
-   * gn_fwd = 1: GroupNorm-FORWARD statistics instead -- the GEMM produces x, the input of a GroupNorm, and writes
-   * {sum v, sum v^2} of its stored bf16 outputs per segment and column (bias / bias2 / rowbias / resid epilogues
-   * allowed; gn_x / gn_tab / gn_silu unused); sdmi_gn_fwd_part consumes them. */
+   * bf16 16-B aligned output). gn_part NULL = off. sdmi_gn_bwd_part consumes the partials. */
   const void* gn_x; int gn_ldx;
   const float* gn_tab;
   float* gn_part;
-  int gn_P, gn_rb, gn_silu, gn_fwd;
+  int gn_P, gn_rb, gn_silu;
 } sdmi_gemm_desc;
 
 /* Split-K plan: how many K slices the launcher will use and the fp32 workspace bytes it needs. */
@@ -197,10 +194,6 @@ int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int 
 int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
                      const float* gamma, int B, int P, int C, int G, int silu, const float* part, int rb, float* ws,
                      float* dgamma, float* dbeta, const void* addend, int ldadd, sdmi_stream_t stream);
-/* GroupNorm (+SiLU) forward whose statistics were produced by the GEMM that wrote x (sdmi_gemm_desc::gn_part with
- * gn_fwd = 1, rb rows per segment): y = act(GroupNorm(x)) and the forward table, one streaming launch. */
-int sdmi_gn_fwd_part(const void* x, int ldx, void* y, int ldy, int B, int P, int C, int G, float eps, const float* gamma,
-                     const float* beta, int silu, const float* part, int rb, float* table, sdmi_stream_t stream);
 
 
 int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, float* ws, void* per_bc, int ld_bc, float* per_c,

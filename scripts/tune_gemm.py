@@ -41,6 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "uncond-unet", "dit", "sample"))
     ap.add_argument("--sample-batch", type=int, default=1)
+    ap.add_argument("--only-new", action="store_true", help="tune only shapes the starting table has no entry for")
     ap.add_argument("--out", default=os.path.join(REPO, "stablediffusion-pytorch_amd", "sdmi", "tuned_gemm.json"))
     args = ap.parse_args()
     from sdmi import _lib, kernels as K
@@ -112,6 +113,8 @@ def main():
         if key in seen:
             n, td, tb = seen[key]
             seen[key] = (n + 1, td, tb)
+            continue
+        if args.only_new and key in table:
             continue
         d.splits_hint = 0
         d.variant_hint = 0

@@ -119,7 +119,7 @@ struct EpiArgs {
   const bf16_t* gn_x; int gn_ldx;
   const float4* gn_tab;
   float* gn_part;
-  int gn_rb, gn_silu, gn_fwd;
+  int gn_rb, gn_silu;
   FastDiv gn_pd;  // rows per sample
   int gn_sl;      // split-K reducer: slab lanes of splitk_reduce_n8_kernel for the same launch (same summation order)
 };
@@ -284,33 +284,6 @@ struct Epi {
   }
 };
 
-// the epilogue values of 8 consecutive columns of one row before the bf16 store: alpha * acc + bias + bias2 + rowbias
-// + resid (the GroupNorm-forward statistics path: no remap / column permute / activation)
-__device__ __forceinline__ void values8(const EpiArgs& g, int row, int col, float* v) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q) v[q] *= g.alpha;
-  if (g.bias) {
-    const float4 b0 = *(const float4*)(g.bias + col), b1 = *(const float4*)(g.bias + col + 4);
-    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-  }
-  if (g.bias2) {
-    const float4 b0 = *(const float4*)(g.bias2 + col), b1 = *(const float4*)(g.bias2 + col + 4);
-    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-  }
-  if (g.rowbias) {
-    float t[8];
-    unpack8(*(const uint4*)(g.rowbias + rb_row(g, row) * g.rb_ld + col), t);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] += t[q];
-  }
-  if (g.resid) {
-    float t[8];
-    unpack8(*(const uint4*)(g.resid + (long long)row * g.ldr + col), t);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] += t[q];
-  }
-}
-
 // dz and dz * xhat of one 8-column chunk of one output row (GroupNorm backward, EpiArgs::gn_part): v = the stored bf16
 // dy values, x the GroupNorm input there, tb the forward table {a, s, mean, rstd} of the chunk's columns
 __device__ __forceinline__ void gn_accum(const EpiArgs& e, const float* v, const uint4 xr, const float4* tb, float* u,
@@ -344,25 +317,13 @@ __device__ __forceinline__ void epi_gn_half(const EpiArgs& e, const float* st, f
       float4 tb[8];
       const float4* tp = e.gn_tab + (long long)b * e.N + col;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) tb[q] = e.gn_fwd ? make_float4(0.f, 0.f, 0.f, 0.f) : tp[q];
+      for (int q = 0; q < 8; ++q) tb[q] = tp[q];
 #pragma unroll 1
       for (int rl = s0 + rl0; rl < s0 + e.gn_rb; rl += R) {
         const int row = m0h + rl;
         if (row >= e.M) break;
         const float4 lo = *(const float4*)(st + rl * SROW + c8 * 8), hi = *(const float4*)(st + rl * SROW + c8 * 8 + 4);
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        if (e.gn_fwd) {  // forward statistics of the stored outputs: sum v, sum v^2
-          values8(e, row, col, v);
-          const uint4 pk = pack8(v);
-          *(uint4*)((bf16_t*)e.C + (long long)row * e.ldc + col) = pk;
-          unpack8(pk, v);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            u[q] += v[q];
-            w[q] = fmaf(v[q], v[q], w[q]);
-          }
-          continue;
-        }
         const uint4 xr = *(const uint4*)(e.gn_x + (long long)row * e.gn_ldx + col);
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] *= e.alpha;
@@ -398,8 +359,10 @@ __device__ __forceinline__ void epi_gn_half(const EpiArgs& e, const float* st, f
 
 // Shared epilogue of the GEMM kernels: acc = this wave's 64 x (NJ*16) sub-tile (4 x NJ MFMA tiles) at (wm, wn) of a
 // TBM x TBN workgroup tile computed by NT threads; smem >= 64 x (TBN + 4) fp32 of LDS that no wave reads any more (the
-// caller synchronises before).
-template <int TBN = BN, bool XCOL = false, int TBM = BM, int NJ = TBN / 32, int NTH = NT>
+// caller synchronises before). GNE: the GroupNorm-statistics form (EpiArgs::gn_part, unsplit launches only) -- a
+// separate instantiation, so the plain epilogue's code and registers stay those of a kernel without it (measured: the
+// runtime-branch form slowed every GEMM of the step, 14.15-14.24 vs 13.90-13.94 ms/step with no statistics in use).
+template <int TBN = BN, bool XCOL = false, int TBM = BM, int NJ = TBN / 32, int NTH = NT, bool GNE = false>
 __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][NJ], char* smem, int m0, int n0,
                                               int wm, int wn, int lane, int z) {
   // Stage the fp32 tile through LDS in 64-row parts; each thread then owns runs of 8 consecutive columns of one
@@ -422,7 +385,7 @@ __device__ __forceinline__ void gemm_epilogue(const EpiArgs& e, f32x4 (&acc)[4][
       }
     }
     __syncthreads();
-    if (e.gn_part && !e.raw) {  // GroupNorm-backward statistics path (plain epilogue, checked on the host)
+    if constexpr (GNE) {  // GroupNorm statistics (plain bf16 epilogue, checked on the host)
       epi_gn_half<TBN, NTH>(e, st, st + 64 * SROW, m0 + half * 64, n0);
       continue;
     }
@@ -509,7 +472,7 @@ __device__ __forceinline__ TileId tile_id() {
 
 // RED (col-major A only): 0 plain GEMM, 1 + VALU row sums of A (bias gradient), 2 + synthesised reduction columns
 // (bias and per-group sums) -- compile-time so the plain instantiations carry none of it
-template <int AM, int BMODE, int RED = 0>
+template <int AM, int BMODE, int RED = 0, bool GNE = false>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs e) {
   __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
   // buffer b: A tile at smem + 2*b*TILE_BYTES, B tile right after it
@@ -766,7 +729,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args g, const EpiArgs
     __syncthreads();
   }
 
-  gemm_epilogue<BN, RED == 2>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
+  gemm_epilogue<BN, RED == 2, BM, BN / 32, NT, GNE>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -877,7 +840,8 @@ __device__ __forceinline__ s16x8 reduce_frag(const Args& g, int r, int kb, int l
 
 // KBK: k depth of one staged tile (64, or 32 for deeper rings in the same LDS: more bytes in flight per CU). Split-K
 // slices stay in units of 64 (host k-tiles).
-template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0, int KBK = BK>
+template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0, int KBK = BK,
+          bool GNE = false>
 __global__ __launch_bounds__((dma_threads<TBM, NWN>()),
                              ((dma_threads<TBM, NWN>() == 256 && STAGES * (TBM + TBN) * KBK * 2 <= 80 * 1024) ? 2 : 1))
 void gemm_dma_kernel(const Args g, const EpiArgs e) {
@@ -1225,7 +1189,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
         }
     }
   }
-  gemm_epilogue<TBN, false, TBM, NJ, NTH>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
+  gemm_epilogue<TBN, false, TBM, NJ, NTH, GNE>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
 }
 
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
@@ -1301,7 +1265,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_gn_kernel(const EpiArgs e) 
     float4 tb[8];
     const float4* tp = e.gn_tab + (long long)b * e.N + col;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) tb[q] = e.gn_fwd ? make_float4(0.f, 0.f, 0.f, 0.f) : tp[q];
+    for (int q = 0; q < 8; ++q) tb[q] = tp[q];
     const int zs = (int)e.split_stride;
 #pragma unroll 1
     for (int rl = rl0; rl < e.gn_rb; rl += 8) {
@@ -1328,18 +1292,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_gn_kernel(const EpiArgs e) 
         }
       }
       float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-      if (e.gn_fwd) {
-        values8(e, row, col, v);
-        const uint4 pk = pack8(v);
-        *(uint4*)((bf16_t*)e.C + (long long)row * e.ldc + col) = pk;
-        unpack8(pk, v);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          u[q] += v[q];
-          w[q] = fmaf(v[q], v[q], w[q]);
-        }
-        continue;
-      }
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] *= e.alpha;
       const uint4 xr = *(const uint4*)(e.gn_x + (long long)row * e.gn_ldx + col);
@@ -1503,10 +1455,17 @@ template <int AM, int BMODE, int STAGES, int TBN, int TBM, int NWN, int RED, int
 hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
   constexpr int NTH = dma_threads<TBM, NWN>();
   constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * KBK * 2, epi = (size_t)64 * (TBN + 4) * 4;
-  // GroupNorm-backward statistics: the row-lane sums (NTH / (TBN / 8) x TBN x 2 floats) after the staged tile
-  const size_t epi_gn = epi + (size_t)(NTH / (TBN / 8)) * TBN * 2 * 4;
-  const size_t need = std::max(ring, (e.gn_part && !e.raw) ? epi_gn : epi);
-  sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid, dim3(NTH), need, s, a, e);
+  if constexpr (RED == 0 && AM != SDMI_A_COLMAJOR && BMODE != SDMI_B_KN_CONV) {
+    if (e.gn_part && !e.raw) {  // GroupNorm statistics: + the row-lane sums (NTH / (TBN / 8) x TBN x 2 floats)
+      const size_t epi_gn = epi + (size_t)(NTH / (TBN / 8)) * TBN * 2 * 4;
+      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, 0, KBK, true>), grid, dim3(NTH),
+                      std::max(ring, epi_gn), s, a, e);
+      return hipGetLastError();
+    }
+  }
+  if (e.gn_part && !e.raw) return hipErrorInvalidValue;
+  sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid, dim3(NTH), std::max(ring, epi), s,
+                  a, e);
   return hipGetLastError();
 }
 
@@ -1551,6 +1510,13 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, i
         return hipGetLastError();
       }
     }
+    if constexpr (AM != SDMI_A_COLMAJOR && BMODE != SDMI_B_KN_CONV) {
+      if (e.gn_part && !e.raw) {
+        sdmi_rt::launch((gemm_kernel<AM, BMODE, 0, true>), grid, dim3(NT), 0, s, a, e);
+        return hipGetLastError();
+      }
+    }
+    if (e.gn_part && !e.raw) return hipErrorInvalidValue;
     sdmi_rt::launch((gemm_kernel<AM, BMODE>), grid, dim3(NT), 0, s, a, e);
     return hipGetLastError();
   }
@@ -1639,14 +1605,13 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
           (!d->bias2 || (uintptr_t)d->bias2 % 16 == 0) && (!d->resid || (uintptr_t)d->resid % 16 == 0) &&
           (!d->rowbias || (uintptr_t)d->rowbias % 16 == 0) &&
           (d->act != 3 || (d->ld_aux % 8 == 0 && (uintptr_t)d->aux % 16 == 0));
-  if (d->gn_part) {  // GroupNorm statistics: bf16 epilogue, whole segments inside one sample
-    if ((!d->gn_fwd && (!d->gn_x || !d->gn_tab)) || d->gn_P <= 0 || d->m % d->gn_P ||
-        (d->gn_rb != 16 && d->gn_rb != 32 && d->gn_rb != 64) || d->gn_P % d->gn_rb || d->gn_P >= (1 << 24))
+  if (d->gn_part) {  // GroupNorm-backward statistics: plain bf16 epilogue, whole segments inside one sample
+    if (!d->gn_x || !d->gn_tab || d->gn_P <= 0 || d->m % d->gn_P || (d->gn_rb != 16 && d->gn_rb != 32 && d->gn_rb != 64) ||
+        d->gn_P % d->gn_rb || d->gn_P >= (1 << 24))
       return -20;
-    // backward statistics: plain epilogue; forward statistics: bias / bias2 / rowbias / resid allowed
-    if ((!d->gn_fwd && (d->bias || d->bias2 || d->rowbias || d->resid)) || d->act || d->remap || d->perm ||
-        has_reductions(d) || d->c_f32 || !e.vec || e.m_store != d->m || e.n_store != d->n || (uintptr_t)d->gn_part % 8 ||
-        (!d->gn_fwd && (d->gn_ldx % 8 || (uintptr_t)d->gn_x % 16 || (uintptr_t)d->gn_tab % 16)))
+    if (d->bias || d->bias2 || d->rowbias || d->resid || d->act || d->remap || d->perm || has_reductions(d) || d->c_f32 ||
+        !e.vec || e.m_store != d->m || e.n_store != d->n || (uintptr_t)d->gn_part % 8 || d->gn_ldx % 8 ||
+        (uintptr_t)d->gn_x % 16 || (uintptr_t)d->gn_tab % 16)
       return -21;
     e.gn_x = (const bf16_t*)d->gn_x;
     e.gn_ldx = d->gn_ldx;
@@ -1654,7 +1619,6 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
     e.gn_part = d->gn_part;
     e.gn_rb = d->gn_rb;
     e.gn_silu = d->gn_silu;
-    e.gn_fwd = d->gn_fwd;
     e.gn_pd = FastDiv::make(d->gn_P);
   }
   return 0;

@@ -791,72 +791,41 @@ __global__ __launch_bounds__(NT) void gn_bwd_apply_kernel(ApplyArgs a) {
   }
 }
 
-// GroupNorm (+SiLU) forward from the producing GEMM's statistics (sdmi_gemm_desc::gn_part with gn_fwd): grid (strips
-// of whole groups, B, pixel splits). Every workgroup sums the P / rb segment partials {sum x, sum x^2} of its (batch
-// row, strip) in segment order, merges each group in double exactly as gn_fwd_pass_kernel does, and streams
-// y = act(x * a + s) over its pixel range; the pixel-split-0 workgroups write the forward table {a, s, mean, rstd}.
-__global__ __launch_bounds__(NT) void gn_fwd_part_kernel(StripArgs a, const float2* part, int rb, bf16_t* y, int ldy) {
-  __shared__ float s1[NT], s2[NT];
-  __shared__ float2 grp[NT];
-  const int strip = blockIdx.x, b = blockIdx.y;
-  const int c0 = strip * a.CW, cw = min(a.CW, a.C - c0);
-  const int t = threadIdx.x, Cg = a.C / a.G;
-  const int nseg = a.P / rb;
-  for (int ch = t; ch < cw; ch += NT) {
-    const float2* pp = part + (long long)b * nseg * a.C + c0 + ch;
-    float x1 = 0.f, x2 = 0.f;
+// s1[ch], s2[ch] (ch < cw <= NT) = the sums over the nseg segment partials {sum, sum2} of (batch row b, channel
+// c0 + ch) for gn_bwd_part_kernel. Each thread loads two channels (16 B) of every SLN-th segment -- SLN = NT / (cw / 2)
+// segment lanes (<= 4), all loads of a lane independent -- and the lanes are merged in lane order: a fixed summation
+// order (deterministic) with nseg / SLN loads per thread instead of nseg.
+__device__ __forceinline__ void part_sums(const float2* part, int b, int nseg, int C, int c0, int cw, float* s1,
+                                          float* s2, float* p1, float* p2) {
+  const int t = threadIdx.x, hc = cw >> 1, sln = min(NT / hc, 4), c2 = t % hc, sl = t / hc;
+  if (sl < sln) {
+    const float4* pp = (const float4*)(part + (long long)b * nseg * C + c0) + c2;
+    const long long ld4 = C >> 1;
+    float x1 = 0.f, x2 = 0.f, y1 = 0.f, y2 = 0.f;
 #pragma unroll 8
-    for (int j = 0; j < nseg; ++j) {
-      const float2 v = pp[(long long)j * a.C];
+    for (int j = sl; j < nseg; j += sln) {
+      const float4 v = pp[(long long)j * ld4];
       x1 += v.x;
       x2 += v.y;
+      y1 += v.z;
+      y2 += v.w;
     }
-    s1[ch] = x1;
-    s2[ch] = x2;
+    p1[sl * cw + 2 * c2] = x1;
+    p2[sl * cw + 2 * c2] = x2;
+    p1[sl * cw + 2 * c2 + 1] = y1;
+    p2[sl * cw + 2 * c2 + 1] = y2;
   }
   __syncthreads();
-  const int ng = cw / Cg;
-  for (int gi = t; gi < ng; gi += NT) {
-    double m1 = 0, m2 = 0;
-    for (int c = gi * Cg; c < (gi + 1) * Cg; ++c) { m1 += s1[c]; m2 += s2[c]; }
-    const double n = (double)a.P * Cg, mu = m1 / n;
-    double var = m2 / n - mu * mu;
-    if (var < 0) var = 0;
-    grp[gi] = make_float2((float)mu, (float)(1.0 / sqrt(var + (double)a.eps)));
+  for (int c = t; c < cw; c += NT) {
+    float a1 = 0.f, a2 = 0.f;
+    for (int l = 0; l < sln; ++l) {
+      a1 += p1[l * cw + c];
+      a2 += p2[l * cw + c];
+    }
+    s1[c] = a1;
+    s2[c] = a2;
   }
   __syncthreads();
-  if (blockIdx.z == 0) {
-    for (int ch = t; ch < cw; ch += NT) {
-      const int c = c0 + ch;
-      const float2 mr = grp[ch / Cg];
-      const float sc = mr.y * a.gamma[c];
-      a.out_tab[(long long)b * a.C + c] = make_float4(sc, a.beta[c] - mr.x * sc, mr.x, mr.y);
-    }
-  }
-  const int L = cw >> 3, R = NT / L, lane = t % L, r = t / L;
-  if (r >= R) return;
-  const int cc = c0 + lane * 8;
-  float ta[8], ts[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float2 mr = grp[(lane * 8 + e) / Cg];
-    ta[e] = mr.y * a.gamma[cc + e];
-    ts[e] = a.beta[cc + e] - mr.x * ta[e];
-  }
-  const int per = (a.P + gridDim.z - 1) / gridDim.z;
-  const int p0 = blockIdx.z * per, p1 = min(a.P, p0 + per);
-  const long long rbase = (long long)b * a.P;
-#pragma unroll 4
-  for (int p = p0 + r; p < p1; p += R) {
-    float xv[8], o[8];
-    unpack8(*(const uint4*)(a.x + (rbase + p) * a.ldx + cc), xv);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float z = fmaf(xv[e], ta[e], ts[e]);
-      o[e] = a.silu ? silu_f(z) : z;
-    }
-    *(uint4*)(y + (rbase + p) * ldy + cc) = pack8(o);
-  }
 }
 
 // GroupNorm (+SiLU) backward from the producing GEMM's statistics (sdmi_gemm_desc::gn_part): grid (strips of whole
@@ -867,27 +836,14 @@ __global__ __launch_bounds__(NT) void gn_fwd_part_kernel(StripArgs a, const floa
 // arrivals per strip sums them (batch_tail).
 __global__ __launch_bounds__(NT) void gn_bwd_part_kernel(StripArgs a, const float2* part, int rb, bf16_t* dx, int lddx,
                                                          const bf16_t* add, int ldadd) {
-  __shared__ float s1[NT], s2[NT];
+  __shared__ float s1[NT], s2[NT], q1[2 * NT], q2[2 * NT];
   __shared__ float2 grp[NT];
   __shared__ float4 stb[NT];
   const int strip = blockIdx.x, b = blockIdx.y;
   const int c0 = strip * a.CW, cw = min(a.CW, a.C - c0);
   const int t = threadIdx.x, Cg = a.C / a.G;
-  const int nseg = a.P / rb;
-  for (int ch = t; ch < cw; ch += NT) {
-    stb[ch] = a.tab[(long long)b * a.C + c0 + ch];
-    const float2* pp = part + (long long)b * nseg * a.C + c0 + ch;
-    float x1 = 0.f, x2 = 0.f;
-#pragma unroll 8
-    for (int j = 0; j < nseg; ++j) {
-      const float2 v = pp[(long long)j * a.C];
-      x1 += v.x;
-      x2 += v.y;
-    }
-    s1[ch] = x1;
-    s2[ch] = x2;
-  }
-  __syncthreads();
+  for (int ch = t; ch < cw; ch += NT) stb[ch] = a.tab[(long long)b * a.C + c0 + ch];
+  part_sums(part, b, a.P / rb, a.C, c0, cw, s1, s2, q1, q2);
   const int ng = cw / Cg;
   const float inv_n = 1.0f / ((float)a.P * Cg);
   for (int gi = t; gi < ng; gi += NT) {
@@ -925,7 +881,7 @@ __global__ __launch_bounds__(NT) void gn_bwd_part_kernel(StripArgs a, const floa
     const int per = (a.P + gridDim.z - 1) / gridDim.z;
     const int p0 = blockIdx.z * per, p1 = min(a.P, p0 + per);
     const long long rbase = (long long)b * a.P;
-#pragma unroll 2
+#pragma unroll 4
     for (int p = p0 + r; p < p1; p += R) {
       const long long row = rbase + p;
       float xv[8], gv[8], av[8], ov[8];
@@ -966,6 +922,15 @@ int strip_width(int C, int unit) {
   int cw = unit;
   while (cw % 8 || (cw < 64 && cw * 2 <= C)) cw += unit;
   while ((C + cw - 1) / cw > SLOT_CTRS) cw += unit;
+  return cw;
+}
+
+// Strip width of the streaming gn_bwd_part_kernel: whole groups AND a multiple of 64 channels (128-B row segments, so no
+// cache line is shared by two strips' workgroups), else the whole row -- e.g. C = 384 in 32 groups: 192, not 72
+int part_strip_width(int C, int unit) {
+  int cw = unit;
+  while (cw % 64 && cw < C) cw += unit;
+  if (cw > C || cw > NT) cw = strip_width(C, unit);
   return cw;
 }
 
@@ -1085,25 +1050,6 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   return 0;
 }
 
-// GroupNorm (+SiLU) forward from the producing GEMM's segment statistics (sdmi_gemm_desc::gn_part, gn_fwd = 1)
-extern "C" int sdmi_gn_fwd_part(const void* x, int ldx, void* y, int ldy, int B, int P, int C, int G, float eps,
-                                const float* gamma, const float* beta, int silu, const float* part, int rb,
-                                float* table, sdmi_stream_t stream) {
-  if (C % 8 || G <= 0 || C % G || B <= 0 || P <= 0 || rb <= 0 || P % rb || !part || ldx % 8 || ldy % 8) return -1;
-  StripArgs a = {};
-  a.x = (const bf16_t*)x; a.ldx = ldx; a.B = B; a.P = P; a.C = C; a.G = G; a.eps = eps; a.silu = silu;
-  a.gamma = gamma; a.beta = beta; a.out_tab = (float4*)table;
-  a.CW = strip_width(C, C / G);
-  const int nch = (C + a.CW - 1) / a.CW;
-  if (a.CW > NT) return -2;
-  int ps = 1;
-  while ((long long)nch * B * ps < 1024 && P / (ps * 2) >= 64) ps *= 2;
-  sdmi_rt::launch(gn_fwd_part_kernel, dim3(nch, B, ps), dim3(NT), 0, (hipStream_t)stream, a, (const float2*)part, rb,
-                  (bf16_t*)y, ldy);
-  SDMI_CHECK_LAUNCH();
-  return 0;
-}
-
 // GroupNorm backward from the dgrad GEMM's segment partials (sdmi_gemm_desc::gn_part, rb rows per segment)
 extern "C" int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
                                 const float* gamma, int B, int P, int C, int G, int silu, const float* part, int rb,
@@ -1116,7 +1062,7 @@ extern "C" int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy
   r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy; r.tab = (const float4*)table;
   r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.gamma = gamma;
   r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
-  r.CW = strip_width(C, C / G);
+  r.CW = part_strip_width(C, C / G);
   const int nch = (C + r.CW - 1) / r.CW;
   if (r.CW > NT || nch > BATCH_CTR) return -2;
   if (dgamma && !(r.ctr = counter_slot())) return -4;

@@ -21,50 +21,80 @@ constexpr int NORM_BLOCKS = 2048;
 // the same partial array -- and norm_finalize_kernel sums it in index order: bitwise the same norm for any split.
 constexpr long long NORM_BLK = 1 << 17;
 
-__global__ __launch_bounds__(NT) void sumsq_block_kernel(const float* g, long long n, float* partial) {
-  const long long b0 = (long long)blockIdx.x * NORM_BLK;
-  const long long e = n - b0 < NORM_BLK ? n - b0 : NORM_BLK;
-  const float* gb = g + b0;
-  float acc = 0.f;
-  const long long e4 = e / 4;
-  for (long long i = threadIdx.x; i < e4; i += NT) {
-    const float4 v = ((const float4*)gb)[i];
-    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-  }
-  for (long long i = e4 * 4 + threadIdx.x; i < e; i += NT) acc += gb[i] * gb[i];
-  __shared__ float red[NT / 64];
+// one 1024-thread workgroup per block: each thread sums its float4s (index t, t + 1024, ...) eight loads at a time in a
+// fixed order, then the wave trees and the 16 waves in order (the same order for a block wherever it is summed)
+constexpr int NTN = 1024;
+
+__device__ __forceinline__ float sq4(const float4 v) { return v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w; }
+
+__device__ __forceinline__ void block_partial(float acc, float* partial) {
+  __shared__ float red[NTN / 64];
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NTN / 64; ++w) s += red[w];
+    *partial = s;
+  }
+}
+
+__global__ __launch_bounds__(NTN) void sumsq_block_kernel(const float* g, long long n, float* partial) {
+  const long long b0 = (long long)blockIdx.x * NORM_BLK;
+  const int e = (int)(n - b0 < NORM_BLK ? n - b0 : NORM_BLK);
+  const float4* gb = (const float4*)(g + b0);
+  const int e4 = e / 4;
+  float acc = 0.f;
+  int i = threadIdx.x;
+  for (; i + 7 * NTN < e4; i += 8 * NTN) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = gb[i + k * NTN];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += sq4(v[k]);
+  }
+  for (; i < e4; i += NTN) acc += sq4(gb[i]);
+  for (int j = e4 * 4 + threadIdx.x; j < e; j += NTN) acc += g[b0 + j] * g[b0 + j];
+  block_partial(acc, partial + blockIdx.x);
 }
 
 // the bf16 gradient wire: dst[i] = float(src[i]) (exact) and, when partial != null, the block sums of squares of dst
-__global__ __launch_bounds__(NT) void widen_sumsq_kernel(const bf16_t* src, float* dst, long long n, float* partial) {
+// (sumsq_block_kernel's order)
+__device__ __forceinline__ float4 widen4(const uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+__global__ __launch_bounds__(NTN) void widen_sumsq_kernel(const bf16_t* src, float* dst, long long n, float* partial) {
   const long long b0 = (long long)blockIdx.x * NORM_BLK;
-  const long long e = n - b0 < NORM_BLK ? n - b0 : NORM_BLK;
-  const bf16_t* sb = src + b0;
-  float* db = dst + b0;
+  const int e = (int)(n - b0 < NORM_BLK ? n - b0 : NORM_BLK);
+  const uint2* sb = (const uint2*)(src + b0);
+  float4* db = (float4*)(dst + b0);
+  const int e4 = e / 4;
   float acc = 0.f;
-  const long long e4 = e / 4;
-  for (long long i = threadIdx.x; i < e4; i += NT) {
-    const uint2 u = ((const uint2*)sb)[i];
-    const float4 v = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                                 __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-    ((float4*)db)[i] = v;
-    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  int i = threadIdx.x;
+  for (; i + 7 * NTN < e4; i += 8 * NTN) {
+    float4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = widen4(sb[i + k * NTN]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      db[i + k * NTN] = v[k];
+      acc += sq4(v[k]);
+    }
   }
-  for (long long i = e4 * 4 + threadIdx.x; i < e; i += NT) {
-    const float v = bf2f(sb[i]);
+  for (; i < e4; i += NTN) {
+    const float4 v = widen4(sb[i]);
     db[i] = v;
+    acc += sq4(v);
+  }
+  for (int j = e4 * 4 + threadIdx.x; j < e; j += NTN) {
+    const float v = bf2f(src[b0 + j]);
+    dst[b0 + j] = v;
     acc += v * v;
   }
-  if (!partial) return;
-  __shared__ float red[NT / 64];
-  acc = wave_sum(acc);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (partial) block_partial(acc, partial + blockIdx.x);
 }
 
 // state layout (fp32 unless noted): [0] grad norm (unscaled)  [1] clip coefficient * inv_scale
@@ -203,7 +233,7 @@ extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm
   const long long nb = (n + NORM_BLK - 1) / NORM_BLK;
   if (nb > NORM_BLOCKS) return -3;  // > 268 M parameters: sdmi_sumsq_blocks into a larger partial array instead
   hipStream_t s = (hipStream_t)stream;
-  sdmi_rt::launch(sumsq_block_kernel, dim3((unsigned)nb), dim3(NT), 0, s, grads, n, ws);
+  sdmi_rt::launch(sumsq_block_kernel, dim3((unsigned)nb), dim3(NTN), 0, s, grads, n, ws);
   SDMI_CHECK_LAUNCH();
   sdmi_rt::launch(norm_finalize_kernel, dim3(1), dim3(NT), 0, s, ws, (int)nb, max_norm, state, growth_interval,
                      skip_if_loss_nonfinite, grad_div);
@@ -214,7 +244,7 @@ extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm
 extern "C" int sdmi_sumsq_blocks(const float* grads, long long n, float* partial, sdmi_stream_t stream) {
   if (!grads || !partial || n < 0 || ((uintptr_t)grads & 15)) return -1;
   if (n == 0) return 0;
-  sdmi_rt::launch(sumsq_block_kernel, dim3((unsigned)((n + NORM_BLK - 1) / NORM_BLK)), dim3(NT), 0,
+  sdmi_rt::launch(sumsq_block_kernel, dim3((unsigned)((n + NORM_BLK - 1) / NORM_BLK)), dim3(NTN), 0,
                   (hipStream_t)stream, grads, n, partial);
   SDMI_CHECK_LAUNCH();
   return 0;
@@ -223,7 +253,7 @@ extern "C" int sdmi_sumsq_blocks(const float* grads, long long n, float* partial
 extern "C" int sdmi_widen_bf16_sumsq(const void* src, float* dst, long long n, float* partial, sdmi_stream_t stream) {
   if (!src || !dst || n < 0 || ((uintptr_t)src & 7) || ((uintptr_t)dst & 15)) return -1;
   if (n == 0) return 0;
-  sdmi_rt::launch(widen_sumsq_kernel, dim3((unsigned)((n + NORM_BLK - 1) / NORM_BLK)), dim3(NT), 0,
+  sdmi_rt::launch(widen_sumsq_kernel, dim3((unsigned)((n + NORM_BLK - 1) / NORM_BLK)), dim3(NTN), 0,
                   (hipStream_t)stream, (const bf16_t*)src, dst, n, partial);
   SDMI_CHECK_LAUNCH();
   return 0;

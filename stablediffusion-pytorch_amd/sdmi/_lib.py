@@ -48,7 +48,7 @@ class GemmDesc(ctypes.Structure):
         ("gn_x", ctypes.c_void_p), ("gn_ldx", ctypes.c_int),
         ("gn_tab", ctypes.c_void_p),
         ("gn_part", ctypes.c_void_p),
-        ("gn_P", ctypes.c_int), ("gn_rb", ctypes.c_int), ("gn_silu", ctypes.c_int), ("gn_fwd", ctypes.c_int),
+        ("gn_P", ctypes.c_int), ("gn_rb", ctypes.c_int), ("gn_silu", ctypes.c_int),
     ]
 
 
@@ -91,7 +91,6 @@ SIGNATURES = {
     "sdmi_gn_apply": ([_P, _I, _P, _I, _P, _I, _I, _I, _I, _P], _I),
     "sdmi_gn_fwd": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _P, _P], _I),
     "sdmi_gn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P], _I),
-    "sdmi_gn_fwd_part": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _I, _P, _P], _I),
     "sdmi_gn_bwd_part": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P], _I),
     "sdmi_chan_sum": ([_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _I, _P], _I),
     "sdmi_prep_input": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),

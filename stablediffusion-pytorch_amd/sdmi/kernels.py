@@ -148,11 +148,8 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
             d.gsum_out, d.gsum_ld, d.sum_group = gsum.data_ptr(), ld_of(gsum), sum_group
     d.tile_n_hint = 0 if (not PHASE or PHASE in TILE192_PHASES) else 128
     if gn is not None:
-        if gn.get("fwd"):
-            d.gn_fwd = 1
-        else:
-            d.gn_x, d.gn_ldx = gn["x"].data_ptr(), ld_of(gn["x"])
-            d.gn_tab = gn["tab"].data_ptr()
+        d.gn_x, d.gn_ldx = gn["x"].data_ptr(), ld_of(gn["x"])
+        d.gn_tab = gn["tab"].data_ptr()
         d.gn_P, d.gn_silu = gn["P"], 1 if gn.get("silu") else 0
         d.gn_rb = gn_rb(gn["P"], 64)
         d.gn_part = 8  # validated by the plan; the real buffer once the split count (and so the segment) is known
@@ -371,16 +368,9 @@ def gn_stats(x, B, P, C, G, gamma, beta, eps=1e-5):
     return tab
 
 
-def gn_fwd(x, B, P, C, G, gamma, beta, silu, out, eps=1e-5, gn=None):
-    """out = [SiLU](GroupNorm(x)); returns the forward table (as gn_stats) for the backward pass. gn: the forward
-    statistics request whose GEMM produced x (gn_request_fwd): one streaming launch (sdmi_gn_fwd_part)."""
+def gn_fwd(x, B, P, C, G, gamma, beta, silu, out, eps=1e-5):
+    """out = [SiLU](GroupNorm(x)); returns the forward table (as gn_stats) for the backward pass."""
     L = _lib.lib()
-    if gn is not None and gn.get("part") is not None:
-        tab = torch.empty(B * C * 4, dtype=torch.float32, device=x.device)
-        with _Prof("gn_fwd", 0, f"B={B} P={P} C={C} part"):
-            check(L.sdmi_gn_fwd_part(_p(x), ld_of(x), _p(out), ld_of(out), B, P, C, G, eps, _p(gamma), _p(beta),
-                                     1 if silu else 0, _p(gn["part"]), gn["rb"], _p(tab), _stream()), "sdmi_gn_fwd_part")
-        return tab
     ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=x.device)
     tab = torch.empty(B * C * 4, dtype=torch.float32, device=x.device)
     with _Prof("gn_fwd", 0, f"B={B} P={P} C={C}"):
@@ -410,14 +400,6 @@ def gn_request(x, tab, P, C, silu):
     if P % 16 or C % 8 or ld_of(x) % 8:
         return None
     return dict(x=x, tab=tab, P=P, silu=silu)
-
-
-def gn_request_fwd(P, C):
-    """GroupNorm-forward statistics request for the GEMM producing a GroupNorm input (gemm(gn=...)): the launch writes
-    {sum x, sum x^2} per segment and column of its stored outputs; gn_fwd(gn=...) then normalises in one pass."""
-    if P % 16 or C % 8:
-        return None
-    return dict(fwd=True, P=P)
 
 
 def gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, silu, dgamma, dbeta, addend=None, gn=None):

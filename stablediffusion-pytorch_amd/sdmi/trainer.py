@@ -170,6 +170,21 @@ class DDPMTrainer:
             if self.engine.pack.late_chunk is not None:
                 plan.record_event(self.late_event, side)
                 self.engine._pending[self.engine.pack.late_chunk] = self.late_event
+        # The optimizer chunks (and the weight-gradient / norm / reducer streams) keep using the persistent buffers
+        # after step() returns; marking them used on those streams makes the caching allocator hold their memory until
+        # that work has finished when the trainer is dropped (no reuse by a later allocation while a chunk still runs).
+        if self.device.type == "cuda":
+            streams = list(getattr(self.engine, "sides", None) or [])
+            if self.norm_parts is not None:
+                streams.append(self.norm_parts.stream)
+            if self.reducer is not None and getattr(self.reducer, "stream", None) is not None:
+                streams.append(self.reducer.stream)
+            bufs = [self.store.params, self.store.grads, self.m, self.v, self.ema, self.state,
+                    getattr(getattr(self.engine, "pack", None), "buf", None)]
+            for b in bufs:
+                if b is not None:
+                    for s in streams:
+                        b.record_stream(s)
 
     # ------------------------------------------------------------------------------------------
     def _watermarks(self, tape):

@@ -24,6 +24,16 @@ from . import _lib
 from . import kernels as K
 from . import plan
 
+# GroupNorm-backward statistics from the producing data-gradient GEMM: used where a sample has >= GN_FUSE_MIN_P pixels
+# (the 32^2 level of the CelebHQ latents). Same-box A/B of the cond-UNet step (scripts/gpu_bisect.sh): every level
+# 13.94 / 13.90, P >= 1024 13.89 / 13.89, none 13.98 / 13.99 ms -- at 16^2 and below the statistics epilogue and the
+# statistics reducer cost more than the standalone single-pass GroupNorm they replace.
+GN_FUSE_MIN_P = 1024
+
+
+def _gn_req(x, tab, P, C, silu):
+    return K.gn_request(x, tab, P, C, silu) if P >= GN_FUSE_MIN_P else None
+
 
 def layout(cfg):
     down = list(cfg["down_channels"])
@@ -324,10 +334,10 @@ class UNetEngine:
         # the cross-attention context branch runs ahead of the forward on a stream of its own
         self.ctx_stream = torch.cuda.Stream(device=self.device) if use_side else None
         self._keep = []
-        # linear data gradients from transposed packed weights (B_NK: the forward GEMM's wider tiles). Off by
-        # default here: the data-gradient GEMMs gain 0.2 ms in isolation but the overlapped step measures
-        # +0.04 ms (same-box A/B); the DiT engine, without a weight-gradient stream, gains 3.5 %.
-        self.dgrad_t = False
+        # linear data gradients from transposed packed weights: B_NK GEMMs, which the deep-ring 64-row mainloops of
+        # the 8^2 / 4^2 levels take (round 2, before those mainloops: +0.04 ms/step; round 4 with the shapes tuned:
+        # -0.14 ms/step, same-box A/B)
+        self.dgrad_t = True
         self._build_pack()
 
     # ------------------------------------------------------------------------------------------
@@ -509,7 +519,6 @@ class UNetEngine:
         K.PHASE = "fwd"
         tape = Tape()
         st = dict(B=B, H=H, W=W)
-        self._fstats = {}
         grads = Grads(dev)
         self._grads = grads
         x = plan.as_operand(x)
@@ -680,8 +689,7 @@ class UNetEngine:
         C = L["conv_out"]
         Pn = H * W
         hs = self._new(B * Pn, C)
-        tab = K.gn_fwd(cur, B, Pn, C, G, P["norm_out.weight"], P["norm_out.bias"], True, hs, gn=self._fstat_take(cur))
-        self._fstats = {}
+        tab = K.gn_fwd(cur, B, Pn, C, G, P["norm_out.weight"], P["norm_out.bias"], True, hs)
         pred = self._new(B * Pn, 8, torch.float32)
         K.conv_fwd(hs, B, H, W, C, C, self.W("conv_out#f"), 8, 3, 3, 1, 1, pred, 8, bias=P["conv_out.bias"],
                    n_store=self.im_channels)
@@ -789,39 +797,24 @@ class UNetEngine:
             grads.declare(oname, y.shape[0], y.shape[1])
         return y, oname
 
-    # ---- GroupNorm-forward statistics from the producing GEMMs ------------------------------------------
-    # A module output y that the next module normalises gets its {sum x, sum x^2} segment statistics from the GEMM
-    # that writes it (kernels.gn_request_fwd); the consuming GroupNorm then runs as one streaming pass. The registry
-    # holds the tensor itself and matches by identity, so a statistic is never applied to other data.
-    def _fstat_req(self, y, P, C):
-        r = K.gn_request_fwd(P, C) if y.shape[1] == C else None
-        if r is not None:
-            self.__dict__.setdefault("_fstats", {})[id(y)] = (y, r)
-        return r
-
-    def _fstat_take(self, x):
-        e = self.__dict__.setdefault("_fstats", {}).pop(id(x), None)
-        return e[1] if e is not None and e[0] is x else None
-
     # ---- resnet ----------------------------------------------------------------------------------
     def _resnet_fwd(self, p, l, cin, cout, x, xname, out, oname, B, h, w, st, tape):
         P, G = self.P, self.L["G"]
         Pn = h * w
         a, b = f"{p}.resnet_conv_first.{l}", f"{p}.resnet_conv_second.{l}"
         h0 = self._new(B * Pn, cin)
-        t1 = K.gn_fwd(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"], True, h0, gn=self._fstat_take(x))
+        t1 = K.gn_fwd(x, B, Pn, cin, G, P[a + ".0.weight"], P[a + ".0.bias"], True, h0)
         h1 = self._new(B * Pn, cout)
         off = self.temb_off.get((p, l))  # None: no time embedding (the VQVAE's blocks, t_emb_dim=None)
-        g2 = K.gn_request_fwd(Pn, cout)  # the second GroupNorm's statistics from the first conv's epilogue
         K.conv_fwd(h0, B, h, w, cin, cin, self.W(a + ".2#f"), cout, 3, 3, 1, 1, h1, cout, bias=P[a + ".2.bias"],
-                   rowbias=st["temb_all"][:, off:] if off is not None else None, rb_ld=self.temb_total, gn=g2)
+                   rowbias=st["temb_all"][:, off:] if off is not None else None, rb_ld=self.temb_total)
         h2 = self._new(B * Pn, cout)
-        t2 = K.gn_fwd(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"], True, h2, gn=g2)
+        t2 = K.gn_fwd(h1, B, Pn, cout, G, P[b + ".0.weight"], P[b + ".0.bias"], True, h2)
         rc = f"{p}.residual_input_conv.{l}"
         y = out if out is not None else self._new(B * Pn, cout)
         # conv2(h2) + residual 1x1(x) in ONE GEMM: A = [im2col(h2) | x], B = [W2 | Wr]
         K.conv_fwd(h2, B, h, w, cout, cout, self.W(f"{p}.res{l}#cat"), cout, 3, 3, 1, 1, y, K.ld_of(y),
-                   bias=P[b + ".2.bias"], x2=x, cin2=cin, bias2=P[rc + ".bias"], gn=self._fstat_req(y, Pn, cout))
+                   bias=P[b + ".2.bias"], x2=x, cin2=cin, bias2=P[rc + ".bias"])
         tape.append((self._resnet_bwd, dict(p=p, l=l, cin=cin, cout=cout, x=x, xn=xname, yn=oname, h0=h0, h1=h1, h2=h2,
                                             t1=t1, t2=t2, B=B, h=h, w=w)))
         return y
@@ -842,7 +835,7 @@ class UNetEngine:
         self._wgrad_linear(dy, c["x"], self.g(rc + ".weight").view(cout, cin))
         dh2 = self._new(B * Pn, cout)
         # the GroupNorm backward's reductions come out of the data-gradient GEMM that produces its input gradient
-        g2 = K.gn_request(c["h1"], c["t2"], Pn, cout, True)
+        g2 = _gn_req(c["h1"], c["t2"], Pn, cout, True)
         K.conv_fwd(dy, B, h, w, cout, ldy, self.W(b + ".2#d"), cout, 3, 3, 1, 1, dh2, cout, gn=g2)
         dx, fresh = grads.get(c["xn"])
         if self.dgrad_t:
@@ -860,7 +853,7 @@ class UNetEngine:
                          bias_grad2=self.g(f"{p}.t_emb_layers.{l}.1.bias") if off is not None else None,
                          group_sums=self.dtemb_all[:, off:off + cout] if off is not None else None)
         dh0 = self._new(B * Pn, cin)
-        g1 = K.gn_request(c["x"], c["t1"], Pn, cin, True)
+        g1 = _gn_req(c["x"], c["t1"], Pn, cin, True)
         K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin, gn=g1)
         K.gn_bwd(c["x"], dh0, dx, c["t1"], P[a + ".0.weight"], B, Pn, cin, G, True,
                  self.g(a + ".0.weight"), self.g(a + ".0.bias"), addend=dx, gn=g1)
@@ -872,7 +865,7 @@ class UNetEngine:
         nk = f"{p}.cross_attention_norms.{l}" if cross else f"{p}.attention_norms.{l}"
         mk = f"{p}.cross_attentions.{l}" if cross else f"{p}.attentions.{l}"
         a = self._new(B * N, C)
-        tab = K.gn_fwd(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"], False, a, gn=self._fstat_take(x))
+        tab = K.gn_fwd(x, B, N, C, G, P[nk + ".weight"], P[nk + ".bias"], False, a)
         Win = self.W(mk + ".in_proj_weight#f")
         bin_ = P[mk + ".in_proj_bias"]
         d = C // Hh
@@ -905,7 +898,7 @@ class UNetEngine:
             c["lse"] = K.attn_fwd(q, kv[:, :C], kv[:, C:], o, B, Hh, N, S, d)
             c.update(q=q, cp=cp, kv=kv, S=S, ctx=ctx, ck=ck)
         y = out if out is not None else self._new(B * N, C)
-        K.linear(o, self.W(mk + ".out_proj#f"), y, bias=P[mk + ".out_proj.bias"], resid=x, gn=self._fstat_req(y, N, C))
+        K.linear(o, self.W(mk + ".out_proj#f"), y, bias=P[mk + ".out_proj.bias"], resid=x)
         tape.append((self._attn_bwd, c))
         return y
 
@@ -923,7 +916,7 @@ class UNetEngine:
         gW = self.g(mk + ".in_proj_weight")
         gb = self.g(mk + ".in_proj_bias")
         da = self._new(B * N, C)
-        ga = K.gn_request(c["x"], c["tab"], N, C, False)
+        ga = _gn_req(c["x"], c["tab"], N, C, False)
         if not c["cross"]:
             qkv = c["qkv"]
             dqkv = self._new(B * N, 3 * C)
@@ -980,7 +973,7 @@ class UNetEngine:
         key = f"{p}.down_sample_conv"
         y = out if out is not None else self._new(B * (h // 2) * (w // 2), C)
         K.conv_fwd(x, B, h, w, C, K.ld_of(x), self.W(key + "#f"), C, 4, 4, 2, 1, y, K.ld_of(y),
-                   bias=self.P[key + ".bias"], gn=self._fstat_req(y, (h // 2) * (w // 2), C))
+                   bias=self.P[key + ".bias"])
         tape.append((self._down_bwd, dict(key=key, C=C, x=x, xn=xname, yn=oname, B=B, h=h, w=w)))
         return y
 
@@ -1034,7 +1027,7 @@ class UNetEngine:
             K.conv_wgrad(dpred, 8, c["hs"], B, H, W, C, C, 8, 3, 3, 1, 1, self.g("conv_out.weight"), H, W,
                          m_store=self.im_channels, bias_grad=self.g("conv_out.bias"))
         dhs = self._new(B * Pn, C)
-        gh = K.gn_request(c["x"], c["tab"], Pn, C, True)
+        gh = _gn_req(c["x"], c["tab"], Pn, C, True)
         K.conv_fwd(dpred, B, H, W, 8, 8, self.W("conv_out#d"), C, 3, 3, 1, 1, dhs, C, gn=gh)
         dx, fresh = grads.get(c["xn"])
         K.gn_bwd(c["x"], dhs, dx, c["tab"], P["norm_out.weight"], B, Pn, C, G, True,

@@ -120,7 +120,6 @@ class VQVAETrainEngine(UNetEngine):
         G = L["G"]
         K.PHASE = "fwd"
         tape = Tape()
-        self._fstats = {}  # GroupNorm-forward statistics registry (UNetEngine._fstat_req), per forward
         st = dict(B=B, H=H, W=W)
         grads = Grads(self.device)
         x = plan.as_operand(x)

@@ -55,3 +55,14 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _device_sync_after_gpu_test(request):
+    """Drain every stream after each GPU test, so an asynchronous device fault is reported by the test whose kernels
+    caused it (not by whichever later test next touches the device)."""
+    yield
+    if "gpu" in request.keywords:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()

@@ -143,50 +143,6 @@ def test_groupnorm_bwd_from_gemm_statistics(B, H, C, prod, silu, splits, monkeyp
     assert torch.equal(dx2, dx)
 
 
-@pytest.mark.parametrize("B,H,C,prod,silu", [(4, 32, 384, "conv", True), (4, 16, 512, "linear", False),
-                                             (32, 4, 512, "conv", True), (8, 8, 768, "linear", True)])
-@pytest.mark.parametrize("splits", [1, 4])
-def test_groupnorm_fwd_from_gemm_statistics(B, H, C, prod, silu, splits, monkeypatch):
-    """GroupNorm forward whose {sum x, sum x^2} come out of the GEMM that writes x (sdmi_gemm_desc::gn_part with gn_fwd:
-    the producers' full epilogues -- conv bias + per-sample time-embedding rowbias, linear bias + residual) followed by
-    the streaming sdmi_gn_fwd_part, against the self-contained sdmi_gn_fwd on the same x: x bitwise unchanged, output
-    and forward table to fp32 summation order."""
-    k = K()
-    monkeypatch.setattr(k, "TUNED", _AllSplit(splits))
-    torch.manual_seed(2)
-    P, G = H * H, 32
-    M = B * P
-    gamma = torch.randn(C, device="cuda") * 0.1 + 1
-    beta = torch.randn(C, device="cuda") * 0.1
-    bias = torch.randn(C, device="cuda") * 0.3
-    if prod == "conv":
-        cin = 256
-        a = bf(torch.randn(M, cin, device="cuda"))
-        wt = bf(torch.randn(C, 9 * cin, device="cuda") * 0.03)
-        temb = bf(torch.randn(B, C, device="cuda"))
-        run = lambda out, gn: k.conv_fwd(a, B, H, H, cin, cin, wt, C, 3, 3, 1, 1, out, C, bias=bias,  # noqa: E731
-                                         rowbias=temb, rb_ld=C, gn=gn)
-    else:
-        a = bf(torch.randn(M, C, device="cuda"))
-        wt = bf(torch.randn(C, C, device="cuda") * 0.05)
-        res = bf(torch.randn(M, C, device="cuda"))
-        run = lambda out, gn: k.linear(a, wt, out, bias=bias, resid=res, gn=gn)  # noqa: E731
-    x_ref = torch.empty(M, C, dtype=torch.bfloat16, device="cuda")
-    run(x_ref, None)
-    x = torch.empty_like(x_ref)
-    req = k.gn_request_fwd(P, C)
-    run(x, req)
-    torch.cuda.synchronize()
-    assert torch.equal(x, x_ref)
-    y_ref, y = torch.empty_like(x), torch.empty_like(x)
-    tab_ref = k.gn_fwd(x, B, P, C, G, gamma, beta, silu, y_ref)
-    tab = k.gn_fwd(x, B, P, C, G, gamma, beta, silu, y, gn=req)
-    torch.cuda.synchronize()
-    assert relerr(tab, tab_ref) < 1e-4, relerr(tab, tab_ref)
-    assert relerr(y, y_ref) < 1e-2, relerr(y, y_ref)
-    assert (y.float() - y_ref.float()).abs().gt(0).float().mean().item() < 0.02  # almost all elements bitwise
-
-
 # d = 8, 24, 40 take the forward's ones-column row sum (d % 16 == 8), incl. ragged N and S = 77
 @pytest.mark.parametrize("B,Hh,N,S,d", [(2, 16, 64, 64, 8), (2, 16, 256, 256, 24), (1, 16, 16, 77, 32),
                                         (2, 4, 1024, 1024, 16), (2, 16, 64, 77, 48), (1, 8, 100, 100, 64),
