@@ -318,19 +318,27 @@ __device__ __forceinline__ void epi_gn_half(const EpiArgs& e, const float* st, f
       const float4* tp = e.gn_tab + (long long)b * e.N + col;
 #pragma unroll
       for (int q = 0; q < 8; ++q) tb[q] = tp[q];
-#pragma unroll 1
-      for (int rl = s0 + rl0; rl < s0 + e.gn_rb; rl += R) {
-        const int row = m0h + rl;
-        if (row >= e.M) break;
+      // every x row of this thread's share of the segment is loaded up front (one memory round trip per segment
+      // instead of one per row); the rows are then consumed in the same order as before
+      constexpr int MR = (64 + R - 1) / R;
+      uint4 xr[MR];
+#pragma unroll
+      for (int k = 0; k < MR; ++k) {
+        const int rl = s0 + rl0 + k * R, row = m0h + rl;
+        if (rl < s0 + e.gn_rb && row < e.M) xr[k] = *(const uint4*)(e.gn_x + (long long)row * e.gn_ldx + col);
+      }
+#pragma unroll
+      for (int k = 0; k < MR; ++k) {
+        const int rl = s0 + rl0 + k * R, row = m0h + rl;
+        if (rl >= s0 + e.gn_rb || row >= e.M) break;
         const float4 lo = *(const float4*)(st + rl * SROW + c8 * 8), hi = *(const float4*)(st + rl * SROW + c8 * 8 + 4);
         float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        const uint4 xr = *(const uint4*)(e.gn_x + (long long)row * e.gn_ldx + col);
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] *= e.alpha;
         const uint4 pk = pack8(v);
         *(uint4*)((bf16_t*)e.C + (long long)row * e.ldc + col) = pk;
         unpack8(pk, v);  // the statistics are of the stored bf16 dy, as the apply pass reads it
-        gn_accum(e, v, xr, tb, u, w);
+        gn_accum(e, v, xr[k], tb, u, w);
       }
     }
     if (rl0 < R) {

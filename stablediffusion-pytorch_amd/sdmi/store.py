@@ -30,6 +30,11 @@ def param_label(key):
     return "input"
 
 
+def _tail_key(k):
+    """the parameters flat_order puts last (read first by the forward): conv_in, cond_conv_in, t_proj, class_emb"""
+    return not re.match(r"(downs|mids|ups)\.", k) and not k.startswith("norm_out") and not k.startswith("conv_out")
+
+
 def flat_order(cfg, keys):
     L = layout(cfg)
     nd = len(L["down"]) - 1
@@ -97,15 +102,28 @@ class FlatStore:
         self.p = {k: self.view(self.params, k) for k in self.order}
         self.g = {k: self.view(self.grads, k) for k in self.order} if with_grads else None
 
-    def forward_chunks(self, n):
+    def forward_chunks(self, n, lead=False):
         """~n contiguous ranges [lo, hi) of the flat buffer in FORWARD order (descending offsets: the backward
         finalises the last layers first, so the flat order is roughly reverse forward order), split at parameter
-        starts; returns (ranges, chunk_of_key)."""
-        starts = sorted(off for off, _ in self.offsets.values())
-        target = max(1, self.numel // n)
+        starts; returns (ranges, chunk_of_key).
+        lead (UNet flat_order): the runs the forward reads first become chunks of their own ahead of the n -- the
+        input / time-MLP parameters, the context projections of every cross-attention, the time-embedding projections
+        of every resnet -- and the first of the n body chunks is a small one (1 / (2n) of the body), so the next
+        forward's first kernels wait for the optimizer update of ~1 M parameters instead of one sixth of all of them."""
         cuts, hi = [], self.numel
-        for s in reversed(starts):  # walk from the top of the buffer down
-            if hi - s >= target and s > 0:
+        if lead:
+            groups = [lambda k: _tail_key(k), lambda k: ".context_proj." in k, lambda k: ".t_emb_layers." in k]
+            for g in groups:
+                offs = [self.offsets[k][0] for k in self.order if g(k)]
+                if offs and min(offs) < hi:
+                    cuts.append((min(offs), hi))
+                    hi = min(offs)
+        starts = sorted(off for off, _ in self.offsets.values() if off < hi)
+        nlead, body = len(cuts), hi
+        target = max(1, body // n)
+        first = max(1, body // (2 * n)) if lead else target
+        for s in reversed(starts):  # walk from the top of the (remaining) buffer down
+            if hi - s >= (first if len(cuts) == nlead else target) and s > 0:
                 cuts.append((s, hi))
                 hi = s
         cuts.append((0, hi))

@@ -82,6 +82,9 @@ def finalize_norm(blocks, max_norm, state, growth, skip_mode, grad_div):
                                              skip_mode, grad_div, K._stream()), "sdmi_clip_finalize")
 
 
+_LEAD_CHUNKS = os.environ.get("SDMI_LEAD_CHUNKS", "0") != "0"  # A/B
+
+
 class DDPMTrainer:
     """base: "cond" / "uncond" (UNet, train_ddpm_cond_celebhq_multi_gpu.py:299-378, EMA 0.9999) or "dit"
     (Model_DiT_12L_train.py:300-375: same step, no EMA -- pass ema_decay=None -- and lr 1e-4)."""
@@ -153,7 +156,7 @@ class DDPMTrainer:
         nchunks = 1 if base == "dit" else 6
         self.opt_ranges = None
         if nchunks > 1 and getattr(self.engine, "side", None) is not None:
-            self.opt_ranges, key_chunk = self.store.forward_chunks(nchunks)
+            self.opt_ranges, key_chunk = self.store.forward_chunks(nchunks, lead=_LEAD_CHUNKS)
             self.engine.set_chunks(key_chunk)
             self.opt_events = [torch.cuda.Event() for _ in self.opt_ranges]
             self.late_event = torch.cuda.Event()
