@@ -107,8 +107,9 @@ typedef struct sdmi_gemm_desc {
   int sum_group;
   /* mainloop request (0 = built-in choice): 1 register-staged operands; LDS-DMA rings: 2 / 3 stages of 64-deep k
    * (128 x {64..192} tiles), 4 = 8-wave 128 x {256, 384} tiles, 5 = 3 stages of 32-deep k, 6 = 4 stages of 64-deep k
-   * (128 x 128), 7 / 8 = 64 x 64 / 64 x 128 tiles with 6 stages of 64-deep k (K-contiguous A and B only: the
-   * latency-bound low-resolution GEMMs). Downgraded where the mode does not support it. Used with the measured
+   * (128 x 128), 7 / 8 = 64 x 64 / 64 x 128 tiles with 6 stages of 64-deep k, 9 / 10 = 64 x 128 tiles with 3 / 2
+   * stages (7-10: K-contiguous A and B only, the low-resolution GEMMs). Downgraded where the mode does not support it.
+   * Used with the measured
    * per-shape table of sdmi/tuned_gemm.json. */
   int variant_hint;
   /* GroupNorm-backward statistics of the output (SDMI_GN_PART): the GEMM produces dy, the gradient of a

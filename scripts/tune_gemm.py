@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "uncond-unet", "dit", "sample"))
     ap.add_argument("--sample-batch", type=int, default=1)
     ap.add_argument("--only-new", action="store_true", help="tune only shapes the starting table has no entry for")
+    ap.add_argument("--against-table", action="store_true",
+                    help="baseline = the starting table's entry (not the heuristic): try only SDMI_TUNE_VARIANTS and "
+                         "replace the entry where one beats it by > 3 %")
     ap.add_argument("--out", default=os.path.join(REPO, "stablediffusion-pytorch_amd", "sdmi", "tuned_gemm.json"))
     args = ap.parse_args()
     from sdmi import _lib, kernels as K
@@ -118,12 +121,15 @@ def main():
             continue
         d.splits_hint = 0
         d.variant_hint = 0
+        cur = table.get(key) if args.against_table else None
+        if cur:
+            d.splits_hint, d.variant_hint = (cur[0], cur[1]) if isinstance(cur, list) else (cur, 0)
         t_def = time_launch(L, d, ws, stream)
-        best, t_best = 0, t_def
+        best, t_best = (cur or 0), t_def
         # mainloops: register staging (1) and the LDS-DMA rings (2, 3, 6: 2 / 3 / 4 stages of 64-deep K; 7, 8: 64-row
         # tiles with 6 stages; 4: 8-wave
         # 128 x {256, 384} tiles; 5: 3 stages of 32-deep K); the library downgrades a request the mode cannot take
-        variants = tuple(int(v) for v in os.environ.get("SDMI_TUNE_VARIANTS", "1,2,3,4,5,6,7,8").split(","))
+        variants = tuple(int(v) for v in os.environ.get("SDMI_TUNE_VARIANTS", "1,2,3,4,5,6,7,8,9,10").split(","))
         for v in variants:
             for s in SPLITS:
                 if s > nkt or s * d.m * d.n * 4 >= min(ws.numel() * 4, 1 << 31):

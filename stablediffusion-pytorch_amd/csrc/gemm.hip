@@ -1397,7 +1397,8 @@ int slab_n(const sdmi_gemm_desc* d) { return n_total(d) + ((has_reductions(d) &&
 // Mainloop choice (SDMI_GEMM_VARIANT overrides for A/B runs): 0 register-staged; LDS-DMA rings: 2 / 3 stages of
 // 64-deep 128-row tiles (4 waves), 4 = 128 x {256, 384} tiles on 8 waves with a 4-stage ring of 32-deep stages (3
 // tiles, 96 KiB, in flight per CU), 5 = 128 x {128, 192} tiles on 4 waves with a 3-stage ring of 32-deep stages (two
-// workgroups per CU). -1 (default) per mode: the DMA ring where it measured faster on the step's shapes (row-major
+// workgroups per CU), 6 = 128 x 128 with 4 stages, 7 / 8 = 64 x {64, 128} tiles with 6 stages, 9 / 10 = 64 x 128 tiles
+// with 3 / 2 stages. -1 (default) per mode: the DMA ring where it measured faster on the step's shapes (row-major
 // and implicit-conv A), register staging for the col-major (weight-gradient) A; the per-shape table
 // sdmi/tuned_gemm.json overrides it through variant_hint.
 int gemm_variant() {
@@ -1405,7 +1406,7 @@ int gemm_variant() {
   if (v == -2) {
     const char* s = getenv("SDMI_GEMM_VARIANT");
     v = s ? atoi(s) : -1;
-    if (v != 0 && (v < 2 || v > 8)) v = -1;
+    if (v != 0 && (v < 2 || v > 10)) v = -1;
   }
   return v;
 }
@@ -1419,7 +1420,7 @@ bool dma_reductions_ok(const sdmi_gemm_desc* d) {
 
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 8) v = d->variant_hint == 1 ? 0 : d->variant_hint;
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 10) v = d->variant_hint == 1 ? 0 : d->variant_hint;
   if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
   if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
   if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
@@ -1429,11 +1430,11 @@ int pick_variant(const sdmi_gemm_desc* d) {
   if (v == 5 && d->a_mode == SDMI_A_CONV && d->a2 && d->k_split % 32) v = 0;
   if (v != 0 && d->a_mode == SDMI_A_COLMAJOR && d->b_mode == SDMI_B_NK) v = 0;  // no DMA instantiation
   // 64-row tiles: K-contiguous images only (row-major / implicit-conv A, [n][k] B), no reduction columns
-  if ((v == 7 || v == 8) && (d->a_mode == SDMI_A_COLMAJOR || d->b_mode != SDMI_B_NK || has_reductions(d))) v = 2;
+  if (v >= 7 && (d->a_mode == SDMI_A_COLMAJOR || d->b_mode != SDMI_B_NK || has_reductions(d))) v = 2;
   return v;
 }
 
-int tile_m(const sdmi_gemm_desc*, int variant) { return variant == 7 || variant == 8 ? 64 : BM; }
+int tile_m(const sdmi_gemm_desc*, int variant) { return variant >= 7 ? 64 : BM; }
 
 // columns the grid covers: the DMA kernels compute the reduction columns outside the column tiles
 int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total(d) : d->n; }
@@ -1443,7 +1444,7 @@ int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total
 int pick_tbn(const sdmi_gemm_desc* d, int variant) {
   if (variant == 4) return d->n % 384 == 0 ? 384 : 256;
   if (variant == 7) return 64;
-  if (variant == 8 || variant == 6) return BN;
+  if (variant >= 8 || variant == 6) return BN;
   if (variant == 5) return d->b_mode == SDMI_B_NK && d->n % 192 == 0 ? 192 : BN;
   if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR) return BN;
   // narrow outputs (N <= 64: the VQVAE's 64-channel convs at 256^2, 4-channel heads, DiT proj_out): a 128-column
@@ -1484,6 +1485,10 @@ hipError_t launch_dma_red(const Args& a, const EpiArgs& e, dim3 grid, hipStream_
   if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR && RED == 0) {
     if (v == 7) return launch_dma<AM, BMODE, 6, 64, 64, 4, 0>(a, e, grid, s);    // 64 x 64, 6 stages (96 KiB)
     if (v == 8) return launch_dma<AM, BMODE, 6, 128, 64, 4, 0>(a, e, grid, s);   // 64 x 128, 6 stages (144 KiB)
+    // 64 x 128 with 3 / 2 stages (72 / 48 KiB: two or three workgroups per CU) -- the M = 2048-8192 GEMMs whose
+    // 128 x 128 grid is one tile per CU (8192 x 512: 256 tiles)
+    if (v == 9) return launch_dma<AM, BMODE, 3, 128, 64, 4, 0>(a, e, grid, s);
+    if (v == 10) return launch_dma<AM, BMODE, 2, 128, 64, 4, 0>(a, e, grid, s);
   }
   if (v == 4) {  // 128 x {256, 384} on 8 waves, 32-deep stages, 4-stage ring (3 tiles in flight)
     if (tbn == 384) return launch_dma<AM, BMODE, 4, 384, BM, 4, RED, 32>(a, e, grid, s);

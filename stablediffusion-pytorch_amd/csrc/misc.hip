@@ -318,6 +318,41 @@ __global__ void pack_kernel(const sdmi_pack_desc* descs, const int2* bmap) {
     }
     return;
   }
+  const int nrows = o_end - bm.y;
+  if (nrows > 1 && nrows * taps * ld <= PACK_LDS_ELEMS) {
+    // short rows (conv_in's 4-channel taps, transposed up-sampling convs): every row of the block is gathered in ONE
+    // pass -- all loads in flight together -- instead of one dependent load round trip and two barriers per row
+    const int per = taps * d.I;
+    const bool cfast = d.si == 1;
+    for (int idx = threadIdx.x; idx < nrows * per; idx += NT) {
+      const int rr = idx / per, rem = idx - rr * per;
+      const int i = cfast ? rem % d.I : rem / taps, t = cfast ? rem / d.I : rem - i * taps;
+      const int a = t / d.KW, b = t - a * d.KW;
+      const int kh = d.kh_off + d.kh_mul * a, kw = d.kw_off + d.kw_mul * b;
+      const float* src = d.src + (long long)(bm.y + rr) * d.so;
+      st[(rr * taps + t) * ld + i] = f2bf(src[(long long)i * d.si + (long long)kh * d.skh + (long long)kw * d.skw]);
+    }
+    __syncthreads();
+    const int q8 = row / 8;
+    for (int q = threadIdx.x; q < nrows * q8; q += NT) {
+      const int rr = q / q8, qq = q - rr * q8;
+      const int t = (qq * 8) / d.Ipad, i0 = qq * 8 - t * d.Ipad;
+      const bf16_t* sr = st + (rr * taps + t) * ld;
+      uint4 v;
+      if (i0 + 8 <= d.I) {
+        v = *(const uint4*)(sr + i0);
+      } else {  // zero padding columns I .. Ipad
+        bf16_t tmp[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tmp[e] = i0 + e < d.I ? sr[i0 + e] : (bf16_t)0;
+        v = *(const uint4*)tmp;
+      }
+      const int o = bm.y + rr;
+      bf16_t* dst = (bf16_t*)d.dst + (d.dst_ld ? (long long)o * d.dst_ld : (long long)o * row);
+      *(uint4*)(dst + qq * 8) = v;
+    }
+    return;
+  }
 #pragma unroll 1
   for (int o = bm.y; o < o_end; ++o) {
     const float* src = d.src + (long long)o * d.so;

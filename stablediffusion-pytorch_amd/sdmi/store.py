@@ -108,22 +108,23 @@ class FlatStore:
         starts; returns (ranges, chunk_of_key).
         lead (UNet flat_order): the runs the forward reads first become chunks of their own ahead of the n -- the
         input / time-MLP parameters, the context projections of every cross-attention, the time-embedding projections
-        of every resnet -- and the first of the n body chunks is a small one (1 / (2n) of the body), so the next
-        forward's first kernels wait for the optimizer update of ~1 M parameters instead of one sixth of all of them."""
+        of every resnet, then the first two down blocks whole -- so the next forward's first kernels wait for the
+        optimizer update of ~1 M parameters instead of one sixth of all of them, and every later wait is for the block
+        the forward is about to run."""
         cuts, hi = [], self.numel
         if lead:
-            groups = [lambda k: _tail_key(k), lambda k: ".context_proj." in k, lambda k: ".t_emb_layers." in k]
+            groups = [lambda k: _tail_key(k), lambda k: ".context_proj." in k, lambda k: ".t_emb_layers." in k,
+                      lambda k: k.startswith("downs.0.") and ".t_emb_layers." not in k and ".context_proj." not in k,
+                      lambda k: k.startswith("downs.1.") and ".t_emb_layers." not in k and ".context_proj." not in k]
             for g in groups:
                 offs = [self.offsets[k][0] for k in self.order if g(k)]
                 if offs and min(offs) < hi:
                     cuts.append((min(offs), hi))
                     hi = min(offs)
         starts = sorted(off for off, _ in self.offsets.values() if off < hi)
-        nlead, body = len(cuts), hi
-        target = max(1, body // n)
-        first = max(1, body // (2 * n)) if lead else target
+        target = max(1, hi // n)
         for s in reversed(starts):  # walk from the top of the (remaining) buffer down
-            if hi - s >= (first if len(cuts) == nlead else target) and s > 0:
+            if hi - s >= target and s > 0:
                 cuts.append((s, hi))
                 hi = s
         cuts.append((0, hi))
