@@ -57,7 +57,9 @@ def kernel_name(tag, info):
     tn = int(re.search(r"tile_n=(\d+)", info).group(1))
     if v == 0:
         return f"gemm_kernel<{a}, {b}>"
-    stages = {2: 2, 3: 3, 4: 4, 5: 3, 6: 4, 7: 6, 8: 6}[v]  # gemm.hip launch_dma_red: variant -> ring depth
+    stages = {2: 2, 3: 3, 4: 4, 5: 3, 6: 4, 7: 6, 8: 6, 9: 3, 10: 2}[v]  # gemm.hip launch_dma_red: variant -> ring depth
+    if v >= 7:  # 64-row tiles
+        return f"gemm_dma_kernel<{a}, {b}, {stages}, {tn}, 64>"
     return f"gemm_dma_kernel<{a}, {b}, {stages}, {tn}>"
 def _latest(pattern):
     """newest round's committed evidence file (profiles/rNN_*)"""

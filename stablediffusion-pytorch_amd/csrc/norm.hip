@@ -46,6 +46,7 @@ struct StripArgs {
   int c_store;
   long long seg;              // mode 2: rows per (virtual) batch row; 0 = P
   int nb;                     // batch rows (virtual for mode 2)
+  int rows_only;              // GroupNorm backward: publish the per-(b, c) sums to rows, no batch tail
 };
 
 __device__ __forceinline__ void st_coherent(float* p, float v) {
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(NT) void gn_bwd_reduce_kernel(StripArgs a) {
     const float4 t = a.tab[(long long)b * a.C + c];
     const float2 qo = grp[ch / Cg];
     a.out_tab[(long long)b * a.C + c] = make_float4(t.x, t.y, qo.x, qo.y);
-    if (a.sum1) {
+    if (a.sum1 || a.rows_only) {
       float* rp = a.rows + ((long long)b * a.C + c) * 2;
       st_coherent(rp, s1[ch]);
       st_coherent(rp + 1, s2[ch]);
@@ -582,7 +583,7 @@ __global__ __launch_bounds__(NTH) void gn_bwd_pass_kernel(StripArgs a, bf16_t* d
     const float rs = tt.w, mu = tt.z;
     grp[gi] = make_float2(-rs * rs * Bc * inv_n, rs * rs * mu * Bc * inv_n - rs * A * inv_n);
   }
-  if (a.sum1) {
+  if (a.sum1 || a.rows_only) {
     for (int ch = t; ch < cw; ch += NTH) {
       float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
       st_coherent(rp, s1[ch]);
@@ -856,7 +857,7 @@ __global__ __launch_bounds__(NT) void gn_bwd_part_kernel(StripArgs a, const floa
     const float rs = tt.w, mu = tt.z;
     grp[gi] = make_float2(-rs * rs * Bc * inv_n, rs * rs * mu * Bc * inv_n - rs * A * inv_n);
   }
-  const bool publish = a.sum1 && blockIdx.z == 0;
+  const bool publish = (a.sum1 || a.rows_only) && blockIdx.z == 0;
   if (publish) {
     for (int ch = t; ch < cw; ch += NT) {
       float* rp = a.rows + ((long long)b * a.C + c0 + ch) * 2;
@@ -902,7 +903,7 @@ __global__ __launch_bounds__(NT) void gn_bwd_part_kernel(StripArgs a, const floa
       *(uint4*)(dx + row * lddx + cc) = pack8(ov);
     }
   }
-  if (!publish) return;
+  if (!publish || !a.sum1) return;
   if (!arrive_last(a.ctr + BATCH_CTR + strip, a.nb)) return;
   batch_tail(a, c0, cw, a.sum1, a.sum2, a.C);
 }
@@ -1015,16 +1016,19 @@ extern "C" int sdmi_gn_apply(const void* x, int ldx, void* y, int ldy, const flo
 }
 
 // table: forward table from sdmi_gn_stats; table2_ws: float4 [B][C] scratch; ws: sdmi_chan_reduce_workspace
-extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
-                           const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws,
-                           float* dgamma, float* dbeta, const void* addend, int ldadd, sdmi_stream_t stream) {
+namespace {
+// rows_out != null: the per-(batch row, channel) sums {sum dz, sum dz*xhat} go to rows_out [B][C][2] and dgamma / dbeta
+// (which must be null) are left to sdmi_gn_rows_sum -- no batch tail on the launching stream
+int gn_bwd_impl(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws, float* dgamma,
+                float* dbeta, float* rows_out, const void* addend, int ldadd, sdmi_stream_t stream) {
   if (C % 8 || G <= 0 || C % G) return -1;
-  if ((dgamma == nullptr) != (dbeta == nullptr)) return -3;
+  if ((dgamma == nullptr) != (dbeta == nullptr) || (rows_out && dgamma)) return -3;
   hipStream_t s = (hipStream_t)stream;
   StripArgs r = {};
   r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy; r.tab = (const float4*)table;
   r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.gamma = gamma; r.out_tab = (float4*)table2_ws;
-  r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
+  r.rows = rows_out ? rows_out : ws; r.rows_only = rows_out != nullptr; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
   PassCfg pc;
   if (pick_pass(B, P, C, G, pc)) {  // single pass
     r.CW = pc.cw;
@@ -1049,19 +1053,35 @@ extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, voi
   SDMI_CHECK_LAUNCH();
   return 0;
 }
+}  // namespace
+
+extern "C" int sdmi_gn_bwd(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                           const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws,
+                           float* dgamma, float* dbeta, const void* addend, int ldadd, sdmi_stream_t stream) {
+  return gn_bwd_impl(x, ldx, dy, lddy, dx, lddx, table, gamma, B, P, C, G, silu, ws, table2_ws, dgamma, dbeta, nullptr,
+                     addend, ldadd, stream);
+}
+
+extern "C" int sdmi_gn_bwd_rows(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                                const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws,
+                                float* rows, const void* addend, int ldadd, sdmi_stream_t stream) {
+  if (!rows) return -1;
+  return gn_bwd_impl(x, ldx, dy, lddy, dx, lddx, table, gamma, B, P, C, G, silu, ws, table2_ws, nullptr, nullptr, rows,
+                     addend, ldadd, stream);
+}
 
 // GroupNorm backward from the dgrad GEMM's segment partials (sdmi_gemm_desc::gn_part, rb rows per segment)
-extern "C" int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
-                                const float* gamma, int B, int P, int C, int G, int silu, const float* part, int rb,
-                                float* ws, float* dgamma, float* dbeta, const void* addend, int ldadd,
-                                sdmi_stream_t stream) {
+namespace {
+int gn_bwd_part_impl(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                     const float* gamma, int B, int P, int C, int G, int silu, const float* part, int rb, float* ws,
+                     float* dgamma, float* dbeta, float* rows_out, const void* addend, int ldadd, sdmi_stream_t stream) {
   if (C % 8 || G <= 0 || C % G || B <= 0 || P <= 0 || rb <= 0 || P % rb || !part) return -1;
-  if ((dgamma == nullptr) != (dbeta == nullptr)) return -3;
+  if ((dgamma == nullptr) != (dbeta == nullptr) || (rows_out && dgamma)) return -3;
   if (ldx % 8 || lddy % 8 || lddx % 8 || (addend && ldadd % 8)) return -5;
   StripArgs r = {};
   r.x = (const bf16_t*)x; r.ldx = ldx; r.dy = (const bf16_t*)dy; r.ldy = lddy; r.tab = (const float4*)table;
   r.B = B; r.P = P; r.C = C; r.G = G; r.silu = silu; r.gamma = gamma;
-  r.rows = ws; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
+  r.rows = rows_out ? rows_out : ws; r.rows_only = rows_out != nullptr; r.nb = B; r.sum1 = dbeta; r.sum2 = dgamma;
   r.CW = part_strip_width(C, C / G);
   const int nch = (C + r.CW - 1) / r.CW;
   if (r.CW > NT || nch > BATCH_CTR) return -2;
@@ -1071,6 +1091,47 @@ extern "C" int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy
   while ((long long)nch * B * ps < 1024 && P / (ps * 2) >= 64) ps *= 2;
   sdmi_rt::launch(gn_bwd_part_kernel, dim3(nch, B, ps), dim3(NT), 0, (hipStream_t)stream, r, (const float2*)part, rb,
                   (bf16_t*)dx, lddx, (const bf16_t*)addend, ldadd);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+// dgamma[c] = sum_b rows[b][c][1], dbeta[c] = sum_b rows[b][c][0], batch rows in order (deterministic)
+__global__ __launch_bounds__(NT) void gn_rows_sum_kernel(const float2* rows, int B, int C, float* dgamma, float* dbeta) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+  for (int b = 0; b < B; ++b) {
+    const float2 v = rows[(long long)b * C + c];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  dbeta[c] = s1;
+  dgamma[c] = s2;
+}
+}  // namespace
+
+extern "C" int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
+                                const float* gamma, int B, int P, int C, int G, int silu, const float* part, int rb,
+                                float* ws, float* dgamma, float* dbeta, const void* addend, int ldadd,
+                                sdmi_stream_t stream) {
+  return gn_bwd_part_impl(x, ldx, dy, lddy, dx, lddx, table, gamma, B, P, C, G, silu, part, rb, ws, dgamma, dbeta,
+                          nullptr, addend, ldadd, stream);
+}
+
+extern "C" int sdmi_gn_bwd_part_rows(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx,
+                                     const float* table, const float* gamma, int B, int P, int C, int G, int silu,
+                                     const float* part, int rb, float* ws, float* rows, const void* addend, int ldadd,
+                                     sdmi_stream_t stream) {
+  if (!rows) return -1;
+  return gn_bwd_part_impl(x, ldx, dy, lddy, dx, lddx, table, gamma, B, P, C, G, silu, part, rb, ws, nullptr, nullptr,
+                          rows, addend, ldadd, stream);
+}
+
+extern "C" int sdmi_gn_rows_sum(const float* rows, int B, int C, float* dgamma, float* dbeta, sdmi_stream_t stream) {
+  if (!rows || !dgamma || !dbeta || B <= 0 || C <= 0 || ((uintptr_t)rows & 7)) return -1;
+  sdmi_rt::launch(gn_rows_sum_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, (hipStream_t)stream, (const float2*)rows, B,
+                  C, dgamma, dbeta);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -92,6 +92,9 @@ SIGNATURES = {
     "sdmi_gn_fwd": ([_P, _I, _P, _I, _I, _I, _I, _I, _F, _P, _P, _I, _P, _P, _P], _I),
     "sdmi_gn_bwd": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P], _I),
     "sdmi_gn_bwd_part": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _I, _P], _I),
+    "sdmi_gn_bwd_rows": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P], _I),
+    "sdmi_gn_bwd_part_rows": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P], _I),
+    "sdmi_gn_rows_sum": ([_P, _I, _I, _P, _P, _P], _I),
     "sdmi_chan_sum": ([_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _I, _P], _I),
     "sdmi_prep_input": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),
     "sdmi_cond_wgrad": ([_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P], _I),

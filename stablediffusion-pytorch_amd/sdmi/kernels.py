@@ -402,25 +402,46 @@ def gn_request(x, tab, P, C, silu):
     return dict(x=x, tab=tab, P=P, silu=silu)
 
 
-def gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, silu, dgamma, dbeta, addend=None, gn=None):
+def gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, silu, dgamma, dbeta, addend=None, gn=None, defer=None):
     """GroupNorm(+SiLU) backward; with gn (the request whose GEMM produced dy) from its segment statistics in one
-    streaming launch (sdmi_gn_bwd_part), else the self-contained sdmi_gn_bwd."""
+    streaming launch (sdmi_gn_bwd_part), else the self-contained sdmi_gn_bwd. defer (a list): dgamma / dbeta are not
+    summed by this launch -- its per-(batch row, channel) sums go to a rows buffer and (rows, B, C, dgamma, dbeta) is
+    appended to defer for gn_rows_sum (the caller issues it off the data-gradient chain)."""
     L = _lib.lib()
     ws = torch.empty(L.sdmi_chan_reduce_workspace(B, P, C) // 4, dtype=torch.float32, device=x.device)
+    rows = torch.empty(B * C * 2, dtype=torch.float32, device=x.device) if defer is not None else None
+    add = (_p(addend), ld_of(addend) if addend is not None else 0)
     if gn is not None:
         assert gn.get("part") is not None, "the producing GEMM did not run with this GroupNorm request"
         with _Prof("gn_bwd", 0, f"B={B} P={P} C={C} part"):
-            check(L.sdmi_gn_bwd_part(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma), B, P, C,
-                                     G, 1 if silu else 0, _p(gn["part"]), gn["rb"], _p(ws), _p(dgamma), _p(dbeta),
-                                     _p(addend), ld_of(addend) if addend is not None else 0, _stream()),
-                  "sdmi_gn_bwd_part")
-        return dx
-    tab2 = torch.empty(B * C * 4, dtype=torch.float32, device=x.device)
-    with _Prof("gn_bwd", 0, f"B={B} P={P} C={C}"):
-        check(L.sdmi_gn_bwd(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma), B, P, C, G,
-                            1 if silu else 0, _p(ws), _p(tab2), _p(dgamma), _p(dbeta), _p(addend),
-                            ld_of(addend) if addend is not None else 0, _stream()), "sdmi_gn_bwd")
+            if rows is None:
+                check(L.sdmi_gn_bwd_part(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma), B, P,
+                                         C, G, 1 if silu else 0, _p(gn["part"]), gn["rb"], _p(ws), _p(dgamma),
+                                         _p(dbeta), *add, _stream()), "sdmi_gn_bwd_part")
+            else:
+                check(L.sdmi_gn_bwd_part_rows(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma),
+                                              B, P, C, G, 1 if silu else 0, _p(gn["part"]), gn["rb"], _p(ws),
+                                              _p(rows), *add, _stream()), "sdmi_gn_bwd_part_rows")
+    else:
+        tab2 = torch.empty(B * C * 4, dtype=torch.float32, device=x.device)
+        with _Prof("gn_bwd", 0, f"B={B} P={P} C={C}"):
+            if rows is None:
+                check(L.sdmi_gn_bwd(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma), B, P, C,
+                                    G, 1 if silu else 0, _p(ws), _p(tab2), _p(dgamma), _p(dbeta), *add, _stream()),
+                      "sdmi_gn_bwd")
+            else:
+                check(L.sdmi_gn_bwd_rows(_p(x), ld_of(x), _p(dy), ld_of(dy), _p(dx), ld_of(dx), _p(tab), _p(gamma), B,
+                                         P, C, G, 1 if silu else 0, _p(ws), _p(tab2), _p(rows), *add, _stream()),
+                      "sdmi_gn_bwd_rows")
+    if rows is not None:
+        defer.append((rows, B, C, dgamma, dbeta))
     return dx
+
+
+def gn_rows_sum(rows, B, C, dgamma, dbeta):
+    """dgamma / dbeta from a deferred GroupNorm backward's rows buffer (gn_bwd(defer=...))."""
+    with _Prof("gn_rows_sum", 0, f"B={B} C={C}"):
+        check(_lib.lib().sdmi_gn_rows_sum(_p(rows), B, C, _p(dgamma), _p(dbeta), _stream()), "sdmi_gn_rows_sum")
 
 
 def chan_sum(dy, B, P, C, *, per_bc=None, per_c=None, per_c2=None, c_store=0):

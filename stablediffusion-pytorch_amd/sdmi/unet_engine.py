@@ -17,6 +17,7 @@ for MI355X:
 Parameters are referenced by the reference's state-dict keys.
 """
 import contextlib
+import os
 
 import torch
 
@@ -29,6 +30,7 @@ from . import plan
 # 13.94 / 13.90, P >= 1024 13.89 / 13.89, none 13.98 / 13.99 ms -- at 16^2 and below the statistics epilogue and the
 # statistics reducer cost more than the standalone single-pass GroupNorm they replace.
 GN_FUSE_MIN_P = 1024
+_GN_DEFER = os.environ.get("SDMI_GN_DEFER", "0") != "0"  # A/B
 
 
 def _gn_req(x, tab, P, C, silu):
@@ -843,7 +845,7 @@ class UNetEngine:
         else:
             K.linear_dgrad(dy, self.W(f"{p}.res{l}#cat")[:, 9 * cout:], dx, resid=None if fresh else dx)
         K.gn_bwd(c["h1"], dh2, dh2, c["t2"], P[b + ".0.weight"], B, Pn, cout, G, True,
-                 self.g(b + ".0.weight"), self.g(b + ".0.bias"), gn=g2)
+                 self.g(b + ".0.weight"), self.g(b + ".0.bias"), gn=g2, defer=self._gn_defer())
         off = self.temb_off.get((p, l))
         with self._wg(dh2):
             # conv1 bias, t_emb_layers bias and the per-sample time-embedding gradient (blocks.py:117-118) are
@@ -856,7 +858,7 @@ class UNetEngine:
         g1 = _gn_req(c["x"], c["t1"], Pn, cin, True)
         K.conv_fwd(dh2, B, h, w, cout, cout, self.W(a + ".2#d"), cin, 3, 3, 1, 1, dh0, cin, gn=g1)
         K.gn_bwd(c["x"], dh0, dx, c["t1"], P[a + ".0.weight"], B, Pn, cin, G, True,
-                 self.g(a + ".0.weight"), self.g(a + ".0.bias"), addend=dx, gn=g1)
+                 self.g(a + ".0.weight"), self.g(a + ".0.bias"), addend=dx, gn=g1, defer=self._gn_defer())
 
     # ---- self / cross attention --------------------------------------------------------------------
     def _attn_fwd(self, p, l, C, x, xname, out, oname, B, h, w, st, tape, cross):
@@ -966,7 +968,7 @@ class UNetEngine:
             else:
                 addend = dy
         K.gn_bwd(c["x"], da, dx, c["tab"], P[nk + ".weight"], B, N, C, G, False,
-                 self.g(nk + ".weight"), self.g(nk + ".bias"), addend=addend, gn=ga)
+                 self.g(nk + ".weight"), self.g(nk + ".bias"), addend=addend, gn=ga, defer=self._gn_defer())
 
     # ---- down / up sampling convs --------------------------------------------------------------------
     def _down_fwd(self, p, C, x, xname, out, oname, B, h, w, tape):
@@ -1031,7 +1033,8 @@ class UNetEngine:
         K.conv_fwd(dpred, B, H, W, 8, 8, self.W("conv_out#d"), C, 3, 3, 1, 1, dhs, C, gn=gh)
         dx, fresh = grads.get(c["xn"])
         K.gn_bwd(c["x"], dhs, dx, c["tab"], P["norm_out.weight"], B, Pn, C, G, True,
-                 self.g("norm_out.weight"), self.g("norm_out.bias"), addend=None if fresh else dx, gn=gh)
+                 self.g("norm_out.weight"), self.g("norm_out.bias"), addend=None if fresh else dx, gn=gh,
+                 defer=self._gn_defer())
 
     def _bwd_input(self, c, grads):
         L = self.L
@@ -1145,14 +1148,30 @@ class UNetEngine:
         self._pending_wg.setdefault(key, []).append((dy, x, gW, gb))
 
     def _flush_wg(self):
-        """Issue the deferred weight gradients (groups of at most SDMI_GEMM_GROUP_MAX = 8)."""
+        """Issue the deferred weight gradients (groups of at most SDMI_GEMM_GROUP_MAX = 8) and the block's deferred
+        GroupNorm dgamma / dbeta sums."""
         pend, self._pending_wg = self._pending_wg, {}
         for items in pend.values():
             for i in range(0, len(items), 8):
                 with self._wg():
                     K.linear_wgrad_grouped(items[i:i + 8])
+        gpend, self._pending_gn = self._pending_gn, []
+        if gpend:
+            # on the first weight-gradient stream, outside the round-robin (the block's other assignments unchanged)
+            side = self.sides[0]
+            plan.wait_stream(side, torch.cuda.current_stream(self.device))
+            self._keep.extend(g[0] for g in gpend)
+            with torch.cuda.stream(side):
+                for rows, B, C, dg, db in gpend:
+                    K.gn_rows_sum(rows, B, C, dg, db)
 
     _pending_wg = {}
+    _pending_gn = []
+
+    def _gn_defer(self):
+        """GroupNorm backward dgamma / dbeta: summed over the batch on a weight-gradient stream at the block's flush
+        (kernels.gn_bwd(defer=...)) -- the data-gradient chain then carries no batch tail per GroupNorm."""
+        return self._pending_gn if (self._grouping() and _GN_DEFER) else None
 
     def _join(self):
         """The current stream waits for all weight-gradient work issued so far."""
@@ -1182,10 +1201,11 @@ class UNetEngine:
         self._wg_next = 0  # same side-stream assignment every step
         K.PHASE = "bwd"
         self._pending_wg = {}
+        self._pending_gn = []
         for k in range(len(tape) - 1, -1, -1):
             fn, c = tape[k]
             fn(c, grads)
-            if self._pending_wg and (k == 0 or tape[k - 1][1].get("label") != c.get("label")):
+            if (self._pending_wg or self._pending_gn) and (k == 0 or tape[k - 1][1].get("label") != c.get("label")):
                 self._flush_wg()  # the block's grouped weight gradients, before its gradients are reported final
             if on_progress is not None:
                 on_progress(tape, k)
