@@ -70,7 +70,7 @@ def test_conv_fwd_and_wgrad(B, H, cin, cout, ks, stride, pad):
     torch.manual_seed(3)
     x = bf(torch.randn(B, cin, H, H, device="cuda"))
     w = bf(torch.randn(cout, cin, ks, ks, device="cuda") * 0.1)
-    ref = F.conv2d(x.float(), w.float(), stride=stride, padding=pad)
+    ref = F.conv2d(x.float().cpu(), w.float().cpu(), stride=stride, padding=pad).cuda()  # host fp32 reference
     OH = ref.shape[-1]
     xn = x.permute(0, 2, 3, 1).contiguous()
     wpk = w.permute(0, 2, 3, 1).contiguous()
@@ -80,13 +80,13 @@ def test_conv_fwd_and_wgrad(B, H, cin, cout, ks, stride, pad):
     close(out.permute(0, 3, 1, 2), ref + rowbias.float()[:, :, None, None])
     # weight gradient
     dy = bf(torch.randn(B, cout, OH, OH, device="cuda"))
-    xr = x.float().requires_grad_(True)
-    wr = w.float().requires_grad_(True)
-    F.conv2d(xr, wr, stride=stride, padding=pad).backward(dy.float())
+    xr = x.float().cpu().requires_grad_(True)
+    wr = w.float().cpu().requires_grad_(True)
+    F.conv2d(xr, wr, stride=stride, padding=pad).backward(dy.float().cpu())
     dw = torch.empty(cout, cin, ks, ks, device="cuda")
     dyn = dy.permute(0, 2, 3, 1).contiguous()
     k.conv_wgrad(dyn, cout, xn, B, H, H, cin, cin, cout, ks, ks, stride, pad, dw, OH, OH)
-    close(dw, wr.grad, 2e-3)
+    close(dw, wr.grad.cuda(), 2e-3)
 
 
 @pytest.mark.parametrize("B,H,cin,cout", [(2, 4, 16, 24), (3, 8, 64, 32)])
@@ -95,7 +95,7 @@ def test_convT_phases(B, H, cin, cout):
     torch.manual_seed(4)
     x = bf(torch.randn(B, cin, H, H, device="cuda"))
     w = bf(torch.randn(cin, cout, 4, 4, device="cuda") * 0.1)
-    ref = F.conv_transpose2d(x.float(), w.float(), stride=2, padding=1)
+    ref = F.conv_transpose2d(x.float().cpu(), w.float().cpu(), stride=2, padding=1).cuda()
     xn = x.permute(0, 2, 3, 1).contiguous()
     wph = []
     for ph in range(2):
@@ -138,7 +138,7 @@ def test_conv_fwd_tile192():
     B, H, cin, cout = 32, 32, 64, 384
     x = bf(torch.randn(B, cin, H, H, device="cuda"))
     w = bf(torch.randn(cout, cin, 3, 3, device="cuda") * 0.1)
-    ref = F.conv2d(x.float(), w.float(), padding=1)
+    ref = F.conv2d(x.float().cpu(), w.float().cpu(), padding=1).cuda()
     xn = x.permute(0, 2, 3, 1).contiguous()
     wpk = w.permute(0, 2, 3, 1).contiguous()
     out = torch.empty(B, H, H, cout, device="cuda", dtype=torch.bfloat16)

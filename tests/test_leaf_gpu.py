@@ -6,6 +6,7 @@
 * whole models with every nn.Conv2d / nn.Linear swapped for a subclass exactly the way the CIM tool does it
   (`new.weight = module.weight`): the swapped layers' own forwards run, the rest runs on the HIP leaves, and the
   output / gradients match the oracle (cond UNet) and the reference fixture (VQVAE encode / decode)."""
+import copy
 import os
 
 import pytest
@@ -32,16 +33,19 @@ def rel(a, b):
 
 
 def _check(mod, inputs, leaf_fn, ref_fn, tol=2e-2):
+    """leaf_fn(*gpu inputs) through the HIP leaf path against ref_fn(cpu module copy, *cpu inputs): the torch
+    reference runs in fp32 on the host (no MIOpen / hipBLASLt kernel in the comparison)."""
     from sdmi import leaf as LF  # noqa: F401
     xs = [x.clone().cuda().requires_grad_(True) for x in inputs]
-    xr = [x.clone().cuda().requires_grad_(True) for x in inputs]
+    xr = [x.clone().requires_grad_(True) for x in inputs]
+    mc = copy.deepcopy(mod).cpu()
     y = leaf_fn(*xs)
-    yr = ref_fn(*xr)
+    yr = ref_fn(mc, *xr)
     assert rel(y.detach(), yr.detach()) <= tol
-    g = torch.randn(yr.shape, generator=torch.Generator().manual_seed(1)).cuda()
+    g = torch.randn(yr.shape, generator=torch.Generator().manual_seed(1))
     params = [p for p in mod.parameters()]
-    gl = torch.autograd.grad(y, xs + params, g, allow_unused=True)
-    gr = torch.autograd.grad(yr, xr + params, g, allow_unused=True)
+    gl = torch.autograd.grad(y, xs + params, g.cuda(), allow_unused=True)
+    gr = torch.autograd.grad(yr, xr + [p for p in mc.parameters()], g, allow_unused=True)
     for a, b in zip(gl, gr):
         if b is None:
             continue
@@ -55,7 +59,7 @@ def test_conv2d_leaf(cin, cout, k, s, p):
     torch.manual_seed(0)
     m = nn.Conv2d(cin, cout, k, s, p).cuda()
     x = torch.randn(2, cin, 12, 10)
-    _check(m, [x], lambda a: LF.conv2d(m, a), lambda a: F.conv2d(a, m.weight, m.bias, s, p))
+    _check(m, [x], lambda a: LF.conv2d(m, a), lambda m_, a: F.conv2d(a, m_.weight, m_.bias, s, p))
 
 
 def test_conv_transpose_linear_gn_silu_leaves():
@@ -63,18 +67,18 @@ def test_conv_transpose_linear_gn_silu_leaves():
     torch.manual_seed(1)
     ct = nn.ConvTranspose2d(16, 16, 4, 2, 1).cuda()
     _check(ct, [torch.randn(2, 16, 6, 5)], lambda a: LF.conv_transpose2d(ct, a),
-           lambda a: F.conv_transpose2d(a, ct.weight, ct.bias, 2, 1))
+           lambda m_, a: F.conv_transpose2d(a, m_.weight, m_.bias, 2, 1))
     lin = nn.Linear(24, 40).cuda()
-    _check(lin, [torch.randn(6, 24)], lambda a: LF.linear(lin, a), lambda a: F.linear(a, lin.weight, lin.bias))
-    _check(lin, [torch.randn(2, 7, 24)], lambda a: LF.linear(lin, a), lambda a: F.linear(a, lin.weight, lin.bias))
+    _check(lin, [torch.randn(6, 24)], lambda a: LF.linear(lin, a), lambda m_, a: F.linear(a, m_.weight, m_.bias))
+    _check(lin, [torch.randn(2, 7, 24)], lambda a: LF.linear(lin, a), lambda m_, a: F.linear(a, m_.weight, m_.bias))
     gn = nn.GroupNorm(8, 32).cuda()
     with torch.no_grad():
         gn.weight.uniform_(0.5, 1.5)
         gn.bias.uniform_(-0.5, 0.5)
-    _check(gn, [torch.randn(2, 32, 9, 7)], lambda a: LF.group_norm(gn, a), lambda a: gn(a))
-    _check(gn, [torch.randn(2, 32, 63)], lambda a: LF.group_norm(gn, a, silu=True), lambda a: F.silu(gn(a)))
+    _check(gn, [torch.randn(2, 32, 9, 7)], lambda a: LF.group_norm(gn, a), lambda m_, a: m_(a))
+    _check(gn, [torch.randn(2, 32, 63)], lambda a: LF.group_norm(gn, a, silu=True), lambda m_, a: F.silu(m_(a)))
     seq = nn.Sequential(nn.SiLU(), lin)
-    _check(lin, [torch.randn(3, 24)], lambda a: LF.call(seq, a), lambda a: seq(a))
+    _check(lin, [torch.randn(3, 24)], lambda a: LF.call(seq, a), lambda m_, a: m_(F.silu(a)))
 
 
 @pytest.mark.parametrize("cross", [False, True])
@@ -85,9 +89,9 @@ def test_mha_leaf(cross):
     q = torch.randn(2, 50, 64)
     if cross:
         kv = torch.randn(2, 13, 64)
-        _check(m, [q, kv], lambda a, c: LF.call(m, a, c, c)[0], lambda a, c: m(a, c, c)[0])
+        _check(m, [q, kv], lambda a, c: LF.call(m, a, c, c)[0], lambda m_, a, c: m_(a, c, c)[0])
     else:
-        _check(m, [q], lambda a: LF.call(m, a, a, a)[0], lambda a: m(a, a, a)[0])
+        _check(m, [q], lambda a: LF.call(m, a, a, a)[0], lambda m_, a: m_(a, a, a)[0])
 
 
 def test_down_block_standalone_vs_oracle():
@@ -259,4 +263,4 @@ def test_linear_leaf_ragged_features():
     from sdmi import leaf as LF
     torch.manual_seed(8)
     lin = nn.Linear(28, 13).cuda()
-    _check(lin, [torch.randn(2, 9, 28)], lambda a: LF.linear(lin, a), lambda a: F.linear(a, lin.weight, lin.bias))
+    _check(lin, [torch.randn(2, 9, 28)], lambda a: LF.linear(lin, a), lambda m_, a: F.linear(a, m_.weight, m_.bias))
