@@ -17,7 +17,6 @@ for MI355X:
 Parameters are referenced by the reference's state-dict keys.
 """
 import contextlib
-import os
 
 import torch
 
@@ -30,7 +29,6 @@ from . import plan
 # 13.94 / 13.90, P >= 1024 13.89 / 13.89, none 13.98 / 13.99 ms -- at 16^2 and below the statistics epilogue and the
 # statistics reducer cost more than the standalone single-pass GroupNorm they replace.
 GN_FUSE_MIN_P = 1024
-_GN_DEFER = os.environ.get("SDMI_GN_DEFER", "0") != "0"  # A/B
 
 
 def _gn_req(x, tab, P, C, silu):
@@ -1170,8 +1168,9 @@ class UNetEngine:
 
     def _gn_defer(self):
         """GroupNorm backward dgamma / dbeta: summed over the batch on a weight-gradient stream at the block's flush
-        (kernels.gn_bwd(defer=...)) -- the data-gradient chain then carries no batch tail per GroupNorm."""
-        return self._pending_gn if (self._grouping() and _GN_DEFER) else None
+        (kernels.gn_bwd(defer=...)) -- the data-gradient chain then carries no batch tail per GroupNorm. Same-box A/B
+        of the cond-UNet step: 13.55 / 13.49 ms inline, 13.37 / 13.34 ms deferred."""
+        return self._pending_gn if self._grouping() else None
 
     def _join(self):
         """The current stream waits for all weight-gradient work issued so far."""
