@@ -17,10 +17,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--gaps", type=int, default=25)
+    ap.add_argument("--marker", default="norm_finalize_kernel", help="kernel that ends a step (ddpm_prev_kernel: sampling)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if "norm_finalize_kernel" in r["Kernel_Name"]]
+    marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     step = rows[marks[-2] + 1: marks[-1] + 1]
     t0 = int(step[0]["Start_Timestamp"])
     t1 = int(step[-1]["End_Timestamp"])
