@@ -198,7 +198,8 @@ int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy, void* dx,
 
 /* The two GroupNorm backward forms with dgamma / dbeta deferred: rows [B][C][2] receives the per-(batch row, channel)
  * sums {sum dz, sum dz*xhat} and the launch has no batch tail; sdmi_gn_rows_sum then writes dbeta[c] = sum_b rows[b][c][0]
- * and dgamma[c] = sum_b rows[b][c][1] (in batch order) -- e.g. on a side stream, off the data-gradient chain. */
+ * and dgamma[c] = sum_b rows[b][c][1] (in batch order; the fused forms' batch tail may group the rows differently, so
+ * the two agree to fp32 summation order) -- e.g. on a side stream, off the data-gradient chain. */
 int sdmi_gn_bwd_rows(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
                      const float* gamma, int B, int P, int C, int G, int silu, float* ws, float* table2_ws, float* rows,
                      const void* addend, int ldadd, sdmi_stream_t stream);
@@ -206,6 +207,16 @@ int sdmi_gn_bwd_part_rows(const void* x, int ldx, const void* dy, int lddy, void
                           const float* gamma, int B, int P, int C, int G, int silu, const float* part, int rb, float* ws,
                           float* rows, const void* addend, int ldadd, sdmi_stream_t stream);
 int sdmi_gn_rows_sum(const float* rows, int B, int C, float* dgamma, float* dbeta, sdmi_stream_t stream);
+/* Up to SDMI_GN_ROWS_GROUP_MAX rows buffers summed in ONE launch (each job exactly as sdmi_gn_rows_sum, bitwise): the
+ * deferred GroupNorm sums of one UNet block are issued together at its weight-gradient flush. */
+#define SDMI_GN_ROWS_GROUP_MAX 16
+typedef struct {
+  const float* rows;
+  float* dgamma;
+  float* dbeta;
+  int B, C;
+} sdmi_gn_rows_job;
+int sdmi_gn_rows_sum_grouped(const sdmi_gn_rows_job* jobs, int njobs, sdmi_stream_t stream);
 
 
 int sdmi_chan_sum(const void* dy, int lddy, int B, int P, int C, float* ws, void* per_bc, int ld_bc, float* per_c,

@@ -1109,6 +1109,27 @@ __global__ __launch_bounds__(NT) void gn_rows_sum_kernel(const float2* rows, int
   dbeta[c] = s1;
   dgamma[c] = s2;
 }
+
+struct RowsGroup {
+  sdmi_gn_rows_job j[SDMI_GN_ROWS_GROUP_MAX];
+};
+
+// blockIdx.y = job; the same per-channel batch-ordered sum as gn_rows_sum_kernel
+__global__ __launch_bounds__(NT) void gn_rows_sum_grouped_kernel(const RowsGroup g) {
+  const sdmi_gn_rows_job& J = g.j[blockIdx.y];
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= J.C) return;
+  const float2* rows = (const float2*)J.rows;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+  for (int b = 0; b < J.B; ++b) {
+    const float2 v = rows[(long long)b * J.C + c];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  J.dbeta[c] = s1;
+  J.dgamma[c] = s2;
+}
 }  // namespace
 
 extern "C" int sdmi_gn_bwd_part(const void* x, int ldx, const void* dy, int lddy, void* dx, int lddx, const float* table,
@@ -1132,6 +1153,21 @@ extern "C" int sdmi_gn_rows_sum(const float* rows, int B, int C, float* dgamma, 
   if (!rows || !dgamma || !dbeta || B <= 0 || C <= 0 || ((uintptr_t)rows & 7)) return -1;
   sdmi_rt::launch(gn_rows_sum_kernel, dim3((C + NT - 1) / NT), dim3(NT), 0, (hipStream_t)stream, (const float2*)rows, B,
                   C, dgamma, dbeta);
+  SDMI_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int sdmi_gn_rows_sum_grouped(const sdmi_gn_rows_job* jobs, int njobs, sdmi_stream_t stream) {
+  if (!jobs || njobs <= 0 || njobs > SDMI_GN_ROWS_GROUP_MAX) return -1;
+  RowsGroup g = {};
+  int cmax = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const sdmi_gn_rows_job& J = jobs[i];
+    if (!J.rows || !J.dgamma || !J.dbeta || J.B <= 0 || J.C <= 0 || ((uintptr_t)J.rows & 7)) return -1;
+    g.j[i] = J;
+    cmax = J.C > cmax ? J.C : cmax;
+  }
+  sdmi_rt::launch(gn_rows_sum_grouped_kernel, dim3((cmax + NT - 1) / NT, njobs), dim3(NT), 0, (hipStream_t)stream, g);
   SDMI_CHECK_LAUNCH();
   return 0;
 }

@@ -59,6 +59,14 @@ _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlon
 _SZ = ctypes.c_size_t
 
 
+class GnRowsJob(ctypes.Structure):
+    _fields_ = [("rows", ctypes.c_void_p), ("dgamma", ctypes.c_void_p), ("dbeta", ctypes.c_void_p),
+                ("B", ctypes.c_int), ("C", ctypes.c_int)]
+
+
+GN_ROWS_GROUP_MAX = 16
+
+
 class TPackDesc(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p)] + [(n, ctypes.c_int) for n in (
         "O", "I", "taps", "src_ld", "src_tap", "dst_ld", "dst_tap")] + [("smap", ctypes.c_byte * 16)]
@@ -95,6 +103,7 @@ SIGNATURES = {
     "sdmi_gn_bwd_rows": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _P], _I),
     "sdmi_gn_bwd_part_rows": ([_P, _I, _P, _I, _P, _I, _P, _P, _I, _I, _I, _I, _I, _P, _I, _P, _P, _P, _I, _P], _I),
     "sdmi_gn_rows_sum": ([_P, _I, _I, _P, _P, _P], _I),
+    "sdmi_gn_rows_sum_grouped": ([_P, _I, _P], _I),
     "sdmi_chan_sum": ([_P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _I, _P], _I),
     "sdmi_prep_input": ([_P, _I, _I, _I, _I, _P, _I, _I, _I, _P, _I, _P, _I, _P, _P], _I),
     "sdmi_cond_wgrad": ([_P, _I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P], _I),

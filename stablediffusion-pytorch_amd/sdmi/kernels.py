@@ -444,6 +444,17 @@ def gn_rows_sum(rows, B, C, dgamma, dbeta):
         check(_lib.lib().sdmi_gn_rows_sum(_p(rows), B, C, _p(dgamma), _p(dbeta), _stream()), "sdmi_gn_rows_sum")
 
 
+def gn_rows_sum_grouped(jobs):
+    """Several deferred GroupNorm sums [(rows, B, C, dgamma, dbeta), ...] in one launch (bitwise gn_rows_sum each)."""
+    import ctypes
+    for i in range(0, len(jobs), _lib.GN_ROWS_GROUP_MAX):
+        part = jobs[i:i + _lib.GN_ROWS_GROUP_MAX]
+        arr = (_lib.GnRowsJob * len(part))(*[_lib.GnRowsJob(_p(r), _p(dg), _p(db), B, C) for r, B, C, dg, db in part])
+        with _Prof("gn_rows_sum", 0, f"grouped n={len(part)}"):
+            check(_lib.lib().sdmi_gn_rows_sum_grouped(ctypes.cast(arr, ctypes.c_void_p), len(part), _stream()),
+                  "sdmi_gn_rows_sum_grouped")
+
+
 def chan_sum(dy, B, P, C, *, per_bc=None, per_c=None, per_c2=None, c_store=0):
     """per-(b,c) sums over pixels -> per_bc (bf16 2-D view [B, ld]) and per-channel sums (fp32)."""
     L = _lib.lib()

@@ -1160,8 +1160,7 @@ class UNetEngine:
             plan.wait_stream(side, torch.cuda.current_stream(self.device))
             self._keep.extend(g[0] for g in gpend)
             with torch.cuda.stream(side):
-                for rows, B, C, dg, db in gpend:
-                    K.gn_rows_sum(rows, B, C, dg, db)
+                K.gn_rows_sum_grouped(gpend)
 
     _pending_wg = {}
     _pending_gn = []

@@ -141,6 +141,52 @@ def test_groupnorm_bwd_from_gemm_statistics(B, H, C, prod, silu, splits, monkeyp
     k.gn_bwd(x, dy, dx2, tab, gamma, B, P, C, G, silu, dg, db, addend=add, gn=req2)
     torch.cuda.synchronize()
     assert torch.equal(dx2, dx)
+    # dgamma / dbeta deferred (per-sample rows, summed by the grouped rows-sum launch): the same bits
+    pend = []
+    dx3, dg3, db3 = torch.empty_like(x), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    req3 = k.gn_request(x, tab, P, C, silu)
+    run(dy, req3)
+    k.gn_bwd(x, dy, dx3, tab, gamma, B, P, C, G, silu, dg3, db3, addend=add, gn=req3, defer=pend)
+    assert len(pend) == 1
+    k.gn_rows_sum_grouped(pend)
+    torch.cuda.synchronize()
+    assert torch.equal(dx3, dx)
+    assert relerr(dg3, dg) < 1e-5 and relerr(db3, db) < 1e-5  # the inline tail may group the batch rows differently
+
+
+@pytest.mark.parametrize("shapes", [[(2, 8, 64)], [(32, 32, 384), (32, 16, 512), (32, 4, 768)],
+                                    [(4, 8, 96)] * 17])  # 17 jobs: two grouped launches
+def test_groupnorm_bwd_deferred_sums_match_inline(shapes):
+    """sdmi_gn_bwd_rows (dgamma / dbeta as per-sample rows, no batch tail) + sdmi_gn_rows_sum_grouped over several
+    GroupNorms against the inline sdmi_gn_bwd: dx bitwise equal, dgamma / dbeta to fp32 summation order (the inline
+    batch tail of a narrow strip sums interleaved groups of batch rows, the rows sum runs in batch order); the grouped
+    launch bitwise equals one sdmi_gn_rows_sum per GroupNorm."""
+    k = K()
+    torch.manual_seed(2)
+    pend, refs, outs = [], [], []
+    for B, H, C in shapes:
+        P, G = H * H, 32
+        x = bf(torch.randn(B * P, C, device="cuda") * 2 + 0.5)
+        gamma = torch.randn(C, device="cuda") * 0.1 + 1
+        beta = torch.randn(C, device="cuda") * 0.1
+        tab = k.gn_fwd(x, B, P, C, G, gamma, beta, True, torch.empty_like(x))
+        dy = bf(torch.randn(B * P, C, device="cuda"))
+        dx_ref, dx = torch.empty_like(x), torch.empty_like(x)
+        dg_ref, db_ref, dg, db = (torch.empty(C, device="cuda") for _ in range(4))
+        k.gn_bwd(x, dy, dx_ref, tab, gamma, B, P, C, G, True, dg_ref, db_ref)
+        k.gn_bwd(x, dy, dx, tab, gamma, B, P, C, G, True, dg, db, defer=pend)
+        refs.append((dx_ref, dg_ref, db_ref))
+        outs.append((dx, dg, db))
+    assert len(pend) == len(shapes)
+    k.gn_rows_sum_grouped(pend)
+    single = [(torch.empty_like(dg), torch.empty_like(db)) for (_, dg, db) in outs]
+    for (rows, B, C, _, _), (dg1, db1) in zip(pend, single):
+        k.gn_rows_sum(rows, B, C, dg1, db1)
+    torch.cuda.synchronize()
+    for (a, b, c), (a2, b2, c2), (b3, c3) in zip(refs, outs, single):
+        assert torch.equal(a2, a)
+        assert relerr(b2, b) < 1e-5 and relerr(c2, c) < 1e-5
+        assert torch.equal(b3, b2) and torch.equal(c3, c2)
 
 
 # d = 8, 24, 40 take the forward's ones-column row sum (d % 16 == 8), incl. ragged N and S = 77
