@@ -304,6 +304,13 @@ def linear_wgrad(dy, x, out, *, bias_grad=None, bias_grad2=None, group_sums=None
                 sum_out=bias_grad, sum_out2=bias_grad2, gsum=group_sums, sum_group=group, m_store=m_store)
 
 
+# Mainloop of grouped weight-gradient launches: variant 3 (LDS-DMA ring, 3 stages of 32-deep k; variant 2 where bias
+# reduction columns ride along). The tuned table holds single-problem entries, mostly the register-staged mainloop,
+# which lost to the DMA ring once 6-8 problems share the grid. Same box: cond-UNet 13.36 / 13.30 -> 13.29 / 13.27 ms,
+# DiT-12L 3.56 / 3.56 -> 3.53 / 3.52 ms.
+GROUPED_VARIANT = 3
+
+
 def linear_wgrad_grouped(items):
     """linear_wgrad of several same-shape problems in ONE launch (sdmi_gemm_grouped): items = [(dy, x, out,
     bias_grad or None)], all dy / x of one shape and row stride, all bias_grad present or all None. The split count is
@@ -337,6 +344,8 @@ def linear_wgrad_grouped(items):
                 descs[i].splits_hint, descs[i].variant_hint = e[0], e[1]
             else:
                 descs[i].splits_hint = e
+    for i in range(G):  # the LDS-DMA mainloop (GROUPED_VARIANT), whatever the single problem's tuned entry
+        descs[i].variant_hint = GROUPED_VARIANT
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_grouped_plan(descs, G, ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_grouped_plan")

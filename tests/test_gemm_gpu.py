@@ -207,7 +207,7 @@ def test_conv_wgrad_with_fused_bias_and_group_sums():
                                          (8, 1024, 128, 128, True)])
 def test_grouped_weight_gradients_match_single_launches(G, M, N, K, bias):
     """sdmi_gemm_grouped: G same-shape weight gradients in one launch give, per problem, exactly the single launch's
-    result at the same split count (weights and bias sums bitwise), with and without split-K."""
+    result at the same split count and mainloop (weights and bias sums bitwise), with and without split-K."""
     from sdmi import _lib, kernels as K_
     import ctypes
     saved, K_.TUNED = K_.TUNED, {}  # built-in heuristics on both sides (no per-shape table hints)
@@ -234,6 +234,7 @@ def _grouped_check(G, M, N, K, bias, _lib, K_, ctypes):
     d.a, d.lda, d.b, d.ldb = items[0][0].data_ptr(), N, items[0][1].data_ptr(), K
     d.c, d.ldc, d.c_f32, d.alpha = items[0][2].data_ptr(), K, 1, 1.0
     d.sum_out = K_._p(items[0][3])
+    d.variant_hint = K_.GROUPED_VARIANT  # the grouped launch's mainloop
     descs = (K_.GemmDesc * G)(*([d] * G))
     sp = ctypes.c_int(0)
     wsb = ctypes.c_size_t(0)
