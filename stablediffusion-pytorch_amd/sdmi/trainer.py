@@ -149,7 +149,8 @@ class DDPMTrainer:
         # side stream, each chunk ending in an event that the engine waits for only where the forward first reads
         # one of that chunk's parameters or packed weights (UNet engine, 6 chunks).
         # DiT: the forward's first GEMM (every layer's adaLN table) needs the largest chunk at once, so pipelining
-        # measured no gain there (4.00 ms/step unchunked vs 4.04-4.07 at 6 chunks): one chunk
+        # measured no gain there (4.00 ms/step unchunked vs 4.04-4.07 at 6 chunks; round 4: 3.53 / 3.53 unchunked vs
+        # 3.55 / 3.55, 3.53 / 3.53, 3.54 / 3.53 at 2 / 3 / 6 forward-ordered chunks): one chunk
         nchunks = 1 if base == "dit" else 6
         self.opt_ranges = None
         if nchunks > 1 and getattr(self.engine, "side", None) is not None:
