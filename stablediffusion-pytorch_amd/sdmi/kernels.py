@@ -160,8 +160,6 @@ def gemm(m, n, k, a, a_mode, lda, b, b_mode, ldb, c, ldc, *, geom=None, bias=Non
             d.splits_hint, d.variant_hint = e[0], e[1]
         else:
             d.splits_hint = e
-    if a_mode == _lib.A_COLMAJOR and d.variant_hint in (0, 1):
-        d.variant_hint = COLMAJOR_VARIANT
     splits = ctypes.c_int(1)
     ws_bytes = ctypes.c_size_t(0)
     check(L.sdmi_gemm_plan(ctypes.byref(d), ctypes.byref(splits), ctypes.byref(ws_bytes)), "sdmi_gemm_plan")
@@ -305,12 +303,6 @@ def linear_wgrad(dy, x, out, *, bias_grad=None, bias_grad2=None, group_sums=None
     return gemm(N, K, M, dy, _lib.A_COLMAJOR, ld_of(dy), x, _lib.B_KN, ld_of(x), out, out.stride(0),
                 sum_out=bias_grad, sum_out2=bias_grad2, gsum=group_sums, sum_group=group, m_store=m_store)
 
-
-# Mainloop of single col-major-A (weight-gradient) launches whose table entry is the register-staged one (or none): the
-# 2-stage LDS-DMA ring (the library falls back to register staging where DMA cannot run the launch's reductions). The
-# tuner measured those shapes alone on an idle GPU; in the step, beside the data-gradient chain, the DMA ring wins:
-# same box, cond-UNet 13.19 / 13.18 -> 13.15 / 13.16 ms, DiT-12L 3.51 / 3.50 -> 3.49 / 3.51 ms.
-COLMAJOR_VARIANT = 2
 
 # Mainloop of grouped weight-gradient launches: variant 3 (LDS-DMA ring, 3 stages of 32-deep k; variant 2 where bias
 # reduction columns ride along). The tuned table holds single-problem entries, mostly the register-staged mainloop,
