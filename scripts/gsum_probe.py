@@ -1,0 +1,51 @@
+"""Run-to-run determinism of the weight-gradient GEMM's reduction outputs (bias sums, second bias, per-sample group
+sums = the time-embedding gradient) for 3x3 conv and linear weight gradients, register staging (v1) vs the LDS-DMA ring
+(v2), split counts 1 / 2 / 4 / 8: each launch repeated 12 times and compared bitwise with the first."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "stablediffusion-pytorch_amd"), REPO]
+import torch  # noqa: E402
+
+
+def main():
+    from sdmi import kernels as K
+    g = torch.Generator().manual_seed(5)
+    bad = 0
+    for (B, H, C, O) in [(2, 32, 32, 64), (2, 16, 64, 64), (2, 8, 64, 128), (4, 8, 32, 32), (2, 4, 128, 128)]:
+        x = torch.randn(B * H * H, C, generator=g).to(torch.bfloat16).cuda()
+        dy = (torch.randn(B * H * H, O, generator=g) * 0.5).to(torch.bfloat16).cuda()
+        for v in (1, 2):
+            for sp in (1, 2, 4, 8):
+                K.TUNED = {"__all__": [sp, v]}
+                saved = K.gemm_key
+                K.gemm_key = lambda d: "__all__"  # noqa: E731
+                outs = []
+                try:
+                    for _ in range(12):
+                        dw = torch.full((O, 9 * C), float("nan"), device="cuda")
+                        bg = torch.full((O,), float("nan"), device="cuda")
+                        bg2 = torch.full((O,), float("nan"), device="cuda")
+                        gs = torch.full((B, O), float("nan"), device="cuda", dtype=torch.bfloat16)
+                        K.conv_wgrad(dy, O, x, B, H, H, C, C, O, 3, 3, 1, 1, dw, H, H, bias_grad=bg, bias_grad2=bg2,
+                                     group_sums=gs)
+                        outs.append((dw, bg, bg2, gs))
+                finally:
+                    K.gemm_key = saved
+                torch.cuda.synchronize()
+                ref = dy.float().view(B, H * H, O).sum(1)
+                o0 = outs[0]
+                same = all(all(torch.equal(a, b) for a, b in zip(o, o0)) for o in outs[1:])
+                gerr = ((o0[3].float() - ref).abs().max() / (ref.abs().max() + 1e-9)).item()
+                berr = ((o0[1] - ref.sum(0)).abs().max() / (ref.sum(0).abs().max() + 1e-9)).item()
+                nan = any(bool(torch.isnan(t.float()).any()) for t in o0)
+                flag = "" if (same and gerr < 2e-2 and berr < 1e-3 and not nan) else "  <-- MISMATCH"
+                bad += bool(flag)
+                print(f"B={B} H={H} C={C} O={O} v={v} splits={sp}: deterministic={same} gsum_err={gerr:.2e} "
+                      f"bias_err={berr:.2e} nan={nan}{flag}", flush=True)
+    print("bad", bad)
+
+
+if __name__ == "__main__":
+    main()
