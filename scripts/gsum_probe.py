@@ -13,17 +13,20 @@ def main():
     from sdmi import kernels as K
     g = torch.Generator().manual_seed(5)
     bad = 0
-    for (B, H, C, O) in [(2, 32, 32, 64), (2, 16, 64, 64), (2, 8, 64, 128), (4, 8, 32, 32), (2, 4, 128, 128)]:
+    shapes = [(2, 32, 32, 64), (2, 16, 64, 64), (2, 8, 64, 128), (4, 8, 32, 32), (2, 4, 128, 128)]
+    if "--step-shapes" in sys.argv:  # the B = 32 cond-UNet's resnet conv1 weight gradients (with t-emb group sums)
+        shapes = [(32, 32, 384, 384), (32, 16, 512, 512), (32, 8, 768, 768), (32, 4, 768, 768)]
+    for (B, H, C, O) in shapes:
         x = torch.randn(B * H * H, C, generator=g).to(torch.bfloat16).cuda()
         dy = (torch.randn(B * H * H, O, generator=g) * 0.5).to(torch.bfloat16).cuda()
         for v in (1, 2):
-            for sp in (1, 2, 4, 8):
+            for sp in ((1, 2, 4, 8) if "--step-shapes" not in sys.argv else (1, 3, 6, 8, 12)):
                 K.TUNED = {"__all__": [sp, v]}
                 saved = K.gemm_key
                 K.gemm_key = lambda d: "__all__"  # noqa: E731
                 outs = []
                 try:
-                    for _ in range(12):
+                    for _ in range(12 if "--step-shapes" not in sys.argv else 4):
                         dw = torch.full((O, 9 * C), float("nan"), device="cuda")
                         bg = torch.full((O,), float("nan"), device="cuda")
                         bg2 = torch.full((O,), float("nan"), device="cuda")
