@@ -1178,6 +1178,10 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   __syncthreads();
   EpiArgs ev = epi_args_late();  // epilogue arguments loaded only from here on (see gemm_kernel)
   if (grp) group_epi(ev, g.Cg[grp], g.sum_g[grp], grp);
+  // The column tiles of this kernel cover only the n GEMM columns; the reduction columns [n_x0, n_gemm) of a split-K
+  // slab belong to the reduction tiles below. The last column tile's padding (n % TBN != 0) must not store its zero
+  // accumulators there: it raced with the reduction tile's stores of the same slab entries (round-4 gsum probe).
+  if (RED == 2) ev.n_gemm = ev.n_x0;
   const EpiArgs* ep = &ev;
   if (RED != 0 && red_tile) {
     // lane holds C[wm + 16i + 4(lane>>4) + q][r*16 + (lane & 15)]: column 0 = row sums, 8 + j = group j
