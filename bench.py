@@ -61,38 +61,60 @@ def kernel_name(tag, info):
     if v >= 7:  # 64-row tiles
         return f"gemm_dma_kernel<{a}, {b}, {stages}, {tn}, 64>"
     return f"gemm_dma_kernel<{a}, {b}, {stages}, {tn}>"
-def _latest(pattern):
-    """newest round's committed evidence file (profiles/rNN_*)"""
+def _evidence_files(workload, kind):
+    """Committed rocprofv3 evidence of `workload` (kind 'pmc_traffic' or 'roofline_evidence'), newest round first:
+    profiles/rNN_<workload>_<kind>.json, written by scripts/gpu_profile.sh from the tree whose source digest
+    (sdmi._build.source_digest) each file records."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", pattern)))
-    return files[-1] if files else os.path.join(REPO, "profiles", pattern.replace("r*", "r01"))
+    wl = workload.replace("-", "_")
+    return sorted(glob.glob(os.path.join(REPO, "profiles", f"r[0-9]*_{wl}_{kind}.json")), reverse=True)
 
 
-PMC_FILE = _latest("r*_pmc_traffic.json")
-ROOF_FILE = _latest("r*_roofline_evidence.json")
+def _load_evidence(workload, kind, digest):
+    """(table, file name, digest matches the running tree) of the newest evidence file measured on THIS tree, else of
+    the newest one at all (flagged stale), else (None, None, False)."""
+    files = _evidence_files(workload, kind)
+    loaded = []
+    for f in files:
+        try:
+            loaded.append((json.load(open(f)), f))
+        except (OSError, ValueError):
+            continue
+    for d, f in loaded:
+        if d.get("_meta", {}).get("source_digest") == digest:
+            return d, os.path.basename(f), True
+    if loaded:
+        return loaded[0][0], os.path.basename(loaded[0][1]), False
+    return None, None, False
 
 
-def pmc_traffic(kernel, unsplit):
-    """(HBM bytes per launch of `kernel` -- read x2-corrected FETCH_SIZE + WRITE_SIZE -- from the committed rocprofv3
-    --pmc passes of this same bench command, unit note) or (None, None). `unsplit`: the bench times only the unsplit
-    launches, so the per-dispatch figure over those launches (scripts/roofline_evidence.py ->
-    profiles/r01_roofline_evidence.json) is preferred; otherwise the all-launch average (profiles/*_pmc_traffic.json)."""
-    try:
-        d = json.load(open(ROOF_FILE))
-        if unsplit and d.get("kernel") == kernel and d.get("traffic_bytes_per_launch"):
-            return d["traffic_bytes_per_launch"], ("bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, the kernel's "
-                                                   "unsplit launches: the ones timed here)")
-    except (OSError, KeyError, TypeError, ValueError):
-        pass
-    try:
-        table = json.load(open(PMC_FILE))
-        # bench-style "gemm_dma_kernel<1, 0, 2, 128>" also names the full instantiation "...<1, 0, 2, 128, 128, ...>"
-        key = kernel if kernel in table else next(k for k in table if k.startswith(kernel[:-1] + ","))
-        d = table[key]
-        return (d["read_bytes_per_launch"] + d["write_bytes_per_launch"],
-                "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, all launches of the kernel)")
-    except (OSError, KeyError, TypeError, ValueError, StopIteration):
-        return None, None
+def pmc_traffic(workload, kernel, unsplit):
+    """HBM bytes per launch of `kernel` (read x2-corrected FETCH_SIZE + WRITE_SIZE) from the committed rocprofv3 --pmc
+    passes of this same bench command: the roofline-evidence file (scripts/roofline_evidence.py: exactly the launches
+    the bench times -- unsplit ones, or all) when it names this kernel and launch set, else the per-kernel table
+    (scripts/pmc_summary.py, all launches). Returns (bytes or None, provenance dict)."""
+    from sdmi._build import source_digest
+    digest = source_digest()
+    ev, ev_file, ev_ok = _load_evidence(workload, "roofline_evidence", digest)
+    launches = "unsplit" if unsplit else "all"
+    if ev and ev.get("kernel") == kernel and ev.get("launches") == launches and ev.get("traffic_bytes_per_launch"):
+        return ev["traffic_bytes_per_launch"], {
+            "file": ev_file, "tree_digest": digest, "measured_on_this_tree": ev_ok,
+            "unit": f"bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, the kernel's {launches} launches: the ones "
+                    "timed here)", "trace_avg_us": ev.get("trace_avg_us")}
+    table, t_file, t_ok = _load_evidence(workload, "pmc_traffic", digest)
+    if table:
+        # bench-style "gemm_dma_kernel<1, 0, 2, 128>" also names the full instantiations "...<1, 0, 2, 128, 128, ...>":
+        # their launch-weighted average
+        keys = [k for k in table if k == kernel or k.startswith(kernel[:-1] + ",")]
+        n = sum(table[k]["launches"] for k in keys)
+        if n:
+            b = sum((table[k]["read_bytes_per_launch"] + table[k]["write_bytes_per_launch"]) * table[k]["launches"]
+                    for k in keys) / n
+            return b, {"file": t_file, "tree_digest": digest, "measured_on_this_tree": t_ok,
+                       "unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE, all launches of the kernel)",
+                       "instantiations": keys}
+    return None, {"file": None, "tree_digest": digest, "measured_on_this_tree": False}
 
 
 def uncond_config():
@@ -490,6 +512,11 @@ def main():
     ap.add_argument("--grad-wire", default=None, choices=("fp32", "bf16"),
                     help="N > 1: gradient all-reduce wire format (default fp32 as the reference's DDP; bf16 halves "
                          "the bytes)")
+    ap.add_argument("--force-reducer", action="store_true",
+                    help="N = 1 only: run the headline step with the N > 1 gradient path forced on -- an RCCL ('nccl') "
+                         "process group of one rank, the bucketed all-reduce reducer on its stream and the per-bucket "
+                         "norm blocks (sdmi.reducer) -- and report exchange_tail_ms: the part of the N > 1 step that "
+                         "this one-GPU pool can time")
     ap.add_argument("--issue", default="plan", choices=("plan", "eager", "graph"),
                     help="plan (default): the step recorded once and its native calls replayed (sdmi.plan); eager: "
                          "per-step Python issue; graph: single-stream hipGraph (N == 1)")
@@ -513,6 +540,14 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     collectives = collective_facts(world, device)
+    forced = args.force_reducer and world == 1
+    if forced:  # an RCCL group of one rank: the reducer's all-reduces are identities, their cost is real
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]))
+        sk.close()
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=device)
 
     from sdmi.trainer import DDPMTrainer, S_LOSS, S_NORM, S_SKIP
     from sdmi import kernels as K
@@ -529,7 +564,8 @@ def main():
         return main_vqvae_train(args, wl, world, rank, device)
     cfg = dit_config() if is_dit else (uncond_config() if is_uncond else cond_config())
     torch.manual_seed(1111)  # identical initial weights on every rank (DDP broadcasts rank 0's)
-    group = dist.group.WORLD if world > 1 else None
+    group = dist.group.WORLD if (world > 1 or forced) else None
+    red_kw = dict(force_reducer=True) if forced else {}
     single = args.issue == "graph" and world == 1  # single-stream hipGraph capture (weight gradients inline)
     if is_dit:
         from models.transformer import DIT
@@ -538,16 +574,16 @@ def main():
             if v.abs().max() == 0:  # the timed step runs on non-trivial data (zeros clock higher, MI355X DVFS)
                 v.normal_(0.0, 0.02)
         trainer = DDPMTrainer(cfg, init, device, base="dit", lr=1e-4, ema_decay=None, group=group,
-                              grad_wire=args.grad_wire, single_stream=single)
+                              grad_wire=args.grad_wire, single_stream=single, **red_kw)
     elif is_uncond:  # tools/train_ddpm_vqvae.py:76-104: Adam(ldm_lr 5e-6, celebhq.yaml:54), no clip, no EMA
         import models.unet_base as mu
         init = mu.Unet(4, cfg).state_dict()
         trainer = DDPMTrainer(cfg, init, device, base="uncond", lr=5e-6, ema_decay=None, max_grad_norm=float("inf"),
                               sched=(1000, 0.0015, 0.0195), group=group, grad_wire=args.grad_wire,
-                              single_stream=single)
+                              single_stream=single, **red_kw)
     else:
         init = mc.Unet(4, cfg).state_dict()
-        trainer = DDPMTrainer(cfg, init, device, group=group, grad_wire=args.grad_wire, single_stream=single)
+        trainer = DDPMTrainer(cfg, init, device, group=group, grad_wire=args.grad_wire, single_stream=single, **red_kw)
     B = args.batch
     x0, text, empty, mask = synthetic_batch(B, device, 1111 + rank)
     gen = torch.Generator(device=device).manual_seed(1111 + rank)
@@ -651,13 +687,14 @@ def main():
         # each event then including its split-K reducer (a lower bound on the kernel's own rate)
         use1 = d["n1"] > 0 and d["fl1"] >= 0.5 * d["fl"]
         dfl, dms, dn, dby = (d["fl1"], d["ms1"], d["n1"], d["by1"]) if use1 else (d["fl"], d["ms"], d["n"], d["by"])
-        traffic, traffic_unit = pmc_traffic(dname, use1)
+        traffic, traffic_src = pmc_traffic(args.workload, dname, use1)
         algo = dby / dn if dn else None  # algorithmic bytes per launch (sdmi.kernels.algo_bytes over the same launches)
-        roof = {"bound": "mfma", "kernel": f"sdmi {dname} ({d['mode']}: implicit-GEMM conv fwd/dgrad)"
+        roof = {"kernel_id": dname, "launch_set": "unsplit" if use1 else "all",
+                "bound": "mfma", "kernel": f"sdmi {dname} ({d['mode']}: implicit-GEMM conv fwd/dgrad)"
                 if d["mode"] == "gemm_a1b0" else f"sdmi {dname} ({d['mode']})",
                 "achieved": dfl / (dms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
                 "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic,
-                "traffic_unit": traffic_unit,
+                "traffic_unit": traffic_src.get("unit"), "traffic_source": traffic_src,
                 "algorithmic_bytes": algo,
                 "algorithmic_bytes_note": "per launch: unique operand bytes at their dtypes (conv im2col = the gathered "
                                           "activation), output and fused epilogue reads, averaged over the same launches",
@@ -695,7 +732,13 @@ def main():
         "issue": issue,
         "roofline": roof,
     }
-    if world > 1:
+    if forced:
+        result["forced_reducer"] = {
+            "note": "N = 1 with the N > 1 gradient path on: RCCL group of one rank, bucketed all-reduce on the reducer "
+                    "stream (identities at one rank), per-bucket norm blocks; compare ms_per_step with the plain line",
+            "backend": dist.get_backend(), "bucket_bytes": trainer.reducer.bucket * trainer.store.grads.element_size()}
+        result["config"]["parallelism"] = "dp1 + forced reducer"
+    if world > 1 or forced:
         result["collectives"] = collectives
         result["grad_wire"] = trainer.grad_wire
         if args.profile_gemm and tails:
@@ -708,7 +751,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline_dit(cfg) if is_dit else cpu_baseline(cfg, uncond=is_uncond)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if world > 1 or forced:
         dist.destroy_process_group()
 
 

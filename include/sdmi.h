@@ -407,6 +407,11 @@ int sdmi_pack_transpose(const sdmi_tpack_desc* descs_dev, const void* bmap_dev, 
 size_t sdmi_optim_workspace(void);
 int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws, int growth_interval,
                       int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
+/* any n: ws holds sdmi_optim_workspace_for(n) bytes (one fp32 partial per 128 Ki-gradient block; -3 if ws_bytes is
+ * smaller). sdmi_clip_unscale is this call with ws_bytes = sdmi_optim_workspace() (n up to ~268 M). */
+size_t sdmi_optim_workspace_for(long long n);
+int sdmi_clip_unscale_ws(const float* grads, long long n, float max_norm, float* state, float* ws, size_t ws_bytes,
+                         int growth_interval, int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream);
 int sdmi_loss_flag(const float* src, float* dst, int mode, sdmi_stream_t stream);
 /* sdmi_clip_finalize reduces the first n block partials (double accumulation, index order) and applies the clip /
  * skip / scaler update above. */

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Secondary bench lines of the round (DiT-12L step, captured DDPM / DDIM sampling at B = 1 and 8, uncond UNet, VQVAE)
+# Secondary bench lines of the round (DiT-12L step, captured DDPM / DDIM sampling at B = 1 and 8, uncond UNet, VQVAE
+# encode + decode and training (BASELINE config 2), the headline step with the N > 1 reducer forced on at N = 1)
 # and the bf16-wire rehearsal kernel traces (1 vs 3 steps): one JSON line each into gpurun_out/<tag>_bench_*.json
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -11,7 +12,9 @@ run() {  # name, bench args
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['ms_per_step'],3), 'ms')" gpurun_out/${T}_bench_$n.json $n
 }
 run dit --workload dit && run sample_1 --workload sample --steps 40 && run sample_8 --workload sample --sample-batch 8 --steps 40 \
-  && run sample_ddim --workload sample --sampler ddim --steps 40 && run uncond_unet --workload uncond-unet || exit 1
+  && run sample_ddim --workload sample --sampler ddim --steps 40 && run uncond_unet --workload uncond-unet \
+  && run vqvae --workload vqvae && run vqvae_train --workload vqvae-train --steps 10 \
+  && run cond_forced_reducer --force-reducer || exit 1
 for S in 1 3; do
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/wire_$S -o run -- python3 scripts/wire_rehearsal.py $S bf16 > gpurun_out/wire_$S.log 2>&1 || { tail -5 gpurun_out/wire_$S.log; exit 1; }
 done

@@ -1,6 +1,6 @@
 """Per-kernel average HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 FETCH_SIZE is doubled (gfx950 tallies 128-B requests of wide streaming reads at 64 B: MI355X_MICROARCH.md HBM).
-Usage: python scripts/pmc_summary.py <fetch_dir> <write_dir> [--json out.json]"""
+Usage: python scripts/pmc_summary.py <fetch_dir> <write_dir> [--json out.json] [--meta WORKLOAD DIGEST]"""
 import collections
 import csv
 import glob
@@ -50,8 +50,11 @@ def main():
         print(f"{name:70s} {n:8d} {fb / 1e6:14.3f} {wb / 1e6:15.3f}")
     if "--json" in sys.argv:
         out = sys.argv[sys.argv.index("--json") + 1]
-        json.dump({r[0]: {"launches": r[1], "read_bytes_per_launch": r[2], "write_bytes_per_launch": r[3]}
-                   for r in rows}, open(out, "w"), indent=1)
+        table = {r[0]: {"launches": r[1], "read_bytes_per_launch": r[2], "write_bytes_per_launch": r[3]} for r in rows}
+        if "--meta" in sys.argv:
+            i = sys.argv.index("--meta")
+            table["_meta"] = {"workload": sys.argv[i + 1], "source_digest": sys.argv[i + 2]}
+        json.dump(table, open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -8,8 +8,12 @@ MI355X_MICROARCH.md's HBM section; both counters in KiB).
 --tail-frac F keeps only the last fraction F of the kernel's dispatches in each file (the isolated-plan passes of
 scripts/gpu_pmc_isolated.sh: 3 step executions while the plan is recorded, then every launch re-issued alone once -> 0.25).
 
+--launches all: every launch of the kernel (split-K ones included: the bench times those with their reducer when the
+kernel's unsplit launches carry less than half its work, roofline.launch_set).
+--meta WORKLOAD DIGEST: recorded as _meta (bench.py matches DIGEST against the running tree's sdmi._build.source_digest).
+
 Usage: python scripts/roofline_evidence.py <kernel_trace.csv|dir> <fetch_dir> <write_dir> "<kernel>" [--json out]
-       [--tail-frac F]"""
+       [--tail-frac F] [--launches unsplit|all] [--meta WORKLOAD DIGEST]"""
 import csv
 import glob
 import json
@@ -40,13 +44,15 @@ def _tail(rows, frac):
 def main():
     trace, fdir, wdir, kernel = sys.argv[1:5]
     frac = float(sys.argv[sys.argv.index("--tail-frac") + 1]) if "--tail-frac" in sys.argv else 1.0
+    launches = sys.argv[sys.argv.index("--launches") + 1] if "--launches" in sys.argv else "unsplit"
+    keep = (lambda z: z == 1) if launches == "unsplit" else (lambda z: z is not None)
     durs = []
     rows = sorted((r for r in csv.DictReader(open(_trace_csv(trace))) if _match(kernel, r["Kernel_Name"])),
                   key=lambda r: int(r["Dispatch_Id"]))
     for r in _tail(rows, frac):
-        if int(r["Grid_Size_Z"]) == 1:
+        if keep(int(r["Grid_Size_Z"])):
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    out = {"kernel": kernel, "trace_unsplit_launches": len(durs),
+    out = {"kernel": kernel, "launches": launches, "trace_launches": len(durs),
            "trace_avg_us": sum(durs) / len(durs) if durs else None}
     for d, cname, mul in ((fdir, "FETCH_SIZE", 2.0), (wdir, "WRITE_SIZE", 1.0)):
         vals = []
@@ -56,12 +62,15 @@ def main():
                            if r["Counter_Name"] == cname and _match(kernel, r["Kernel_Name"])),
                           key=lambda r: int(r["Dispatch_Id"]))
             for r in _tail(rows, frac):
-                if gz.get(r["Dispatch_Id"]) == 1:
+                if keep(gz.get(r["Dispatch_Id"])):
                     vals.append(float(r["Counter_Value"]) * 1024 * mul)
         out[cname.lower() + "_bytes_per_launch"] = sum(vals) / len(vals) if vals else None
         out[cname.lower() + "_launches"] = len(vals)
     if out["fetch_size_bytes_per_launch"] is not None and out["write_size_bytes_per_launch"] is not None:
         out["traffic_bytes_per_launch"] = out["fetch_size_bytes_per_launch"] + out["write_size_bytes_per_launch"]
+    if "--meta" in sys.argv:
+        i = sys.argv.index("--meta")
+        out["_meta"] = {"workload": sys.argv[i + 1], "source_digest": sys.argv[i + 2]}
     print(json.dumps(out, indent=1))
     if "--json" in sys.argv:
         json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)

@@ -224,14 +224,21 @@ __global__ void cast_bf16_kernel(const float* p, bf16_t* pb, long long n) {
 
 extern "C" size_t sdmi_optim_workspace(void) { return NORM_BLOCKS * sizeof(float); }
 
+// workspace of sdmi_clip_unscale_ws over n gradients: one partial per NORM_BLK block (at least the fixed size above)
+extern "C" size_t sdmi_optim_workspace_for(long long n) {
+  const long long nb = n > 0 ? (n + NORM_BLK - 1) / NORM_BLK : 0;
+  return (size_t)(nb > NORM_BLOCKS ? nb : NORM_BLOCKS) * sizeof(float);
+}
+
 extern "C" long long sdmi_norm_block(void) { return NORM_BLK; }
 
 // state: device float[8], initialise to {0, 0, init_scale, 0, 0, 0, 0, 0}
-extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws,
-                                 int growth_interval, int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream) {
+extern "C" int sdmi_clip_unscale_ws(const float* grads, long long n, float max_norm, float* state, float* ws,
+                                    size_t ws_bytes, int growth_interval, int skip_if_loss_nonfinite, float grad_div,
+                                    sdmi_stream_t stream) {
   if (!grads || !state || !ws || n <= 0 || ((uintptr_t)grads & 15)) return -1;
   const long long nb = (n + NORM_BLK - 1) / NORM_BLK;
-  if (nb > NORM_BLOCKS) return -3;  // > 268 M parameters: sdmi_sumsq_blocks into a larger partial array instead
+  if ((size_t)nb * sizeof(float) > ws_bytes) return -3;  // workspace smaller than sdmi_optim_workspace_for(n)
   hipStream_t s = (hipStream_t)stream;
   sdmi_rt::launch(sumsq_block_kernel, dim3((unsigned)nb), dim3(NTN), 0, s, grads, n, ws);
   SDMI_CHECK_LAUNCH();
@@ -239,6 +246,13 @@ extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm
                      skip_if_loss_nonfinite, grad_div);
   SDMI_CHECK_LAUNCH();
   return 0;
+}
+
+// the fixed-workspace form (ws of sdmi_optim_workspace() bytes: up to NORM_BLOCKS * NORM_BLK ~ 268 M gradients)
+extern "C" int sdmi_clip_unscale(const float* grads, long long n, float max_norm, float* state, float* ws,
+                                 int growth_interval, int skip_if_loss_nonfinite, float grad_div, sdmi_stream_t stream) {
+  return sdmi_clip_unscale_ws(grads, n, max_norm, state, ws, sdmi_optim_workspace(), growth_interval,
+                              skip_if_loss_nonfinite, grad_div, stream);
 }
 
 extern "C" int sdmi_sumsq_blocks(const float* grads, long long n, float* partial, sdmi_stream_t stream) {

@@ -87,6 +87,20 @@ def build(force=False, verbose=False):
     return LIB
 
 
+def source_digest():
+    """16-hex-digit sha256 over the library's sources (csrc/*.hip, csrc/*.h, include/sdmi.h, by name): the tree a
+    committed profile (profiles/rNN_<workload>_pmc_traffic.json / _roofline_evidence.json) was measured on. bench.py
+    compares it with the running tree's, so a stale PMC file is reported as such instead of silently reused."""
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+    for f in files:
+        h.update(f.encode())
+        h.update(open(os.path.join(CSRC, f), "rb").read())
+    h.update(open(os.path.join(REPO, "include", "sdmi.h"), "rb").read())
+    return h.hexdigest()[:16]
+
+
 CABI_SRC = os.path.join(REPO, "tests", "cabi", "cabi_check.c")
 CABI_BIN = os.path.join(REPO, "tests", "cabi", "cabi_check")
 
@@ -106,4 +120,7 @@ def build_cabi_check():
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if "--digest" in sys.argv:
+        print(source_digest())
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

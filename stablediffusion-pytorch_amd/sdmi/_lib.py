@@ -122,6 +122,8 @@ SIGNATURES = {
     "sdmi_pack_transpose": ([_P, _P, _I, _P], _I),
     "sdmi_optim_workspace": ([], _SZ),
     "sdmi_clip_unscale": ([_P, _L, _F, _P, _P, _I, _I, _F, _P], _I),
+    "sdmi_optim_workspace_for": ([_L], _SZ),
+    "sdmi_clip_unscale_ws": ([_P, _L, _F, _P, _P, _SZ, _I, _I, _F, _P], _I),
     "sdmi_loss_flag": ([_P, _P, _I, _P], _I),
     "sdmi_clip_finalize": ([_P, _I, _F, _P, _I, _I, _F, _P], _I),
     "sdmi_norm_block": ([], _L),

@@ -399,8 +399,21 @@ class DiTEngine:
     # layers from the last layer down: the group issued after the final layer's backward is the tail the step waits
     # for, so it is kept short. Measured DiT-12L step, same box, uniform groups of 1 / 3 / 6 layers: 4.44 / 4.11 / 4.04
     # ms (round 3); 6+6 3.66 / 3.66, 6+4+2 3.58 / 3.57, 7+3+2 3.56 / 3.55, 5+4+2+1 3.62, 6+4+1+1 3.63 ms (round 4)
-    _dit_groups = (7, 3, 2)
+    # Any depth: a short 3 + 2 tail and groups of at most 7 layers before it, evened out (12 layers: 7, 3, 2; 28 layers:
+    # 6, 6, 6, 5, 3, 2), so a deeper DiT keeps issuing weight gradients (and DP buckets / norm pieces) as it goes.
     _pending_wg = {}
+
+    @staticmethod
+    def dit_groups(n_layers):
+        if n_layers <= 5:
+            return (n_layers,)
+        head = n_layers - 5
+        k = -(-head // 7)
+        return tuple(head // k + (1 if i < head % k else 0) for i in range(k)) + (3, 2)
+
+    @property
+    def _dit_groups(self):
+        return self.dit_groups(self.L["n_layers"])
 
     def _flush_after(self, n_done):
         """True when the grouped weight gradients are issued after the backward of n_done layers."""

@@ -261,7 +261,6 @@ class DDPMTrainer:
                 eng.backward(ctx, dpred, on_progress=self._on_progress)
         else:
             eng.backward(ctx, dpred)
-        ws = torch.empty(L.sdmi_optim_workspace() // 4, dtype=torch.float32, device=self.device)
         hp = self.hp
         # Non-finite loss: the reference skips before scaler.update() (:348-352), leaving the scale alone. N > 1: the
         # all-reduced sum of every rank's flag decides, so all replicas skip together (and keep their scale) when any
@@ -276,9 +275,11 @@ class DDPMTrainer:
             finalize_norm(self.red_norm, hp["clip"], self.state, hp["growth"], 1 if self.world == 1 else 2,
                           float(self.world))
         else:
-            _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(),
-                                           ws.data_ptr(), hp["growth"], 1 if self.world == 1 else 2, float(self.world),
-                                           K._stream()), "sdmi_clip_unscale")
+            wsb = L.sdmi_optim_workspace_for(st.numel)  # one partial per norm block, any model size
+            ws = torch.empty(wsb // 4, dtype=torch.float32, device=self.device)
+            _lib.check(L.sdmi_clip_unscale_ws(st.grads.data_ptr(), st.numel, hp["clip"], self.state.data_ptr(),
+                                              ws.data_ptr(), wsb, hp["growth"], 1 if self.world == 1 else 2,
+                                              float(self.world), K._stream()), "sdmi_clip_unscale_ws")
         ema_decay = hp["ema"] if hp["ema"] is not None else 0.0
         if self.opt_ranges is None:
             _lib.check(L.sdmi_adam_ema_bf16(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(),
@@ -355,9 +356,12 @@ class DDPMTrainer:
         return v if v.is_contiguous() else v.contiguous()
 
     def state_dict(self):
-        """Model state dict (views of the flat fp32 master weights), safe to read or save on the current stream:
-        it first waits for the chunked optimizer step still in flight on the side stream. Never read
-        store.params / store.p directly after step() without sync_optimizer()."""
+        """Model state dict: READ-ONLY snapshots of the flat fp32 master weights, safe to read or save on the current
+        stream (it first waits for the chunked optimizer step still in flight on the side stream). Entries are views
+        of the master buffer for torch-order weights but contiguous COPIES for the GEMM-natural (co, kh, kw, ci) conv
+        weights, so writing into them does not update the model consistently: load weights through the module's
+        load_state_dict / sdmi_invalidate path, or a new DDPMTrainer. Never read store.params / store.p directly after
+        step() without sync_optimizer()."""
         self.sync_optimizer()
         return {k: self._export(self.store.p[k]) for k in self.store.order}
 

@@ -375,11 +375,13 @@ class VQVAETrainer:
             self.reducer.finish()
         self.vq_loss, self.indices, self.out = ctx["vq_loss"], ctx["indices"], out
         L = _lib.lib()
-        ws = torch.empty(L.sdmi_optim_workspace() // 4, dtype=torch.float32, device=self.device)
+        wsb = L.sdmi_optim_workspace_for(st.numel)
+        ws = torch.empty(wsb // 4, dtype=torch.float32, device=self.device)
         # no loss scaler (growth_interval 0: the scale stays 1) and no clipping (max norm inf): the gradient
         # coefficient is exactly 1 / world. A non-finite gradient skips the update instead of poisoning the weights.
-        _lib.check(L.sdmi_clip_unscale(st.grads.data_ptr(), st.numel, float("inf"), self.state.data_ptr(),
-                                       ws.data_ptr(), 0, 0, float(self.world), K._stream()), "sdmi_clip_unscale")
+        _lib.check(L.sdmi_clip_unscale_ws(st.grads.data_ptr(), st.numel, float("inf"), self.state.data_ptr(),
+                                          ws.data_ptr(), wsb, 0, 0, float(self.world), K._stream()),
+                   "sdmi_clip_unscale_ws")
         _lib.check(L.sdmi_adam_ema(st.params.data_ptr(), st.grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
                                    None, st.numel, self.state.data_ptr(), hp["lr"], hp["b1"], hp["b2"], hp["eps"], 0.0,
                                    1.0, K._stream()), "sdmi_adam_ema")
