@@ -48,19 +48,36 @@ PEAK_BF16 = 2.5e15             # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
 
 
-# GEMM mode tag -> kernel symbol (gemm.hip launch_t: DMA mainloop for row-major / conv A, register staging for col-major A)
+# GEMM mode tag -> kernel symbol (gemm.hip): the launch's mainloop variant (as the library reports it after its own
+# downgrades, sdmi_gemm_kernel_info) -> the template arguments of its instantiation
+#   gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK, GNE, KG>  (RED / GNE: '*', one name for all of them)
+DMA_VARIANTS = {2: (2, None, 128, 2, 64, 1), 3: (3, 128, 128, 2, 64, 1), 4: (4, None, 128, 4, 32, 1),
+                5: (3, None, 128, 2, 32, 1), 6: (4, 128, 128, 2, 64, 1), 7: (6, 64, 64, 4, 64, 1),
+                8: (6, 128, 64, 4, 64, 1), 9: (3, 128, 64, 4, 64, 1), 10: (2, 128, 64, 4, 64, 1),
+                11: (2, 128, 128, 2, 64, 2)}
+
+
 def kernel_name(tag, info):
-    """Kernel instantiation of a profiled sdmi_gemm launch (as rocprofv3 names it), from its mode tag
-    (gemm_a<A>b<B>) and the variant / tile_n the library reported (sdmi_gemm_kernel_info)."""
+    """Kernel instantiation of a profiled sdmi_gemm launch as a glob over rocprofv3's demangled names, from its mode
+    tag (gemm_a<A>b<B>) and the variant / tile_n the library reported."""
     a, b = re.match(r"gemm_a(\d)b(\d)", tag).groups()
     v = int(re.search(r"variant=(\d+)", info).group(1))
     tn = int(re.search(r"tile_n=(\d+)", info).group(1))
     if v == 0:
-        return f"gemm_kernel<{a}, {b}>"
-    stages = {2: 2, 3: 3, 4: 4, 5: 3, 6: 4, 7: 6, 8: 6, 9: 3, 10: 2}[v]  # gemm.hip launch_dma_red: variant -> ring depth
-    if v >= 7:  # 64-row tiles
-        return f"gemm_dma_kernel<{a}, {b}, {stages}, {tn}, 64>"
-    return f"gemm_dma_kernel<{a}, {b}, {stages}, {tn}>"
+        return f"gemm_kernel<{a}, {b}, *>"
+    st, tbn, tbm, nwn, kbk, kg = DMA_VARIANTS[v]
+    return f"gemm_dma_kernel<{a}, {b}, {st}, {tbn or tn}, {tbm}, {nwn}, *, {kbk}, *, {kg}>"
+
+
+def kernel_matches(pattern, name):
+    """rocprofv3 kernel name (demangled, possibly with 'void (anonymous namespace)::' and an argument list) vs a
+    kernel_name() glob"""
+    import fnmatch
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "").strip()
+    n = n[:n.index(">(") + 1] if ">(" in n else n
+    return fnmatch.fnmatchcase(n, pattern)
+
+
 def _evidence_files(workload, kind):
     """Committed rocprofv3 evidence of `workload` (kind 'pmc_traffic' or 'roofline_evidence'), newest round first:
     profiles/rNN_<workload>_<kind>.json, written by scripts/gpu_profile.sh from the tree whose source digest
@@ -104,9 +121,8 @@ def pmc_traffic(workload, kernel, unsplit):
                     "timed here)", "trace_avg_us": ev.get("trace_avg_us")}
     table, t_file, t_ok = _load_evidence(workload, "pmc_traffic", digest)
     if table:
-        # bench-style "gemm_dma_kernel<1, 0, 2, 128>" also names the full instantiations "...<1, 0, 2, 128, 128, ...>":
-        # their launch-weighted average
-        keys = [k for k in table if k == kernel or k.startswith(kernel[:-1] + ",")]
+        # the kernel_name() glob covers several instantiations (RED / GNE): their launch-weighted average
+        keys = [k for k in table if k != "_meta" and kernel_matches(kernel, k)]
         n = sum(table[k]["launches"] for k in keys)
         if n:
             b = sum((table[k]["read_bytes_per_launch"] + table[k]["write_bytes_per_launch"]) * table[k]["launches"]

@@ -85,7 +85,7 @@ def main():
           f"(GEMM calls matched {gi}/{len(log)})")
     fam = {}
     for o in ops:
-        f = fam.setdefault(o["name"][:40], [0.0, 0])
+        f = fam.setdefault(o["name"][:62], [0.0, 0])
         f[0] += o["us"]
         f[1] += 1
     print("--- by kernel (isolated) ---")

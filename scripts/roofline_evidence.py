@@ -33,8 +33,10 @@ def _grid_z(d):
 
 
 def _match(kernel, name):
-    """bench-style name gemm_dma_kernel<1, 0, 2, 128> also matches the full instantiation <1, 0, 2, 128, 128, ...>"""
-    return kernel in name or (kernel.endswith(">") and kernel[:-1] + "," in name)
+    """bench.py's kernel_name() glob (e.g. gemm_dma_kernel<2, 2, 2, 128, 128, 2, *, 64, *, 1>) vs a demangled name"""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_matches
+    return kernel_matches(kernel, name)
 
 
 def _tail(rows, frac):

@@ -10,7 +10,7 @@ import re
 def short(name):
     name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)
-    return name.replace("void ", "")[:48]
+    return name.replace("void ", "")[:62]
 
 
 def main():
@@ -79,7 +79,7 @@ def main():
         print(f"{t / 1e3:9.1f} us {c:5d}x  avg {t / c / 1e3:7.1f} us  {n}")
     print("--- by kernel + grid (blocks x, y, z) ---")
     for (n, grid), (c, t) in sorted(groups.items(), key=lambda kv: -kv[1][1])[:args.top]:
-        print(f"{t / 1e3:9.1f} us {c:4d}x  avg {t / c / 1e3:7.1f} us  {n:40s} grid {grid}")
+        print(f"{t / 1e3:9.1f} us {c:4d}x  avg {t / c / 1e3:7.1f} us  {n:62s} grid {grid}")
 
 
 if __name__ == "__main__":

@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--against-table", action="store_true",
                     help="baseline = the starting table's entry (not the heuristic): try only SDMI_TUNE_VARIANTS and "
                          "replace the entry where one beats it by > 3 %")
+    ap.add_argument("--only-colmajor", action="store_true",
+                    help="tune only the weight-gradient (col-major A) launches, e.g. for a new weight-gradient mainloop")
     ap.add_argument("--out", default=os.path.join(REPO, "stablediffusion-pytorch_amd", "sdmi", "tuned_gemm.json"))
     args = ap.parse_args()
     from sdmi import _lib, kernels as K
@@ -119,6 +121,8 @@ def main():
             continue
         if args.only_new and key in table:
             continue
+        if args.only_colmajor and d.a_mode != _lib.A_COLMAJOR:
+            continue
         d.splits_hint = 0
         d.variant_hint = 0
         cur = table.get(key) if args.against_table else None
@@ -129,7 +133,8 @@ def main():
         # mainloops: register staging (1) and the LDS-DMA rings (2, 3, 6: 2 / 3 / 4 stages of 64-deep K; 7, 8: 64-row
         # tiles with 6 stages; 4: 8-wave
         # 128 x {256, 384} tiles; 5: 3 stages of 32-deep K); the library downgrades a request the mode cannot take
-        variants = tuple(int(v) for v in os.environ.get("SDMI_TUNE_VARIANTS", "1,2,3,4,5,6,7,8,9,10").split(","))
+        # 11: two k-groups of 4 waves per 128 x 128 weight-gradient tile (fewer split-K slabs)
+        variants = tuple(int(v) for v in os.environ.get("SDMI_TUNE_VARIANTS", "1,2,3,4,5,6,7,8,9,10,11").split(","))
         for v in variants:
             for s in SPLITS:
                 if s > nkt or s * d.m * d.n * 4 >= min(ws.numel() * 4, 1 << 31):

@@ -42,7 +42,21 @@ struct AttnArgs {
   float scale;  // 1/sqrt(d)
   float* dq_part;     // fused backward: per-key-block fp32 dQ partials [nkb][B*H][N][d] (nkb > 1)
   unsigned* ctr;      // fused backward: per-(b*h, query tile) arrival counters (zero between launches)
+  int nblk;           // row blocks per (b, h) of the launch (the grid is 1-D: nblk * B * H workgroups)
 };
+
+// XCD-local block order. Workgroups are dealt round-robin over the 8 XCDs (dispatch id d runs on XCD d % 8, each XCD
+// has its own 4 MiB L2). A (blocks, B*H) grid put the 8 query (key) blocks of one head on 8 different XCDs, so every
+// XCD's L2 fetched that head's whole K / V (Q / dO) from HBM: 4.8x the algorithmic reads in the 32^2 backward
+// (profiles/pmc_r04j_summary.txt). The 1-D grid is re-numbered so every XCD owns a CONTIGUOUS band of logical ids
+// (bijective for any grid size), logical id = bh * nblk + block: the blocks of one head share one L2.
+__device__ __forceinline__ void xcd_block(int nblk, int& blk, int& bh) {
+  const int total = gridDim.x, d = blockIdx.x;
+  const int xcd = d & 7, q = total >> 3, r = total & 7;
+  const int l = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (d >> 3);
+  bh = l / nblk;
+  blk = l - bh * nblk;
+}
 
 template <int DP> struct Tile {
   static constexpr int LD = DP;  // unpadded rows; the 16-B chunks are XOR-swizzled per row (toff)
@@ -195,7 +209,9 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  int blk, bh;
+  xcd_block(a.nblk, blk, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
   const float c = a.scale * LOG2E;
   const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
   const bf16_t* K = a.k + (long long)b * a.S * a.ldk;
@@ -207,7 +223,7 @@ __global__ __launch_bounds__(NT, 2) void attn_fwd_kernel(AttnArgs a) {
   f32x4 o[2][DT];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    myq[g] = blockIdx.x * ROWS + wave * 32 + g * 16 + (lane & 15);
+    myq[g] = blk * ROWS + wave * 32 + g * 16 + (lane & 15);
     row_frags<DP>(qf[g], Q, a.ldq, myq[g], a.N, h * a.d, a.d, lane);
     m[g] = -INFINITY;
     l[g] = 0.f;
@@ -339,7 +355,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][Q|dO]
   __shared__ __attribute__((aligned(16))) float sLD[2][2][64];               // [buf][-lse|-delta]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  int blk, bh;
+  xcd_block(a.nblk, blk, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
   const float c = a.scale * LOG2E;
   const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
   const bf16_t* dO = a.dout + (long long)b * a.N * a.lddo;
@@ -349,7 +367,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   f32x4 dk[G][DT], dv[G][DT];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    mykey[g] = blockIdx.x * (64 * G) + wave * 16 * G + g * 16 + (lane & 15);
+    mykey[g] = blk * (64 * G) + wave * 16 * G + g * 16 + (lane & 15);
     row_frags<DP>(kf[g], a.k + (long long)b * a.S * a.ldk, a.ldk, mykey[g], a.S, h * a.d, a.d, lane);
     row_frags<DP>(vf[g], a.v + (long long)b * a.S * a.ldv, a.ldv, mykey[g], a.S, h * a.d, a.d, lane);
 #pragma unroll
@@ -455,7 +473,9 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int DP = Dim<DT>::DP, KS = Dim<DT>::KS;
   __shared__ __attribute__((aligned(16))) bf16_t smem[4 * Tile<DP>::ELEMS];  // [buf][K|V]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
+  int blk, bh;
+  xcd_block(a.nblk, blk, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
   const float c = a.scale * LOG2E;
   const bf16_t* K = a.k + (long long)b * a.S * a.ldk;
   const bf16_t* V = a.v + (long long)b * a.S * a.ldv;
@@ -466,7 +486,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
   f32x4 dq[G][DT];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    myq[g] = blockIdx.x * (64 * G) + wave * 16 * G + g * 16 + (lane & 15);
+    myq[g] = blk * (64 * G) + wave * 16 * G + g * 16 + (lane & 15);
     row_frags<DP>(qf[g], a.q + (long long)b * a.N * a.ldq, a.ldq, myq[g], a.N, h * a.d, a.d, lane);
     row_frags<DP>(of[g], a.dout + (long long)b * a.N * a.lddo, a.lddo, myq[g], a.N, h * a.d, a.d, lane);
     const bool ok = myq[g] < a.N;
@@ -585,7 +605,7 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 // (dS^T [key][query], bf16, the same values the dK product consumes) into LDS, and after one barrier wave w forms
 // dQ^T for queries 16w .. 16w+15 of the tile over all 128 keys of the workgroup from transposed reads of dS^T and
 // of the workgroup's key block (staged once). One key block (S <= 128: cross-attention over the 77 text tokens)
-// stores dQ directly; otherwise every key block writes an fp32 partial and the LAST of the gridDim.x key blocks to
+// stores dQ directly; otherwise every key block writes an fp32 partial and the LAST of the nblk key blocks to
 // finish a (b*h, query tile) -- device-scope arrival counter, no spinning -- sums the partials in key-block order
 // (deterministic) and stores dQ. Partials are written and read with sc1 (device-coherent) buffer operations: the
 // summing workgroup may run on another XCD. delta = rowsum(dO * O) comes from attn_delta_kernel.
@@ -618,8 +638,10 @@ __global__ __launch_bounds__(NT, 2) void attn_bwd_fused_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) float sLD[2][2][64];               // [buf][-lse|-delta]
   __shared__ int sflag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh - b * a.H;
-  const int kb = blockIdx.x, nkb = gridDim.x;
+  int kb, bh;
+  xcd_block(a.nblk, kb, bh);
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int nkb = a.nblk;
   const float c = a.scale * LOG2E;
   const bf16_t* Q = a.q + (long long)b * a.N * a.ldq;
   const bf16_t* dO = a.dout + (long long)b * a.N * a.lddo;
@@ -838,7 +860,8 @@ extern "C" int sdmi_attn_fwd(const void* q, int ldq, const void* k, int ldk, con
   a.B = B; a.H = H; a.N = N; a.S = S; a.d = d; a.scale = 1.0f / sqrtf((float)d);
   int rc = check_args(a);
   if (rc) return rc;
-  dim3 grid((N + ROWS - 1) / ROWS, B * H);
+  a.nblk = (N + ROWS - 1) / ROWS;
+  dim3 grid(a.nblk * B * H);
   hipStream_t s = (hipStream_t)stream;
   // ONES: the softmax row sum through the PV MFMA where the padded head dim leaves a free column (d % 16 == 8)
   const bool ones = d % 16 == 8;
@@ -878,19 +901,22 @@ extern "C" int sdmi_attn_bwd(const void* q, int ldq, const void* k, int ldk, con
   const long long wg4 = (long long)B * H * ((std::min(N, S) + 255) / 256);
   const int g4 = d <= 32 && N <= 256 && S <= 256 && wg4 >= 512;
   const int rows = g4 ? 256 : ROWS;
-  dim3 gk((S + rows - 1) / rows, B * H), gq((N + rows - 1) / rows, B * H);
+  AttnArgs aq = a, ak = a;
+  aq.nblk = (N + rows - 1) / rows;
+  ak.nblk = (S + rows - 1) / rows;
+  dim3 gk(ak.nblk * B * H), gq(aq.nblk * B * H);
   switch ((d + 15) / 16) {
 #define SDMI_ATTN_BWD(DT)                                                               \
   case DT:                                                                              \
     if constexpr (DT <= 2) {                                                            \
       if (g4) {                                                                         \
-        sdmi_rt::launch(attn_bwd_dq_kernel<DT, 4>, gq, dim3(NT), 0, s, a);              \
-        sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 4>, gk, dim3(NT), 0, s, a);             \
+        sdmi_rt::launch(attn_bwd_dq_kernel<DT, 4>, gq, dim3(NT), 0, s, aq);             \
+        sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 4>, gk, dim3(NT), 0, s, ak);            \
         break;                                                                          \
       }                                                                                 \
     }                                                                                   \
-    sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2>, gq, dim3(NT), 0, s, a);                  \
-    sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2>, gk, dim3(NT), 0, s, a);                 \
+    sdmi_rt::launch(attn_bwd_dq_kernel<DT, 2>, gq, dim3(NT), 0, s, aq);                 \
+    sdmi_rt::launch(attn_bwd_dkv_kernel<DT, 2>, gk, dim3(NT), 0, s, ak);                \
     break;
     SDMI_ATTN_BWD(1)
     SDMI_ATTN_BWD(2)
@@ -939,7 +965,8 @@ extern "C" int sdmi_attn_bwd_fused(const void* q, int ldq, const void* k, int ld
   hipStream_t s = (hipStream_t)stream;
   const long long rows = (long long)B * N * H;
   sdmi_rt::launch(attn_delta_kernel, dim3((unsigned)((rows + NT - 1) / NT)), dim3(NT), 0, s, a);
-  dim3 gk((S + ROWS - 1) / ROWS, B * H);
+  a.nblk = (S + ROWS - 1) / ROWS;
+  dim3 gk(a.nblk * B * H);
   switch ((d + 15) / 16) {
     case 1: sdmi_rt::launch(attn_bwd_fused_kernel<1>, gk, dim3(NT), 0, s, a); break;
     case 2: sdmi_rt::launch(attn_bwd_fused_kernel<2>, gk, dim3(NT), 0, s, a); break;

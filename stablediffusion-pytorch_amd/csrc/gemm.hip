@@ -848,13 +848,22 @@ __device__ __forceinline__ s16x8 reduce_frag(const Args& g, int r, int kb, int l
 
 // KBK: k depth of one staged tile (64, or 32 for deeper rings in the same LDS: more bytes in flight per CU). Split-K
 // slices stay in units of 64 (host k-tiles).
+// KG (col-major A, the weight gradients): k-groups per workgroup. KG wave groups, each with its own LDS ring, compute
+// the same output tile over interleaved k-tiles of the split's range (group g: tiles g, g + KG, ...); their fp32
+// accumulators are summed through LDS in group order (deterministic) before the epilogue. A tile's k range then
+// needs KG x fewer split-K slices for the same number of waves on the chip: fewer fp32 slabs written, read and reduced.
+template <int TBM, int NWN, int KG>
+constexpr int dma_min_waves(int ring_bytes) {
+  return KG > 1 ? 2 : ((dma_threads<TBM, NWN>() == 256 && ring_bytes <= 80 * 1024) ? 2 : 1);
+}
+
 template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0, int KBK = BK,
-          bool GNE = false>
-__global__ __launch_bounds__((dma_threads<TBM, NWN>()),
-                             ((dma_threads<TBM, NWN>() == 256 && STAGES * (TBM + TBN) * KBK * 2 <= 80 * 1024) ? 2 : 1))
+          bool GNE = false, int KG = 1>
+__global__ __launch_bounds__((dma_threads<TBM, NWN>() * KG),
+                             (dma_min_waves<TBM, NWN, KG>(STAGES * (TBM + TBN) * KBK * 2)))
 void gemm_dma_kernel(const Args g, const EpiArgs e) {
-  constexpr int NTH = dma_threads<TBM, NWN>();
-  constexpr int NW = NTH / 64;
+  constexpr int NTH = dma_threads<TBM, NWN>() * KG;  // all threads; the DMA pieces are shared out per k-group
+  constexpr int NW = NTH / 64 / KG;                    // waves per k-group
   constexpr int WTN = TBN / NWN;                     // columns per wave
   constexpr int NJ = WTN / 16;                       // 16-column MFMA tiles per wave
   constexpr bool A_MN = AM == SDMI_A_COLMAJOR, B_MN = BMODE != SDMI_B_NK;
@@ -871,11 +880,15 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   static_assert(!B_MN || TBN % 128 == 0, "MN-contiguous B: 128-column sub-tiles");
   static_assert(WTN % 16 == 0 && TBM % 64 == 0, "wave tile");
   static_assert(RED == 0 || A_MN, "reductions: col-major A only");
+  // the implicit-conv A keeps incremental tap state over consecutive k-tiles: k-groups only on col-major A
+  static_assert(KG == 1 || (A_MN && !GNE), "k-groups: weight-gradient (col-major A) launches only");
   constexpr int RPW = RED == 0 ? 0 : (RED == 1 ? 1 : (3 + NWN - 1) / NWN);  // reduction tiles per wave (<= 3 total)
   extern __shared__ __attribute__((aligned(16))) char smem[];  // STAGES x (A | B)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform: scalar LDS bases / M0
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform: scalar LDS bases / M0
+  const int kg = wave_all / NW, wave = wave_all - kg * NW;            // k-group, wave within it
+  char* const ring = smem + kg * STAGES * (TBM + TBN) * KBK * 2;       // this k-group's LDS ring
   const int wm = (wave / NWN) * 64, wn = (wave % NWN) * WTN;
   const TileId tl = tile_id<TBN, TBM>();
   const int m0 = tl.m0, n0 = tl.n0;
@@ -1069,7 +1082,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   };
 
   auto issue = [&](int kt, int stage) __attribute__((always_inline)) {
-    char* sa = smem + stage * STAGE_BYTES;
+    char* sa = ring + stage * STAGE_BYTES;
     char* sb = sa + A_BYTES;
     const int k0 = kt * KBK;
     if (k0 + KBK <= g.K && (AM != SDMI_A_CONV || (cin64 && k0 + KBK <= g.k_split))) {
@@ -1120,13 +1133,16 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) accr[rr][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nt = kt1 - kt0;
-  if (nt > 0) {
+  // this k-group's tiles of the split: local tile t is k-tile kt0 + t * KG + kg (KG == 1: all of them, in order)
+  const int nt_all = kt1 - kt0;
+  const int nt = nt_all > kg ? (nt_all - kg + KG - 1) / KG : 0;
+  const int nt_loop = (nt_all + KG - 1) / KG;  // barrier count: every k-group runs the first group's trip count
+  if (nt_loop > 0) {
     // prologue: STAGES-1 tiles in flight
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
-      if (s < nt) issue(kt0 + s, s);
-    for (int t = 0; t < nt; ++t) {
+      if (s < nt) issue(kt0 + s * KG + kg, s);
+    for (int t = 0; t < nt_loop; ++t) {
       // tile t landed for this thread: at most (tiles issued after t) x (A_PW + B_PW) DMA instructions outstanding
       // (in the last STAGES-2 tiles fewer are in flight: wait for all)
       if (STAGES > 2 && t + STAGES - 2 < nt)
@@ -1134,8 +1150,9 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMA for tile t done; every wave done with tile t-1
-      if (t + STAGES - 1 < nt) issue(kt0 + t + STAGES - 1, (t + STAGES - 1) % STAGES);
-      const char* ta = smem + (t % STAGES) * STAGE_BYTES;
+      if (KG > 1 && t >= nt) continue;  // this k-group has no tile t (its last barriers only)
+      if (t + STAGES - 1 < nt) issue(kt0 + (t + STAGES - 1) * KG + kg, (t + STAGES - 1) % STAGES);
+      const char* ta = ring + (t % STAGES) * STAGE_BYTES;
       const char* tb = ta + A_BYTES;
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1159,7 +1176,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
           for (int j = 0; j < NJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         if (RED != 0 && red_tile) {
-          const int kb = (kt0 + t) * KBK + ks * 32 + (lane >> 4) * 8;
+          const int kb = (kt0 + t * KG + kg) * KBK + ks * 32 + (lane >> 4) * 8;
 #pragma unroll
           for (int rr = 0; rr < RPW; ++rr) {
             const int r = wave % NWN + rr * NWN;
@@ -1176,6 +1193,42 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
     }
   }
   __syncthreads();
+  if constexpr (KG > 1) {
+    // k-group g > 0 hands its accumulators (and reduction-tile sums) to k-group 0 through LDS, one group after the
+    // other in group order: a fixed summation order, so the result does not depend on timing. Lane-linear 16-B slots
+    // (conflict-free ds_write_b128 / ds_read_b128); NE4 float4 per lane, one [NE4][64] block per wave.
+    constexpr int NE4 = 4 * NJ + (RPW > 0 ? RPW : 1) * 4;
+    float4* xs = (float4*)smem + (long long)wave * NE4 * 64 + lane;
+#pragma unroll 1
+    for (int src = 1; src < KG; ++src) {
+      if (kg == src) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) xs[(i * NJ + j) * 64] = __builtin_bit_cast(float4, acc[i][j]);
+        if constexpr (RED != 0) {
+#pragma unroll
+          for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) xs[(4 * NJ + rr * 4 + i) * 64] = __builtin_bit_cast(float4, accr[rr][i]);
+        }
+      }
+      __syncthreads();
+      if (kg == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] += __builtin_bit_cast(f32x4, xs[(i * NJ + j) * 64]);
+        if constexpr (RED != 0) {
+#pragma unroll
+          for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) accr[rr][i] += __builtin_bit_cast(f32x4, xs[(4 * NJ + rr * 4 + i) * 64]);
+        }
+      }
+      __syncthreads();
+    }
+  }
   EpiArgs ev = epi_args_late();  // epilogue arguments loaded only from here on (see gemm_kernel)
   if (grp) group_epi(ev, g.Cg[grp], g.sum_g[grp], grp);
   // The column tiles of this kernel cover only the n GEMM columns; the reduction columns [n_x0, n_gemm) of a split-K
@@ -1183,7 +1236,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   // accumulators there: it raced with the reduction tile's stores of the same slab entries (round-4 gsum probe).
   if (RED == 2) ev.n_gemm = ev.n_x0;
   const EpiArgs* ep = &ev;
-  if (RED != 0 && red_tile) {
+  if (RED != 0 && red_tile && kg == 0) {
     // lane holds C[wm + 16i + 4(lane>>4) + q][r*16 + (lane & 15)]: column 0 = row sums, 8 + j = group j
 #pragma unroll
     for (int rr = 0; rr < RPW; ++rr) {
@@ -1201,7 +1254,8 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
         }
     }
   }
-  gemm_epilogue<TBN, false, TBM, NJ, NTH, GNE>(*ep, acc, smem, m0, n0, wm, wn, lane, z);
+  // only k-group 0 holds the tile (wm = -1: the other groups' waves stage nothing, but share the stores)
+  gemm_epilogue<TBN, false, TBM, NJ, NTH, GNE>(*ep, acc, smem, m0, n0, kg == 0 ? wm : -1, wn, lane, z);
 }
 
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
@@ -1410,7 +1464,7 @@ int gemm_variant() {
   if (v == -2) {
     const char* s = getenv("SDMI_GEMM_VARIANT");
     v = s ? atoi(s) : -1;
-    if (v != 0 && (v < 2 || v > 10)) v = -1;
+    if (v != 0 && (v < 2 || v > 11)) v = -1;
   }
   return v;
 }
@@ -1424,7 +1478,7 @@ bool dma_reductions_ok(const sdmi_gemm_desc* d) {
 
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 10) v = d->variant_hint == 1 ? 0 : d->variant_hint;
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 11) v = d->variant_hint == 1 ? 0 : d->variant_hint;
   if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
   if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
   if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
@@ -1434,11 +1488,13 @@ int pick_variant(const sdmi_gemm_desc* d) {
   if (v == 5 && d->a_mode == SDMI_A_CONV && d->a2 && d->k_split % 32) v = 0;
   if (v != 0 && d->a_mode == SDMI_A_COLMAJOR && d->b_mode == SDMI_B_NK) v = 0;  // no DMA instantiation
   // 64-row tiles: K-contiguous images only (row-major / implicit-conv A, [n][k] B), no reduction columns
-  if (v >= 7 && (d->a_mode == SDMI_A_COLMAJOR || d->b_mode != SDMI_B_NK || has_reductions(d))) v = 2;
+  if (v >= 7 && v <= 10 && (d->a_mode == SDMI_A_COLMAJOR || d->b_mode != SDMI_B_NK || has_reductions(d))) v = 2;
+  // k-groups: col-major A (weight gradients) with an MN-contiguous B only
+  if (v == 11 && (d->a_mode != SDMI_A_COLMAJOR || d->b_mode == SDMI_B_NK)) v = 2;
   return v;
 }
 
-int tile_m(const sdmi_gemm_desc*, int variant) { return variant >= 7 ? 64 : BM; }
+int tile_m(const sdmi_gemm_desc*, int variant) { return variant >= 7 && variant <= 10 ? 64 : BM; }
 
 // columns the grid covers: the DMA kernels compute the reduction columns outside the column tiles
 int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total(d) : d->n; }
@@ -1448,7 +1504,7 @@ int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total
 int pick_tbn(const sdmi_gemm_desc* d, int variant) {
   if (variant == 4) return d->n % 384 == 0 ? 384 : 256;
   if (variant == 7) return 64;
-  if (variant >= 8 || variant == 6) return BN;
+  if (variant >= 8 || variant == 6) return BN;  // incl. 11 (k-groups)
   if (variant == 5) return d->b_mode == SDMI_B_NK && d->n % 192 == 0 ? 192 : BN;
   if (variant != 2 || d->b_mode != SDMI_B_NK || d->a_mode == SDMI_A_COLMAJOR) return BN;
   // narrow outputs (N <= 64: the VQVAE's 64-channel convs at 256^2, 4-channel heads, DiT proj_out): a 128-column
@@ -1464,10 +1520,10 @@ int pick_tbn(const sdmi_gemm_desc* d, int variant) {
   return r192 * 192 <= r128 * 128 ? 192 : BN;
 }
 
-template <int AM, int BMODE, int STAGES, int TBN, int TBM, int NWN, int RED, int KBK = BK>
+template <int AM, int BMODE, int STAGES, int TBN, int TBM, int NWN, int RED, int KBK = BK, int KG = 1>
 hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s) {
   constexpr int NTH = dma_threads<TBM, NWN>();
-  constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * KBK * 2, epi = (size_t)64 * (TBN + 4) * 4;
+  constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * KBK * 2 * KG, epi = (size_t)64 * (TBN + 4) * 4;
   if constexpr (RED == 0 && AM != SDMI_A_COLMAJOR && BMODE != SDMI_B_KN_CONV) {
     if (e.gn_part && !e.raw) {  // GroupNorm statistics: + the row-lane sums (NTH / (TBN / 8) x TBN x 2 floats)
       const size_t epi_gn = epi + (size_t)(NTH / (TBN / 8)) * TBN * 2 * 4;
@@ -1477,6 +1533,15 @@ hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s)
     }
   }
   if (e.gn_part && !e.raw) return hipErrorInvalidValue;
+  if constexpr (KG > 1) {
+    // + the k-group hand-off of the accumulators: (4 NJ + 4 RPW) float4 per lane, per wave of one group
+    constexpr int NJ = TBN / NWN / 16, RPW = RED == 0 ? 1 : (RED == 1 ? 1 : (3 + NWN - 1) / NWN);
+    constexpr size_t xs = (size_t)(4 * NJ + 4 * RPW) * 16 * NTH;
+    static_assert(std::max(ring, std::max(epi, xs)) <= 160 * 1024, "LDS");
+    sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK, false, KG>), grid, dim3(NTH * KG),
+                    std::max(ring, std::max(epi, xs)), s, a, e);
+    return hipGetLastError();
+  }
   sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid, dim3(NTH), std::max(ring, epi), s,
                   a, e);
   return hipGetLastError();
@@ -1485,6 +1550,10 @@ hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s)
 template <int AM, int BMODE, int RED>
 hipError_t launch_dma_red(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
   if (v == 3 && RED == 0) return launch_dma<AM, BMODE, 3, BN, BM, 2, 0>(a, e, grid, s);
+  if constexpr (AM == SDMI_A_COLMAJOR) {
+    // two k-groups of 4 waves on one 128 x 128 tile, 2-stage 64-deep rings (128 KiB): one 8-wave workgroup per CU
+    if (v == 11) return launch_dma<AM, BMODE, 2, BN, BM, 2, RED, BK, 2>(a, e, grid, s);
+  }
   if (v == 6) return launch_dma<AM, BMODE, 4, BN, BM, 2, RED>(a, e, grid, s);  // 4-stage 128 x 128 (128 KiB ring)
   if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR && RED == 0) {
     if (v == 7) return launch_dma<AM, BMODE, 6, 64, 64, 4, 0>(a, e, grid, s);    // 64 x 64, 6 stages (96 KiB)

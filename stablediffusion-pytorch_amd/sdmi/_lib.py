@@ -180,7 +180,10 @@ class _Lib:
 
     def __init__(self, cdll):
         self._cdll = cdll
+        ab = bool(os.environ.get("SDMI_LIB_PATH"))  # A/B timing against an older library: newer entry points may lack
         for name, (argt, rest) in SIGNATURES.items():
+            if ab and not hasattr(cdll, name):
+                continue
             fn = getattr(cdll, name)
             fn.argtypes = argt
             fn.restype = rest

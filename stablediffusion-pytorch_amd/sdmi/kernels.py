@@ -308,7 +308,7 @@ def linear_wgrad(dy, x, out, *, bias_grad=None, bias_grad2=None, group_sums=None
 # reduction columns ride along). The tuned table holds single-problem entries, mostly the register-staged mainloop,
 # which lost to the DMA ring once 6-8 problems share the grid. Same box: cond-UNet 13.36 / 13.30 -> 13.29 / 13.27 ms,
 # DiT-12L 3.56 / 3.56 -> 3.53 / 3.52 ms.
-GROUPED_VARIANT = 3
+GROUPED_VARIANT = int(os.environ.get("SDMI_GROUPED_VARIANT", "3"))  # diagnostic override (A/B of mainloops)
 
 
 def linear_wgrad_grouped(items):

@@ -11,8 +11,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 # tuned-table mainloop ids (sdmi/tuned_gemm.json): 1 register staging, 2 / 3 / 5 / 6 LDS-DMA rings (3 falls back to 2
-# where reduction columns ride along), 4 = 128 x {256, 384} tiles on 8 waves
-VARIANTS = (1, 2, 3, 5, 6)
+# where reduction columns ride along), 4 = 128 x {256, 384} tiles on 8 waves, 11 = two k-groups of 4 waves per tile
+VARIANTS = (1, 2, 3, 5, 6, 11)
 SPLITS = (1, 2, 4, 8)
 
 
@@ -98,7 +98,7 @@ def test_linear_wgrad_reductions_deterministic(monkeypatch, M, N, K, group, vari
         assert _relerr(outs[0][2], gref) < 1e-2, tag
 
 
-@pytest.mark.parametrize("variant", (2, 3, 5))
+@pytest.mark.parametrize("variant", (2, 3, 5, 11))
 @pytest.mark.parametrize("G,M,N,K,splits", [(2, 8192, 288, 288, 24), (3, 8192, 288, 1152, 12), (6, 512, 512, 512, 8),
                                              (7, 2048, 136, 264, 4)])
 def test_grouped_wgrad_bias_deterministic(monkeypatch, G, M, N, K, splits, variant):
@@ -125,3 +125,24 @@ def test_grouped_wgrad_bias_deterministic(monkeypatch, G, M, N, K, splits, varia
     for dy, x, o, b in runs[0]:
         assert _relerr(o, dy.float().t() @ x.float()) < 2e-3
         assert _relerr(b, dy.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("splits", (1, 2, 3, 5))
+@pytest.mark.parametrize("M,N,K", [(136, 264, 200), (384, 512, 192), (128, 1152, 4160), (256, 384, 64)])
+def test_kgroup_mainloop_plain_colmajor(monkeypatch, M, N, K, splits):
+    """Variant 11 (two k-groups per workgroup, interleaved k-tiles, accumulators summed through LDS in group order) on
+    plain col-major weight-gradient GEMMs, including splits whose k-tile count is odd or smaller than the group count
+    (one group idles through its barriers): bitwise deterministic over repeats and within fp32 tolerance."""
+    from sdmi import kernels as Kn, _lib as L
+    _forced(monkeypatch, Kn, splits, 11)
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    at = torch.randn(K, M, generator=g).to(torch.bfloat16).cuda()
+    b = torch.randn(K, N, generator=g).to(torch.bfloat16).cuda()
+    outs = []
+    for _ in range(3):
+        c = torch.full((M, N), float("nan"), device="cuda")
+        Kn.gemm(M, N, K, at, L.A_COLMAJOR, M, b, L.B_KN, N, c, N)
+        outs.append(c)
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, outs[0]) for o in outs[1:])
+    assert _relerr(outs[0], at.float().t() @ b.float()) < 2e-3
