@@ -24,6 +24,7 @@
 #include <string.h>
 #include <algorithm>
 #include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
@@ -47,6 +48,12 @@ struct Args {
   // 1: row sums of A over k accumulated from the staged A chunks in VALU (bias gradient without the extra tile
   // column the synthesised-column path costs; used when no per-group sums are wanted)
   int rowsum;
+  // implicit-im2col B (weight gradients, k = pixel): how a full k-tile of KBK consecutive pixels maps onto the output
+  // grid, bit flags per staged depth (bits 0-1: KBK 64, bits 2-3: KBK 32). Form 1: the tile is KBK / ow whole rows of
+  // one image (oh * ow % KBK == 0, KBK % ow == 0) -> image and first row are tile-uniform, each lane's row offset and
+  // column are fixed; form 2: the tile is KBK / (oh * ow) whole images (KBK % (oh * ow) == 0) -> only the first image
+  // is tile-uniform. Either way the per-piece gather needs no division (DMA kernel, issue_fast_b).
+  int bfast;
   // grouped launch (sdmi_gemm_grouped): ngroups > 1 independent problems of one shape; the grid's z runs over
   // (problem, split) and problem p reads its operands from Ag[p] / Bg[p] (Ag[0] = A, Bg[0] = B)
   int ngroups;
@@ -808,6 +815,36 @@ __device__ __forceinline__ s16x8 frag_tr_asm(const char* tile, int cbase, int ks
   return r;
 }
 
+// the same read at LDS byte address a + OFF (OFF < 65536: the instruction's offset field), so the loop-invariant part of
+// an address stays in one VGPR and the stage / k-step / row part is an immediate (no per-iteration VALU address adds)
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_tr_off(unsigned a) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF) : "memory");
+  return r;
+}
+
+template <int OFF>
+__device__ __forceinline__ s16x8 frag_tr_off(unsigned a) {
+  const s16x4 lo = ds_tr_off<OFF>(a), hi = ds_tr_off<OFF + 1024>(a);  // k-rows +4: same swizzle (tr_swz ignores bit 2)
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// lane part of frag_tr_asm's address for column base cbase (% 128) at k-step 0 (k-step ks adds 32 rows = 8192 B: the
+// swizzle ignores bit 5 of the row)
+__device__ __forceinline__ int frag_tr_lane(int cbase, int lane) {
+  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  return tr_off(gq * 8 + q, (cbase >> 3) + (p >> 1)) + (p & 1) * 8;
+}
+
+template <int N>
+struct IC { static constexpr int value = N; };
+struct RT { int value; };  // a runtime ring stage (K-contiguous-only kernels keep their plain loop)
+
 // all LDS reads issued so far have landed; the fragments are re-defined after the wait so no consumer (an MFMA is
 // register-only and would otherwise be hoisted above an asm wait) reads them earlier
 template <int N>
@@ -971,6 +1008,32 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
       }
     }
   }
+  // implicit-im2col B, full k-tiles of a regular pixel grid (Args::bfast): the tile-invariant part of every lane's
+  // gather offset, so issue_fast_b needs an add, a range check and a select per piece (no per-piece divisions)
+  const int bform = BMODE == SDMI_B_KN_CONV ? ((g.bfast >> (KBK == 64 ? 0 : 2)) & 3) : 0;
+  int bf_c[B_PW], bf_y[B_PW];
+#pragma unroll
+  for (int j = 0; j < B_PW; ++j) {
+    bf_c[j] = OOB;
+    bf_y[j] = -(1 << 29);
+    if (BMODE == SDMI_B_KN_CONV && bform) {
+      const int kr = b_kk[j];
+      if (bform == 1) {  // lane row kr of the tile: row dy below the tile's first output row, column ox
+        const int dy = (int)g.ow_d.div((unsigned)kr), ox = kr - dy * g.ow_d.d();
+        const int ix = ox * g.sx + g.ox0 + b_tx[j];
+        if (b_ok[j] && (unsigned)ix < (unsigned)g.iw) {
+          bf_y[j] = dy * g.sy + g.oy0 + b_ty[j];
+          bf_c[j] = (ix * g.ldx + b_base[j]) * 2;
+        }
+      } else {  // image db after the tile's first image, at (oy, ox)
+        const int db = (int)g.ohw_d.div((unsigned)kr), r = kr - db * g.ohw_d.d();
+        const int oy = (int)g.ow_d.div((unsigned)r), ox = r - oy * g.ow_d.d();
+        const int iy = oy * g.sy + g.oy0 + b_ty[j], ix = ox * g.sx + g.ox0 + b_tx[j];
+        if (b_ok[j] && (unsigned)iy < (unsigned)g.ih && (unsigned)ix < (unsigned)g.iw)
+          bf_c[j] = (((db * g.ih + iy) * g.iw + ix) * g.ldx + b_base[j]) * 2;
+      }
+    }
+  }
 
   // implicit-conv tap state (cin % 64 == 0): the (ty, tx, channel offset) of the next k-tile to issue, advanced
   // incrementally -- issue() is called for consecutive k-tiles -- instead of two runtime divisions per tile
@@ -1081,6 +1144,25 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
     }
   };
 
+  // full k-tile of implicit-im2col B at pixel k0 (k0 % KBK == 0), bform != 0: the tile's image (and first output row)
+  // are wave-uniform scalars
+  auto issue_fast_b = [&](int k0, char* sb) __attribute__((always_inline)) {
+    const int b = (int)g.ohw_d.div((unsigned)k0);
+    const int sbase = b * g.ih * g.iw * g.ldx * 2;
+    if (bform == 1) {
+      const int soy = (int)g.ow_d.div((unsigned)(k0 - b * g.ohw_d.d())) * g.sy;
+      const int rowb = g.iw * g.ldx * 2;
+#pragma unroll
+      for (int j = 0; j < B_PW; ++j) {
+        const int iy = bf_y[j] + soy;
+        dma16(rsB, sb + (wave * B_PW + j) * 1024, (unsigned)iy < (unsigned)g.ih ? sbase + iy * rowb + bf_c[j] : OOB);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < B_PW; ++j) dma16(rsB, sb + (wave * B_PW + j) * 1024, bf_c[j] + sbase);  // OOB stays OOB
+    }
+  };
+
   auto issue = [&](int kt, int stage) __attribute__((always_inline)) {
     char* sa = ring + stage * STAGE_BYTES;
     char* sb = sa + A_BYTES;
@@ -1113,6 +1195,10 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
         for (int j = 0; j < B_PW; ++j) dma16(rsB, sb + (wave * B_PW + j) * 1024, b_v[j] + bsh);
         return;
       }
+      if (bform) {
+        issue_fast_b(k0, sb);
+        return;
+      }
     } else {
       issue_general_a(k0, sa);
     }
@@ -1137,59 +1223,114 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   const int nt_all = kt1 - kt0;
   const int nt = nt_all > kg ? (nt_all - kg + KG - 1) / KG : 0;
   const int nt_loop = (nt_all + KG - 1) / KG;  // barrier count: every k-group runs the first group's trip count
+  // Transposed (MN-contiguous) fragment reads: the lane's address at stage 0, k-step 0 is loop-invariant (one VGPR per
+  // 16-row / 16-column fragment); stage, k-step and the +4-row half are immediates of ds_read_b64_tr_b16 when the ring
+  // fits the 16-bit offset field, else the stage part is one add per fragment and stage. The loop body is unrolled
+  // over the ring's stages so the stage index is a compile-time constant. (The round-4 loop recomputed every read
+  // address from a runtime stage base: 44 VALU adds per 32 MFMAs in the weight-gradient kernel.)
+  const unsigned ring_lds = (unsigned)(uintptr_t)(SDMI_LDS const char*)ring;
+  unsigned fa_base[4], fb_base[NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int mb = wm + 16 * i;
+    fa_base[i] = ring_lds + (mb >> 7) * SUB + frag_tr_lane(mb & 127, lane);
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nb = wn + 16 * j;
+    fb_base[j] = ring_lds + A_BYTES + (nb >> 7) * SUB + frag_tr_lane(nb & 127, lane);
+  }
+  // largest immediate: last stage + last k-step + the +4-row half
+  constexpr bool STAGE_IMM = (STAGES - 1) * STAGE_BYTES + (KS - 1) * 8192 + 1024 < 65536;
+  static_assert(STAGES <= 6, "stage-unrolled loop");
+
+  // one k-tile of this k-group at ring stage st_c (IC: compile time; RT: run time): wait, barrier, refill, MFMAs
+  auto step = [&](int t, auto st_c) __attribute__((always_inline)) {
+    using SC = decltype(st_c);
+    constexpr bool CST = !std::is_same<SC, RT>::value;
+    const int ST = st_c.value;
+    // tile t landed for this thread: at most (tiles issued after t) x (A_PW + B_PW) DMA instructions outstanding
+    // (in the last STAGES-2 tiles fewer are in flight: wait for all)
+    if (STAGES > 2 && t + STAGES - 2 < nt)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((STAGES > 2 ? STAGES - 2 : 0) * (A_PW + B_PW)) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for tile t done; every wave done with tile t-1
+    if (KG > 1 && t >= nt) return;  // this k-group has no tile t (its last barriers only)
+    if (t + STAGES - 1 < nt) issue(kt0 + (t + STAGES - 1) * KG + kg, (ST + STAGES - 1) % STAGES);
+    const char* ta = ring + ST * STAGE_BYTES;
+    const char* tb = ta + A_BYTES;
+    (void)ta;
+    (void)tb;
+    constexpr int SOFF = [] {
+      if constexpr (CST) return STAGE_IMM ? SC::value * STAGE_BYTES : 0;
+      else return 0;
+    }();
+    unsigned fa_b[4], fb_b[NJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa_b[i] = STAGE_IMM ? fa_base[i] : fa_base[i] + ST * STAGE_BYTES;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) fb_b[j] = STAGE_IMM ? fb_base[j] : fb_base[j] + ST * STAGE_BYTES;
+    __builtin_amdgcn_s_setprio(1);
+    auto kstep = [&](auto ks_c) __attribute__((always_inline)) {
+      constexpr int ks = decltype(ks_c)::value;
+      s16x8 fa[4], fb[NJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mb = wm + 16 * i;
+        if constexpr (A_MN) fa[i] = frag_tr_off<SOFF + ks * 8192>(fa_b[i]);
+        else fa[i] = frag_kc_k<KBK>(ta, mb, ks, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int nb = wn + 16 * j;
+        if constexpr (B_MN) fb[j] = frag_tr_off<SOFF + ks * 8192>(fb_b[j]);
+        else fb[j] = frag_kc_k<KBK>(tb, nb, ks, lane);
+      }
+      if constexpr (A_MN) lds_wait_frags(fa);
+      if constexpr (B_MN) lds_wait_frags(fb);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if (RED != 0 && red_tile) {
+        const int kb = (kt0 + t * KG + kg) * KBK + ks * 32 + (lane >> 4) * 8;
+#pragma unroll
+        for (int rr = 0; rr < RPW; ++rr) {
+          const int r = wave % NWN + rr * NWN;
+          if (r < nred) {
+            const s16x8 fr = reduce_frag<RED>(g, r, kb, lane);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              accr[rr][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fr, accr[rr][i], 0, 0, 0);
+          }
+        }
+      }
+    };
+    kstep(IC<0>{});
+    if constexpr (KS > 1) kstep(IC<1>{});
+    __builtin_amdgcn_s_setprio(0);
+  };
+
   if (nt_loop > 0) {
     // prologue: STAGES-1 tiles in flight
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s)
       if (s < nt) issue(kt0 + s * KG + kg, s);
-    for (int t = 0; t < nt_loop; ++t) {
-      // tile t landed for this thread: at most (tiles issued after t) x (A_PW + B_PW) DMA instructions outstanding
-      // (in the last STAGES-2 tiles fewer are in flight: wait for all)
-      if (STAGES > 2 && t + STAGES - 2 < nt)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"((STAGES > 2 ? STAGES - 2 : 0) * (A_PW + B_PW)) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's DMA for tile t done; every wave done with tile t-1
-      if (KG > 1 && t >= nt) continue;  // this k-group has no tile t (its last barriers only)
-      if (t + STAGES - 1 < nt) issue(kt0 + (t + STAGES - 1) * KG + kg, (t + STAGES - 1) % STAGES);
-      const char* ta = ring + (t % STAGES) * STAGE_BYTES;
-      const char* tb = ta + A_BYTES;
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        s16x8 fa[4], fb[NJ];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int mb = wm + 16 * i;
-          fa[i] = A_MN ? frag_tr_asm(ta + (mb >> 7) * SUB, mb & 127, ks, lane) : frag_kc_k<KBK>(ta, mb, ks, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int nb = wn + 16 * j;
-          fb[j] = B_MN ? frag_tr_asm(tb + (nb >> 7) * SUB, nb & 127, ks, lane) : frag_kc_k<KBK>(tb, nb, ks, lane);
-        }
-        if constexpr (A_MN) lds_wait_frags(fa);
-        if constexpr (B_MN) lds_wait_frags(fb);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        if (RED != 0 && red_tile) {
-          const int kb = (kt0 + t * KG + kg) * KBK + ks * 32 + (lane >> 4) * 8;
-#pragma unroll
-          for (int rr = 0; rr < RPW; ++rr) {
-            const int r = wave % NWN + rr * NWN;
-            if (r < nred) {
-              const s16x8 fr = reduce_frag<RED>(g, r, kb, lane);
-#pragma unroll
-              for (int i = 0; i < 4; ++i)
-                accr[rr][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fr, accr[rr][i], 0, 0, 0);
-            }
-          }
-        }
-      }
-      __builtin_amdgcn_s_setprio(0);
+    // tile t sits in ring stage t % STAGES: with transposed reads the loop advances STAGES tiles per trip with the
+    // stage as a constant; the K-contiguous-only kernels keep the plain loop (their reads fold the stage base
+    // themselves, and the unrolled form measured slower for the 32^2 conv forward: 88 -> 93 us)
+    if constexpr (!A_MN && !B_MN) {
+      for (int t = 0; t < nt_loop; ++t) step(t, RT{t % STAGES});
+    } else
+    for (int t0 = 0; t0 < nt_loop; t0 += STAGES) {
+      step(t0, IC<0>{});
+      if constexpr (STAGES > 1) if (t0 + 1 < nt_loop) step(t0 + 1, IC<1 % STAGES>{});
+      if constexpr (STAGES > 2) if (t0 + 2 < nt_loop) step(t0 + 2, IC<2 % STAGES>{});
+      if constexpr (STAGES > 3) if (t0 + 3 < nt_loop) step(t0 + 3, IC<3 % STAGES>{});
+      if constexpr (STAGES > 4) if (t0 + 4 < nt_loop) step(t0 + 4, IC<4 % STAGES>{});
+      if constexpr (STAGES > 5) if (t0 + 5 < nt_loop) step(t0 + 5, IC<5 % STAGES>{});
     }
   }
   __syncthreads();
@@ -1634,6 +1775,14 @@ int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
   a.ohw_d = FastDiv::make(std::max(1, d->geom.oh * d->geom.ow));
   a.ow_d = FastDiv::make(std::max(1, d->geom.ow));
   a.sy = d->geom.sy; a.sx = d->geom.sx; a.oy0 = d->geom.oy0; a.ox0 = d->geom.ox0;
+  if (d->b_mode == SDMI_B_KN_CONV) {
+    const int ohw = d->geom.oh * d->geom.ow, ow = d->geom.ow;
+    for (int sh = 0; sh < 2; ++sh) {  // KBK 64, then 32
+      const int kb = sh ? 32 : 64;
+      const int f = (ohw % kb == 0 && kb % ow == 0) ? 1 : (kb % ohw == 0 ? 2 : 0);
+      a.bfast |= f << (2 * sh);
+    }
+  }
   a.A2 = (const bf16_t*)d->a2; a.lda2 = d->lda2;
   a.k_split = (d->a_mode == SDMI_A_CONV && d->a2) ? d->k_split : d->k;
   e.M = d->m; e.N = d->n;
