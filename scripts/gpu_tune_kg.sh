@@ -5,8 +5,12 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 T=${TAG:-kg}
 cp stablediffusion-pytorch_amd/sdmi/tuned_gemm.json gpurun_out/tuned_$T.json
+if [ -n "$TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_$T.log 2>&1
+  rc=$?; tail -2 gpurun_out/t_$T.log; [ $rc -eq 0 ] || exit 1
+fi
 for WL in ${WLS:-cond-unet dit}; do
-  SDMI_TUNE_VARIANTS=${VARS:-11} timeout -k 10 900 python -u scripts/tune_gemm.py --workload $WL --against-table --only-colmajor --out gpurun_out/tuned_$T.json > gpurun_out/tune_${T}_$WL.log 2>&1 || { tail -5 gpurun_out/tune_${T}_$WL.log; exit 1; }
+  SDMI_TUNE_VARIANTS=${VARS:-11} timeout -k 10 900 python -u scripts/tune_gemm.py --workload $WL --against-table ${MODESEL:---only-colmajor} --out gpurun_out/tuned_$T.json > gpurun_out/tune_${T}_$WL.log 2>&1 || { tail -5 gpurun_out/tune_${T}_$WL.log; exit 1; }
   tail -2 gpurun_out/tune_${T}_$WL.log
 done
 ms() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(round(d['ms_per_step'],3))" $1; }

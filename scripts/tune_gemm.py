@@ -47,6 +47,7 @@ def main():
                          "replace the entry where one beats it by > 3 %")
     ap.add_argument("--only-colmajor", action="store_true",
                     help="tune only the weight-gradient (col-major A) launches, e.g. for a new weight-gradient mainloop")
+    ap.add_argument("--skip-colmajor", action="store_true", help="tune only the forward / data-gradient launches")
     ap.add_argument("--out", default=os.path.join(REPO, "stablediffusion-pytorch_amd", "sdmi", "tuned_gemm.json"))
     args = ap.parse_args()
     from sdmi import _lib, kernels as K
@@ -122,6 +123,8 @@ def main():
         if args.only_new and key in table:
             continue
         if args.only_colmajor and d.a_mode != _lib.A_COLMAJOR:
+            continue
+        if args.skip_colmajor and d.a_mode == _lib.A_COLMAJOR:
             continue
         d.splits_hint = 0
         d.variant_hint = 0

@@ -146,3 +146,55 @@ def test_kgroup_mainloop_plain_colmajor(monkeypatch, M, N, K, splits):
     torch.cuda.synchronize()
     assert all(torch.equal(o, outs[0]) for o in outs[1:])
     assert _relerr(outs[0], at.float().t() @ b.float()) < 2e-3
+
+
+@pytest.mark.parametrize("splits", (1, 2, 3))
+def test_kgroup_mainloop_rowmajor_and_conv(monkeypatch, splits):
+    """Variant 11 on the forward / data-gradient operand modes: a ragged row-major linear with bias + residual, an
+    implicit-GEMM 3x3 conv with cin % 64 == 0 (incremental tap state advanced per k-group), one with cin = 32 (general
+    gather), and a conv with the K-concatenated 1x1 second source; repeated bitwise and against torch fp32."""
+    import torch.nn.functional as F
+    from sdmi import kernels as Kn, _lib as L
+    _forced(monkeypatch, Kn, splits, 11)
+    g = torch.Generator().manual_seed(41 + splits)
+    bf = torch.bfloat16
+    M, N, Kd = 300, 200, 136
+    a = torch.randn(M, Kd, generator=g).to(bf).cuda()
+    w = torch.randn(N, Kd, generator=g).to(bf).cuda()
+    bias = torch.randn(N, generator=g).cuda()
+    res = torch.randn(M, N, generator=g).to(bf).cuda()
+    outs = []
+    for _ in range(3):
+        c = torch.full((M, N), float("nan"), device="cuda")
+        Kn.gemm(M, N, Kd, a, L.A_ROWMAJOR, Kd, w, L.B_NK, Kd, c, N, bias=bias, resid=res, ldr=N)
+        outs.append(c)
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, outs[0]) for o in outs[1:])
+    assert _relerr(outs[0], a.float() @ w.float().t() + bias + res.float()) < 2e-3
+    for (B, H, cin, cout) in ((2, 8, 64, 128), (3, 8, 32, 64)):
+        x = torch.randn(B, cin, H, H, generator=g).to(bf)
+        wt = (torch.randn(cout, cin, 3, 3, generator=g) * 0.1).to(bf)
+        ref = F.conv2d(x.float(), wt.float(), padding=1).cuda()
+        xn = x.permute(0, 2, 3, 1).contiguous().cuda()
+        wpk = wt.permute(0, 2, 3, 1).contiguous().cuda()
+        outs = []
+        for _ in range(3):
+            y = torch.full((B, H, H, cout), float("nan"), device="cuda")
+            Kn.conv_fwd(xn, B, H, H, cin, cin, wpk, cout, 3, 3, 1, 1, y, cout)
+            outs.append(y)
+        torch.cuda.synchronize()
+        assert all(torch.equal(o, outs[0]) for o in outs[1:])
+        assert _relerr(outs[0].permute(0, 3, 1, 2), ref) < 2e-3
+    # conv + fused 1x1 of a second source (the resnet's conv2 + residual conv): W = [W3x3 | W1x1] along K
+    B, H, cin, cin2, cout = 2, 8, 64, 128, 64
+    x = torch.randn(B, cin, H, H, generator=g).to(bf)
+    x2 = torch.randn(B, cin2, H, H, generator=g).to(bf)
+    w3 = (torch.randn(cout, cin, 3, 3, generator=g) * 0.1).to(bf)
+    w1 = (torch.randn(cout, cin2, 1, 1, generator=g) * 0.1).to(bf)
+    ref = (F.conv2d(x.float(), w3.float(), padding=1) + F.conv2d(x2.float(), w1.float())).cuda()
+    wcat = torch.cat([w3.permute(0, 2, 3, 1).reshape(cout, -1), w1.reshape(cout, -1)], 1).contiguous().cuda()
+    xn, x2n = x.permute(0, 2, 3, 1).contiguous().cuda(), x2.permute(0, 2, 3, 1).contiguous().cuda()
+    y = torch.full((B, H, H, cout), float("nan"), device="cuda")
+    Kn.conv_fwd(xn, B, H, H, cin, cin, wcat, cout, 3, 3, 1, 1, y, cout, x2=x2n.view(-1, cin2), cin2=cin2)
+    torch.cuda.synchronize()
+    assert _relerr(y.permute(0, 3, 1, 2), ref) < 2e-3
