@@ -917,8 +917,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   static_assert(!B_MN || TBN % 128 == 0, "MN-contiguous B: 128-column sub-tiles");
   static_assert(WTN % 16 == 0 && TBM % 64 == 0, "wave tile");
   static_assert(RED == 0 || A_MN, "reductions: col-major A only");
-  // the implicit-conv A keeps incremental tap state over consecutive k-tiles: k-groups only on col-major A
-  static_assert(KG == 1 || (A_MN && !GNE), "k-groups: weight-gradient (col-major A) launches only");
+  static_assert(KG == 1 || TBM == 128, "k-groups: 128-row tiles");
   constexpr int RPW = RED == 0 ? 0 : (RED == 1 ? 1 : (3 + NWN - 1) / NWN);  // reduction tiles per wave (<= 3 total)
   extern __shared__ __attribute__((aligned(16))) char smem[];  // STAGES x (A | B)
   const int tid = threadIdx.x;
@@ -1038,12 +1037,26 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   // implicit-conv tap state (cin % 64 == 0): the (ty, tx, channel offset) of the next k-tile to issue, advanced
   // incrementally -- issue() is called for consecutive k-tiles -- instead of two runtime divisions per tile
   int c_ty = 0, c_tx = 0, c_ci = 0;
-  if (AM == SDMI_A_CONV && cin64 && kt0 * KBK < g.k_split) {
-    const int tap = (kt0 * KBK) / g.cin;
-    c_ci = kt0 * KBK - tap * g.cin;
+  // (k-groups: this group's first tile is kt0 + kg, and each issue advances KG tiles)
+  if (AM == SDMI_A_CONV && cin64 && (kt0 + kg) * KBK < g.k_split) {
+    const int tap = ((kt0 + kg) * KBK) / g.cin;
+    c_ci = (kt0 + kg) * KBK - tap * g.cin;
     c_ty = tap / g.kw;
     c_tx = tap - c_ty * g.kw;
   }
+  auto advance_tap = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < KG; ++q) {
+      c_ci += KBK;
+      if (c_ci >= g.cin) {
+        c_ci = 0;
+        if (++c_tx == g.kw) {
+          c_tx = 0;
+          ++c_ty;
+        }
+      }
+    }
+  };
   // Fast issue path for full k-tiles: every per-lane part of a DMA source offset is fixed over the K loop, the
   // per-tile part is wave-uniform (k0, or the conv tap shift), so a piece costs an add and a select instead of the
   // general path's coordinate math and bounds checks. Invalid lanes keep OOB (+ a uniform offset < 2^31: still out
@@ -1110,16 +1123,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
       }
       dma16(rsA, dst, off);
     }
-    if (AM == SDMI_A_CONV && cin64 && k0 < g.k_split) {
-      c_ci += KBK;
-      if (c_ci >= g.cin) {
-        c_ci = 0;
-        if (++c_tx == g.kw) {
-          c_tx = 0;
-          ++c_ty;
-        }
-      }
-    }
+    if (AM == SDMI_A_CONV && cin64 && k0 < g.k_split) advance_tap();
   };
   auto issue_general_b = [&](int k0, char* sb) __attribute__((always_inline)) {
 #pragma unroll
@@ -1179,16 +1183,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
         else off = a_v[j] + ash;
         dma16(rsA, sa + (wave * A_PW + j) * 1024, off);
       }
-      if (AM == SDMI_A_CONV) {
-        c_ci += KBK;
-        if (c_ci >= g.cin) {
-          c_ci = 0;
-          if (++c_tx == g.kw) {
-            c_tx = 0;
-            ++c_ty;
-          }
-        }
-      }
+      if (AM == SDMI_A_CONV) advance_tap();
       if (BMODE != SDMI_B_KN_CONV) {
         const int bsh = BMODE == SDMI_B_NK ? k0 * 2 : k0 * g.ldb * 2;
 #pragma unroll
@@ -1630,8 +1625,8 @@ int pick_variant(const sdmi_gemm_desc* d) {
   if (v != 0 && d->a_mode == SDMI_A_COLMAJOR && d->b_mode == SDMI_B_NK) v = 0;  // no DMA instantiation
   // 64-row tiles: K-contiguous images only (row-major / implicit-conv A, [n][k] B), no reduction columns
   if (v >= 7 && v <= 10 && (d->a_mode == SDMI_A_COLMAJOR || d->b_mode != SDMI_B_NK || has_reductions(d))) v = 2;
-  // k-groups: col-major A (weight gradients) with an MN-contiguous B only
-  if (v == 11 && (d->a_mode != SDMI_A_COLMAJOR || d->b_mode == SDMI_B_NK)) v = 2;
+  // k-groups (128 x 128 tiles of two 4-wave groups): the DMA modes; the conv A's fused second source needs whole
+  // 64-deep tiles on either side of k_split (checked above for every DMA variant)
   return v;
 }
 
@@ -1667,9 +1662,11 @@ hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s)
   constexpr size_t ring = (size_t)STAGES * (TBM + TBN) * KBK * 2 * KG, epi = (size_t)64 * (TBN + 4) * 4;
   if constexpr (RED == 0 && AM != SDMI_A_COLMAJOR && BMODE != SDMI_B_KN_CONV) {
     if (e.gn_part && !e.raw) {  // GroupNorm statistics: + the row-lane sums (NTH / (TBN / 8) x TBN x 2 floats)
-      const size_t epi_gn = epi + (size_t)(NTH / (TBN / 8)) * TBN * 2 * 4;
-      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, 0, KBK, true>), grid, dim3(NTH),
-                      std::max(ring, epi_gn), s, a, e);
+      const size_t epi_gn = epi + (size_t)(NTH * KG / (TBN / 8)) * TBN * 2 * 4;
+      size_t lds = std::max(ring, epi_gn);
+      if constexpr (KG > 1) lds = std::max(lds, (size_t)(4 * (TBN / NWN / 16) + 4) * 16 * NTH);
+      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, 0, KBK, true, KG>), grid, dim3(NTH * KG), lds, s,
+                      a, e);
       return hipGetLastError();
     }
   }
@@ -1691,10 +1688,8 @@ hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s)
 template <int AM, int BMODE, int RED>
 hipError_t launch_dma_red(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, int v, int tbn) {
   if (v == 3 && RED == 0) return launch_dma<AM, BMODE, 3, BN, BM, 2, 0>(a, e, grid, s);
-  if constexpr (AM == SDMI_A_COLMAJOR) {
-    // two k-groups of 4 waves on one 128 x 128 tile, 2-stage 64-deep rings (128 KiB): one 8-wave workgroup per CU
-    if (v == 11) return launch_dma<AM, BMODE, 2, BN, BM, 2, RED, BK, 2>(a, e, grid, s);
-  }
+  // two k-groups of 4 waves on one 128 x 128 tile, 2-stage 64-deep rings (128 KiB): one 8-wave workgroup per CU
+  if (v == 11) return launch_dma<AM, BMODE, 2, BN, BM, 2, RED, BK, 2>(a, e, grid, s);
   if (v == 6) return launch_dma<AM, BMODE, 4, BN, BM, 2, RED>(a, e, grid, s);  // 4-stage 128 x 128 (128 KiB ring)
   if constexpr (BMODE == SDMI_B_NK && AM != SDMI_A_COLMAJOR && RED == 0) {
     if (v == 7) return launch_dma<AM, BMODE, 6, 64, 64, 4, 0>(a, e, grid, s);    // 64 x 64, 6 stages (96 KiB)
