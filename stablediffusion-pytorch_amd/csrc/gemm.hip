@@ -1615,7 +1615,7 @@ bool dma_reductions_ok(const sdmi_gemm_desc* d) {
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
   if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 11) v = d->variant_hint == 1 ? 0 : d->variant_hint;
-  if (v < 0) v = d->a_mode == SDMI_A_COLMAJOR ? 0 : 2;
+  if (v < 0) v = 2;  // (col-major A with [n][k] B has no DMA instantiation: register staging below)
   if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
   if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
   // the DMA path needs a tile-uniform second source (k_split % BK == 0)
