@@ -17,6 +17,7 @@ for MI355X:
 Parameters are referenced by the reference's state-dict keys.
 """
 import contextlib
+import os
 
 import torch
 
@@ -1109,11 +1110,12 @@ class UNetEngine:
 
     # ------------------------------------------------------------------------------------------
     @contextlib.contextmanager
-    def _wg(self, *keep):
+    def _wg(self, *keep, balance=False):
         """Weight-gradient work: issued on the side stream after everything issued so far on the current
         stream. `keep` pins the operand tensors until the backward's final join, so the caching
         allocator cannot hand their memory to the current stream while the side stream still reads it.
-        The block's completion event is left in self.wg_event."""
+        The block's completion event is left in self.wg_event. balance: the side stream with the fewer GEMM FLOPs
+        issued so far in this backward (the block flushes' grouped launches), else round-robin."""
         prev = K.PHASE
         K.PHASE = "wg"
         if self.side is None:
@@ -1123,19 +1125,26 @@ class UNetEngine:
                 K.PHASE = prev
             return
         self._keep.extend(keep)
-        si = self._wg_next % len(self.sides)  # round-robin (FLOP-balanced measured no better)
+        sflops = self.__dict__.setdefault("_side_flops", [0.0] * len(self.sides))  # reset per backward
+        if balance:
+            si = min(range(len(self.sides)), key=lambda i: sflops[i])
+        else:
+            si = self._wg_next % len(self.sides)  # round-robin (FLOP-balanced for every block measured no better)
+            self._wg_next += 1
         side = self.sides[si]
-        self._wg_next += 1
         plan.wait_stream(side, torch.cuda.current_stream(self.device))
+        f0 = K.FLOPS_ISSUED
         try:
             with torch.cuda.stream(side):
                 yield
         finally:
             K.PHASE = prev
+        sflops[si] += K.FLOPS_ISSUED - f0
         self.wg_event = torch.cuda.Event()
         plan.record_event(self.wg_event, side)
 
     _group_wg = True  # engines whose backward loop does not flush per block (VQVAETrainEngine) set False
+    wg_balance = os.environ.get("SDMI_WG_FLUSH_BALANCE", "1") != "0"  # A/B switch of the flush-group stream choice
 
     def _grouping(self):
         return self._group_wg and self.side is not None
@@ -1158,10 +1167,14 @@ class UNetEngine:
         """Issue the deferred weight gradients (groups of at most SDMI_GEMM_GROUP_MAX = 8) and the block's deferred
         GroupNorm dgamma / dbeta sums."""
         pend, self._pending_wg = self._pending_wg, {}
-        for items in pend.values():
-            for i in range(0, len(items), 8):
-                with self._wg():
-                    K.linear_wgrad_grouped(items[i:i + 8])
+        # largest groups first, each on the side stream with less work issued so far: at the end of the backward the
+        # last block's grouped launches are the tail the optimizer waits for (round 5: two ~160 us launches of the
+        # 32^2 down block had both landed on one stream by round-robin parity while the other went idle)
+        groups = [items[i:i + 8] for items in pend.values() for i in range(0, len(items), 8)]
+        groups.sort(key=lambda g: -g[0][0].shape[0] * g[0][0].shape[1] * g[0][1].shape[1] * len(g))
+        for grp in groups:
+            with self._wg(balance=self.wg_balance):
+                K.linear_wgrad_grouped(grp)
         gpend, self._pending_gn = self._pending_gn, []
         if gpend:
             # on the first weight-gradient stream, outside the round-robin (the block's other assignments unchanged)
@@ -1212,6 +1225,7 @@ class UNetEngine:
         tape = ctx["tape"]
         self._need_all()  # the optimizer chunks read the gradient buffers the backward is about to overwrite
         self._wg_next = 0  # same side-stream assignment every step
+        self._side_flops = [0.0] * len(self.sides)
         K.PHASE = "bwd"
         self._pending_wg = {}
         self._pending_gn = []
