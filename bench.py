@@ -546,15 +546,19 @@ def main():
     backend = os.environ.get("SDMI_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    # the engines' concurrent streams bound to hardware queues of their own before RCCL binds its streams
+    # (sdmi/streams.py: HIP binds a stream to a queue at first use, rotating once all four exist)
+    if os.environ.get("SDMI_RESERVE_STREAMS", "1") == "1":
+        from sdmi import streams
+        streams.reserve(device)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     collectives = collective_facts(world, device)
     forced = args.force_reducer and world == 1
     if forced:  # an RCCL group of one rank: the reducer's all-reduces are identities, their cost is real

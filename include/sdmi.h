@@ -474,10 +474,27 @@ int sdmi_plan_note_callout(int id);
 int sdmi_plan_info(const void* plan, int* ops, int* launches);
 int sdmi_plan_replay(void* plan, int start, int* callout, int* next);
 int sdmi_plan_destroy(void* plan);
-/* profiling: op kind (0 launch, 1 event record, 2 stream wait, 3 callout), kernel name, grid[3], block, LDS bytes;
+/* profiling: op kind (0 launch, 1 event record, 2 stream wait, 3 callout, 4 all-reduce), kernel name, grid[3], block,
+ * LDS bytes;
  * and the average device time of launch op i re-issued alone (iters times after warm untimed issues). */
 int sdmi_plan_op_info(const void* plan, int i, int* kind, const char** name, int* grid, int* block, int* shmem);
 int sdmi_plan_time_op(void* plan, int i, int warm, int iters, float* us);
+
+/* ---------------------------------------------------------------------------------------------
+ * Gradient all-reduce through RCCL, issued by the library on the caller's stream (replaces the DDP bucket hook's
+ * NCCL all-reduce, train_ddpm_cond_celebhq_multi_gpu.py:257-263 -> torch DDP, and this package's earlier
+ * torch.distributed callouts). sdmi_comm_load binds the RCCL shared library the process already uses (path: torch's
+ * bundled librccl.so, or any RCCL) by dlopen -- libsdmi.so does not link RCCL. Rank 0 makes the unique id
+ * (NCCL_UNIQUE_ID_BYTES = 128 bytes), the caller broadcasts it, every rank calls sdmi_comm_init (collective, blocking)
+ * with the device current. sdmi_allreduce: in-place sum of count elements (dtype 0 fp32, 1 bf16) on `stream`;
+ * while a plan records it is recorded and replayed natively (no callout). Status: 0 ok, 1000 + ncclResult_t on an
+ * RCCL error, negative on bad arguments / RCCL not loaded.
+ * ------------------------------------------------------------------------------------------- */
+int sdmi_comm_load(const char* rccl_path);
+int sdmi_comm_unique_id(unsigned char* id);
+int sdmi_comm_init(const unsigned char* id, int nranks, int rank, void** comm);
+int sdmi_allreduce(void* comm, void* buf, long long count, int dtype, sdmi_stream_t stream);
+int sdmi_comm_destroy(void* comm);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,7 @@ for W in ${WLS:-cond-unet}; do
     for E in "${A[@]}"; do
       i=$((i+1))
       if [ "$E" = "." ]; then EE=""; else EE="$E"; fi
-      env $EE timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 --workload $W > gpurun_out/envab_${W}_$i$r.log 2>&1 || { tail -5 gpurun_out/envab_${W}_$i$r.log; exit 1; }
+      env $EE timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 30 $BARGS --workload $W > gpurun_out/envab_${W}_$i$r.log 2>&1 || { tail -5 gpurun_out/envab_${W}_$i$r.log; exit 1; }
       echo "$W [$E] r$r $(ms gpurun_out/envab_${W}_$i$r.log)"
     done
   done

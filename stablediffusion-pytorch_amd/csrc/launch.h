@@ -18,6 +18,10 @@ extern void* g_recording;
 void record_launch(const void* fn, dim3 grid, dim3 block, unsigned shmem, hipStream_t stream, const void* args,
                    size_t bytes, const unsigned* offsets, int nargs);
 
+// in-place sum all-reduce through the library's RCCL communicator (comm.hip); the plan records and replays it
+void record_allreduce(void* comm, void* buf, size_t count, int dtype, hipStream_t stream);
+int issue_allreduce(void* comm, void* buf, size_t count, int dtype, hipStream_t stream);
+
 template <typename Tuple, size_t... I>
 inline void arg_ptrs(Tuple& t, void** ptrs, unsigned* offs, std::index_sequence<I...>) {
   ((ptrs[I] = (void*)&std::get<I>(t), offs[I] = (unsigned)((const char*)&std::get<I>(t) - (const char*)&t)), ...);

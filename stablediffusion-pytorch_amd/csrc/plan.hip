@@ -21,7 +21,7 @@ void* g_recording = nullptr;
 
 namespace {
 
-enum OpKind { OP_LAUNCH = 0, OP_EVENT = 1, OP_WAIT = 2, OP_CALLOUT = 3 };
+enum OpKind { OP_LAUNCH = 0, OP_EVENT = 1, OP_WAIT = 2, OP_CALLOUT = 3, OP_ALLREDUCE = 4 };
 
 struct alignas(16) Chunk16 {
   unsigned char b[16];
@@ -35,6 +35,10 @@ struct Op {
   hipStream_t stream = nullptr;
   hipEvent_t event = nullptr;
   int callout = -1;
+  void* comm = nullptr;  // OP_ALLREDUCE: communicator, buffer, element count, dtype (0 fp32, 1 bf16)
+  void* buf = nullptr;
+  size_t count = 0;
+  int dtype = 0;
   std::vector<Chunk16> args;   // copy of the argument tuple (16-B aligned)
   std::vector<unsigned> offs;  // byte offset of each argument inside it
 };
@@ -63,6 +67,18 @@ void record_launch(const void* fn, dim3 grid, dim3 block, unsigned shmem, hipStr
   if ((int)p->scratch.size() < nargs) p->scratch.resize(nargs);
   p->ops.push_back(std::move(op));
   ++p->launches;
+}
+
+void record_allreduce(void* comm, void* buf, size_t count, int dtype, hipStream_t stream) {
+  Plan* p = (Plan*)g_recording;
+  Op op;
+  op.kind = OP_ALLREDUCE;
+  op.comm = comm;
+  op.buf = buf;
+  op.count = count;
+  op.dtype = dtype;
+  op.stream = stream;
+  p->ops.push_back(std::move(op));
 }
 
 }  // namespace sdmi_rt
@@ -143,6 +159,15 @@ extern "C" int sdmi_plan_replay(void* plan, int start, int* callout, int* next) 
       }
       case sdmi_rt::OP_EVENT: e = hipEventRecord(op.event, op.stream); break;
       case sdmi_rt::OP_WAIT: e = hipStreamWaitEvent(op.stream, op.event, 0); break;
+      case sdmi_rt::OP_ALLREDUCE: {
+        const int rc = sdmi_rt::issue_allreduce(op.comm, op.buf, op.count, op.dtype, op.stream);
+        if (rc != 0) {
+          *callout = -1;
+          *next = i;
+          return rc;
+        }
+        break;
+      }
       default:
         *callout = op.callout;
         *next = i + 1;
@@ -160,7 +185,7 @@ extern "C" int sdmi_plan_replay(void* plan, int start, int* callout, int* next) 
 }
 
 // Per-op inspection for profiling tools (scripts/plan_profile.py): op kind (0 launch, 1 event record, 2 stream wait,
-// 3 callout), kernel name, grid / block, LDS bytes.
+// 3 callout, 4 all-reduce), kernel name, grid / block, LDS bytes.
 extern "C" int sdmi_plan_op_info(const void* plan, int i, int* kind, const char** name, int* grid, int* block,
                                  int* shmem) {
   const Plan* p = (const Plan*)plan;

@@ -171,6 +171,11 @@ SIGNATURES = {
     "sdmi_plan_op_info": ([_P, _I, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
     "sdmi_plan_time_op": ([_P, _I, _I, _I, ctypes.POINTER(ctypes.c_float)], _I),
+    "sdmi_comm_load": ([ctypes.c_char_p], _I),
+    "sdmi_comm_unique_id": ([_P], _I),
+    "sdmi_comm_init": ([_P, _I, _I, ctypes.POINTER(ctypes.c_void_p)], _I),
+    "sdmi_allreduce": ([_P, _P, _L, _I, _P], _I),
+    "sdmi_comm_destroy": ([_P], _I),
 }
 
 

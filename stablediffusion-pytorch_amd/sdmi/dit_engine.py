@@ -19,6 +19,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
+from . import streams
 from . import plan
 from .unet_engine import PackPlan, UNetEngine, _WaitingParams, contiguous_run
 
@@ -106,7 +107,7 @@ class DiTEngine:
         self.device = next(iter(params.values())).device
         # weight-gradient GEMMs of the backward run round-robin on side streams, overlapped with the data-gradient
         # chain on the current stream: one side stream (measured 0 / 1 / 2 / 3 streams -> 4.47 / 4.00 / 4.08 / 4.11 ms/step)
-        self.sides = [torch.cuda.Stream(device=self.device)] if self.device.type == "cuda" and not single_stream else []
+        self.sides = [streams.new_stream(self.device)] if self.device.type == "cuda" and not single_stream else []
         self.side = self.sides[0] if self.sides else None
         self._wg_next = 0
         self._keep = []

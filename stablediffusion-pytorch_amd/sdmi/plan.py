@@ -116,8 +116,14 @@ class StepPlan:
         return self.info()[0]
 
     def collectives(self):
-        """Number of recorded all-reduce callouts (sdmi.reducer bucket issues)."""
-        return sum(1 for fn, _ in self.ops if getattr(fn, "__name__", "") == "_issue")
+        """Number of recorded bucket all-reduces: native RCCL ops (sdmi_allreduce) plus torch.distributed callouts."""
+        lib = _lib()
+        n, kind = self.info()[0], ctypes.c_int(0)
+        native = 0
+        for i in range(n):
+            _check(lib.sdmi_plan_op_info(self.handle, i, ctypes.byref(kind), None, None, None, None), "sdmi_plan_op_info")
+            native += kind.value == 4
+        return native + sum(1 for fn, _ in self.ops if getattr(fn, "__name__", "") == "_issue")
 
     def replay(self):
         lib = _lib()

@@ -13,17 +13,26 @@ so after the last bucket only the last bucket's pieces and the finalisation rema
 blocks, and a block's partial depends only on its own (all-reduced) data, so the norm is bitwise the whole-buffer norm
 (csrc/optim.hip sumsq_block_kernel).
 
+With an "nccl" (RCCL) group on the GPU the bucket all-reduces are issued by the library's own RCCL communicator on
+the reducer stream (NativeComm, csrc/comm.hip): no torch.distributed call per bucket, no Python callout in a replayed
+plan, and the collective runs on the reducer's hardware queue instead of the process group's internal stream, which
+shares a queue with one of the step's compute streams (sdmi/streams.py; SDMI_NATIVE_COMM=0: torch.distributed).
+
 wire="bf16" (off by default; SDMI_GRAD_WIRE=bf16 in the trainer) sends each bucket as bf16: half the bytes on the
 xGMI links, at the cost of bf16 rounding of every rank's gradient and of the ring's partial sums (the reference's DDP
 averages fp32 gradients). The fp32 bucket is rounded into a persistent bf16 staging buffer by a HIP kernel on the
 reducer stream (sdmi_cast_bf16), all-reduced, and widened back by a HIP kernel that also produces the bucket's norm
 blocks (sdmi_widen_bf16_sumsq): no aten kernel on the exchange path."""
+import ctypes
 import math
+import os
 
 import torch
 import torch.distributed as dist
 
+from . import _lib
 from . import plan
+from . import streams
 
 CPU_NORM_BLOCK = 1 << 17  # CPU (gloo test) tensors: the same block size as csrc/optim.hip NORM_BLK
 
@@ -93,8 +102,49 @@ class NormBlocks:
         self.launch(g, 0, self.numel)
 
 
+def rccl_path():
+    """The RCCL shared library torch itself uses (one RCCL in the process), else the system's."""
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "librccl.so"
+
+
+class NativeComm:
+    """An RCCL communicator owned by libsdmi over the ranks of `group` (rank 0's unique id broadcast through the
+    group), used for in-place SUM all-reduces on a given stream (sdmi_allreduce)."""
+
+    def __init__(self, group, device):
+        lib = _lib.lib()
+        _lib.check(lib.sdmi_comm_load(rccl_path().encode()), "sdmi_comm_load")
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        uid = (ctypes.c_ubyte * 128)()
+        if self.rank == 0:
+            _lib.check(lib.sdmi_comm_unique_id(uid), "sdmi_comm_unique_id")
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = (ctypes.c_ubyte * 128).from_buffer_copy(box[0])
+        h = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            _lib.check(lib.sdmi_comm_init(uid, self.world, self.rank, ctypes.byref(h)), "sdmi_comm_init")
+        self.handle = h
+
+    def all_reduce(self, buf, stream):
+        dt = {torch.float32: 0, torch.bfloat16: 1}[buf.dtype]
+        _lib.check(_lib.lib().sdmi_allreduce(self.handle, buf.data_ptr(), buf.numel(), dt, stream.cuda_stream),
+                   "sdmi_allreduce")
+
+    def __del__(self):
+        import sys
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and not sys.is_finalizing():  # (at exit the process ends the communicator)
+            try:
+                _lib.lib().sdmi_comm_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
 class BucketReducer:
-    def __init__(self, flat, group=None, bucket_bytes=64 << 20, wire="fp32", norm=None):
+    def __init__(self, flat, group=None, bucket_bytes=64 << 20, wire="fp32", norm=None, stream=None):
         if wire not in ("fp32", "bf16"):
             raise ValueError(f"gradient wire format {wire!r}: fp32 or bf16")
         self.flat = flat
@@ -106,9 +156,14 @@ class BucketReducer:
             self.bucket = max(norm.blk, (self.bucket + norm.blk - 1) // norm.blk * norm.blk)
         self.total = flat.numel()
         self.cuda = flat.is_cuda
-        self.stream = torch.cuda.Stream(device=flat.device) if self.cuda else None
+        # stream: an existing stream idle during the backward (the engine's context stream) to run on, so the step
+        # does not add one more stream to the few hardware queues a process gets
+        self.stream = (stream or streams.new_stream(flat.device)) if self.cuda else None
         self.wire_buf = torch.empty(self.total, dtype=torch.bfloat16, device=flat.device) if wire == "bf16" else None
         self.producers = []  # extra streams that write gradients (the engine's weight-gradient stream)
+        self.comm = (NativeComm(group, flat.device)
+                     if self.cuda and dist.get_backend(group) == "nccl" and os.environ.get("SDMI_NATIVE_COMM", "1") != "0"
+                     else None)
         self.reset()
 
     def reset(self):
@@ -119,6 +174,9 @@ class BucketReducer:
 
     def _issue(self, i, lo, hi):
         """all-reduce of bucket i on the reducer stream (the unit a recorded StepPlan re-issues as a callout)."""
+        if self.comm is not None:
+            self.comm.all_reduce(self.wire_buf[lo:hi] if self.wire == "bf16" else self.flat[lo:hi], self.stream)
+            return
         if self.cuda:
             with torch.cuda.stream(self.stream):
                 self._issue_on(i, lo, hi)
@@ -140,7 +198,8 @@ class BucketReducer:
 
     def _complete(self, i, lo, hi):
         """after bucket i's all-reduce: widen (bf16 wire) and the bucket's norm blocks, on the reducer stream."""
-        plan.record(self._wait, i)
+        if self.comm is None:  # (native: the collective ran on the reducer stream itself)
+            plan.record(self._wait, i)
         if self.wire == "bf16":
             if self.norm is not None:
                 self.norm.widen(self.wire_buf, self.flat, lo, hi, self.stream)
@@ -169,7 +228,10 @@ class BucketReducer:
                 self.wire_buf[lo:hi].copy_(self.flat[lo:hi])
         i = self.nb
         self.nb += 1
-        plan.record(self._issue, i, lo, hi)
+        if self.comm is not None:  # recorded into a plan by the library itself
+            self._issue(i, lo, hi)
+        else:
+            plan.record(self._issue, i, lo, hi)
         # the previous bucket completes behind this one's issue, so its widening / norm overlaps this collective
         while self.pending:
             j, jlo, jhi = self.pending.pop(0)

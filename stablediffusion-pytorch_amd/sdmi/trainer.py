@@ -18,6 +18,7 @@ import torch.distributed as dist
 from . import _lib
 from . import kernels as K
 from . import plan
+from . import streams
 from .reducer import BucketReducer, NormBlocks
 from .store import FlatStore, param_label, unet_gemm_natural
 from .unet_engine import UNetEngine
@@ -44,11 +45,11 @@ class NormParts:
     them in block order: bitwise the norm of one whole-buffer pass (sdmi_clip_unscale) and of the data-parallel
     reducer's per-bucket pieces."""
 
-    def __init__(self, grads, numel, producers=(), chunk_elems=16 << 20):
+    def __init__(self, grads, numel, producers=(), chunk_elems=16 << 20, stream=None):
         self.g, self.numel = grads, numel
         self.chunk = chunk_elems
         self.producers = list(producers)
-        self.stream = torch.cuda.Stream(device=grads.device)
+        self.stream = stream or streams.new_stream(grads.device)
         self.blocks = NormBlocks(numel, grads.device)
         self.reset()
 
@@ -132,7 +133,10 @@ class DDPMTrainer:
         # the reducer also produces the gradient norm: each bucket's block partials right after its all-reduce
         self.red_norm = (NormBlocks(self.store.numel, self.device)
                          if (self.world > 1 or force_reducer) and self.device.type == "cuda" else None)
-        self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes, wire=self.grad_wire, norm=self.red_norm)
+        red_stream = (getattr(self.engine, "ctx_stream", None)
+                      if os.environ.get("SDMI_RED_STREAM", "ctx") == "ctx" else None)
+        self.reducer = (BucketReducer(self.store.grads, group, bucket_bytes, wire=self.grad_wire, norm=self.red_norm,
+                                      stream=red_stream)
                         if self.world > 1 or force_reducer else None)
         self.tail_events = None  # (after backward, after the all-reduce drain): set by measure_exchange_tail()
         # one GPU: the gradient norm in pieces overlapped with the backward.
@@ -140,7 +144,9 @@ class DDPMTrainer:
         self.norm_parts = None
         if self.world == 1 and self.reducer is None and self.device.type == "cuda":
             self.norm_parts = NormParts(self.store.grads, self.store.numel,
-                                        getattr(self.engine, "sides", None) or [])
+                                        getattr(self.engine, "sides", None) or [],
+                                        stream=(getattr(self.engine, "ctx_stream", None)
+                                                if os.environ.get("SDMI_NORM_STREAM", "ctx") == "ctx" else None))
         if self.reducer is not None and getattr(self.engine, "side", None) is not None:
             self.reducer.producers.extend(getattr(self.engine, "sides", None) or [self.engine.side])
         self._progress = None

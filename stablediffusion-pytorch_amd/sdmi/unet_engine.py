@@ -24,6 +24,7 @@ import torch
 from . import _lib
 from . import kernels as K
 from . import plan
+from . import streams
 
 # GroupNorm-backward statistics from the producing data-gradient GEMM: used where a sample has >= GN_FUSE_MIN_P pixels
 # (the 32^2 level of the CelebHQ latents). Same-box A/B of the cond-UNet step (scripts/gpu_bisect.sh): every level
@@ -326,14 +327,14 @@ class UNetEngine:
         # weight-gradient work (wgrad GEMMs, bias sums) runs on a side stream, overlapped with the
         # data-gradient chain of the backward on the current stream
         use_side = self.device.type == "cuda" and not single_stream
-        self.side = torch.cuda.Stream(device=self.device) if use_side else None
+        self.side = streams.new_stream(self.device) if use_side else None
         # the weight-gradient blocks go round-robin over two side streams (the first is self.side, which also runs the
         # optimizer chunks), so independent small weight-gradient GEMMs overlap each other as well as the
         # data-gradient chain (measured 1 / 2 / 3 / 4 streams: 15.3-15.7 / 15.04-15.09 / 15.2 / 15.1-15.2 ms/step)
-        self.sides = [self.side, torch.cuda.Stream(device=self.device)] if use_side else []
+        self.sides = [self.side, streams.new_stream(self.device)] if use_side else []
         self._wg_next = 0
         # the cross-attention context branch runs ahead of the forward on a stream of its own
-        self.ctx_stream = torch.cuda.Stream(device=self.device) if use_side else None
+        self.ctx_stream = streams.new_stream(self.device) if use_side else None
         self._keep = []
         # linear data gradients from transposed packed weights: B_NK GEMMs, which the deep-ring 64-row mainloops of
         # the 8^2 / 4^2 levels take (round 2, before those mainloops: +0.04 ms/step; round 4 with the shapes tuned:

@@ -18,6 +18,7 @@ import torch.distributed as dist
 from . import _lib
 from . import kernels as K
 from . import plan
+from . import streams
 from .store import FlatStore
 from .unet_engine import Grads, PackPlan, Tape, UNetEngine
 from .vqvae_engine import vqvae_layout
@@ -49,7 +50,7 @@ class VQVAETrainEngine(UNetEngine):
         self.cin_pad = (im_channels + 7) // 8 * 8
         self.temb_off = {}  # no time embedding anywhere (blocks built with t_emb_dim=None)
         self.temb_total = 0
-        self.side = torch.cuda.Stream(device=self.device) if self.device.type == "cuda" else None
+        self.side = streams.new_stream(self.device) if self.device.type == "cuda" else None
         self.sides = [self.side] if self.side is not None else []  # the UNet engine's _wg / _join round-robin
         self._wg_next = 0
         self._keep = []

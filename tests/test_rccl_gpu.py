@@ -2,7 +2,8 @@
 BucketReducer forced on, the step recorded once by sdmi.plan.StepPlan and replayed. The bucket all-reduces run
 through RCCL on the reducer stream between the backward's gradient producers and the optimizer; with one rank
 they are identities, so parameters, Adam moments, EMA and GradScaler state must be bit-identical to a trainer
-without a reducer fed the same inputs."""
+without a reducer fed the same inputs. Both issue paths: the library's own RCCL communicator (native plan ops,
+csrc/comm.hip) and torch.distributed callouts (SDMI_NATIVE_COMM=0)."""
 import os
 import socket
 
@@ -33,8 +34,8 @@ def _inputs(step, B=2):
     return [v.cuda() for v in (x0, noise, t, text, mask)]
 
 
-def _worker(rank, port, out):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, port, out, native):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SDMI_NATIVE_COMM=native)
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from oracle import sd_oracle as O
@@ -45,6 +46,7 @@ def _worker(rank, port, out):
     red = DDPMTrainer(SMALL_COND, sd, "cuda", lr=1e-3, group=dist.group.WORLD, force_reducer=True,
                       bucket_bytes=1 << 20)
     assert red.reducer is not None and red.world == 1
+    assert (red.reducer.comm is not None) == (native == "1")
     ref = DDPMTrainer(SMALL_COND, sd, "cuda", lr=1e-3)
     bufs = [torch.empty_like(v) for v in _inputs(0)]
     plan = None
@@ -63,14 +65,18 @@ def _worker(rank, port, out):
           and torch.equal(red.v, ref.v) and torch.equal(red.ema, ref.ema) and torch.equal(red.state, ref.state))
     out["ok"] = ok
     out["collectives"] = plan.collectives()
+    out["reducer_callouts"] = sum(1 for fn, _ in plan.ops if getattr(fn, "__name__", "") in ("_issue", "_wait"))
     out["backend"] = dist.get_backend()
     dist.destroy_process_group()
 
 
-def test_rccl_bucket_allreduce_in_replayed_plan():
+@pytest.mark.parametrize("native", ["1", "0"])
+def test_rccl_bucket_allreduce_in_replayed_plan(native):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(_port(), out), nprocs=1, join=True)
+    mp.spawn(_worker, args=(_port(), out, native), nprocs=1, join=True)
     assert out["backend"] == "nccl"
     assert out["collectives"] >= 2  # the flat gradient buffer went out in more than one bucket
+    if native == "1":
+        assert out["reducer_callouts"] == 0  # the exchange replays natively
     assert out["ok"]
