@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--timeline-steps", type=int, default=2)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from sdmi import streams
+    streams.reserve(dev)  # as bench.py: the engines' streams on queues of their own
     cap = make(a.workload, dev)
     for _ in range(3):
         cap.step()
