@@ -756,7 +756,9 @@ def main():
         result["forced_reducer"] = {
             "note": "N = 1 with the N > 1 gradient path on: RCCL group of one rank, bucketed all-reduce on the reducer "
                     "stream (identities at one rank), per-bucket norm blocks; compare ms_per_step with the plain line",
-            "backend": dist.get_backend(), "bucket_bytes": trainer.reducer.bucket * trainer.store.grads.element_size()}
+            "backend": dist.get_backend(), "bucket_bytes": trainer.reducer.bucket * trainer.store.grads.element_size(),
+            "issue": ("library RCCL communicator, native plan ops (csrc/comm.hip)" if trainer.reducer.comm is not None
+                      else "torch.distributed callouts")}
         result["config"]["parallelism"] = "dp1 + forced reducer"
     if world > 1 or forced:
         result["collectives"] = collectives

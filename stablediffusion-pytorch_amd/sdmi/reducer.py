@@ -161,9 +161,14 @@ class BucketReducer:
         self.stream = (stream or streams.new_stream(flat.device)) if self.cuda else None
         self.wire_buf = torch.empty(self.total, dtype=torch.bfloat16, device=flat.device) if wire == "bf16" else None
         self.producers = []  # extra streams that write gradients (the engine's weight-gradient stream)
-        self.comm = (NativeComm(group, flat.device)
-                     if self.cuda and dist.get_backend(group) == "nccl" and os.environ.get("SDMI_NATIVE_COMM", "1") != "0"
-                     else None)
+        self.comm = None
+        if self.cuda and dist.get_backend(group) == "nccl" and os.environ.get("SDMI_NATIVE_COMM", "1") != "0":
+            try:
+                self.comm = NativeComm(group, flat.device)
+            except RuntimeError as e:  # RCCL not bindable / init refused: the torch.distributed path, said out loud
+                import sys
+                print(f"sdmi.reducer: library RCCL communicator unavailable ({e}); bucket all-reduces go through "
+                      f"torch.distributed", file=sys.stderr)
         self.reset()
 
     def reset(self):
