@@ -894,6 +894,20 @@ constexpr int dma_min_waves(int ring_bytes) {
   return KG > 1 ? 2 : ((dma_threads<TBM, NWN>() == 256 && ring_bytes <= 80 * 1024) ? 2 : 1);
 }
 
+#ifdef SDMI_GEMM_TRACE
+// Probe build only (scripts/gemm_phase_probe.py): per-workgroup phase timestamps of the LDS-DMA kernel, 100 MHz
+// s_memrealtime -- entry, first k-tile landed, main loop done, epilogue done -- by thread 0, vector stores.
+__device__ unsigned long long g_gemm_trace[1 << 20];
+#define SDMI_TRACE_T(i) \
+  do {                  \
+    if (threadIdx.x == 0) tr_t[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define SDMI_TRACE_T(i) \
+  do {                  \
+  } while (0)
+#endif
+
 template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0, int KBK = BK,
           bool GNE = false, int KG = 1>
 __global__ __launch_bounds__((dma_threads<TBM, NWN>() * KG),
@@ -926,6 +940,10 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   const int kg = wave_all / NW, wave = wave_all - kg * NW;            // k-group, wave within it
   char* const ring = smem + kg * STAGES * (TBM + TBN) * KBK * 2;       // this k-group's LDS ring
   const int wm = (wave / NWN) * 64, wn = (wave % NWN) * WTN;
+#ifdef SDMI_GEMM_TRACE
+  unsigned long long tr_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  SDMI_TRACE_T(0);
   const TileId tl = tile_id<TBN, TBM>();
   const int m0 = tl.m0, n0 = tl.n0;
   const int grp = g.ngroups > 1 ? tl.z / g.nsplit : 0;  // grouped launch: problem index, then the split within it
@@ -1251,6 +1269,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's DMA for tile t done; every wave done with tile t-1
+    if (t == 0) SDMI_TRACE_T(1);
     if (KG > 1 && t >= nt) return;  // this k-group has no tile t (its last barriers only)
     if (t + STAGES - 1 < nt) issue(kt0 + (t + STAGES - 1) * KG + kg, (ST + STAGES - 1) % STAGES);
     const char* ta = ring + ST * STAGE_BYTES;
@@ -1328,7 +1347,9 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
       if constexpr (STAGES > 5) if (t0 + 5 < nt_loop) step(t0 + 5, IC<5 % STAGES>{});
     }
   }
+  SDMI_TRACE_T(2);
   __syncthreads();
+  SDMI_TRACE_T(4);
   if constexpr (KG > 1) {
     // k-group g > 0 hands its accumulators (and reduction-tile sums) to k-group 0 through LDS, one group after the
     // other in group order: a fixed summation order, so the result does not depend on timing. Lane-linear 16-B slots
@@ -1391,7 +1412,18 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
     }
   }
   // only k-group 0 holds the tile (wm = -1: the other groups' waves stage nothing, but share the stores)
+  SDMI_TRACE_T(5);
   gemm_epilogue<TBN, false, TBM, NJ, NTH, GNE>(*ep, acc, smem, m0, n0, kg == 0 ? wm : -1, wn, lane, z);
+#ifdef SDMI_GEMM_TRACE
+  SDMI_TRACE_T(3);
+  if (threadIdx.x == 0) {
+    const unsigned d = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (d < (1u << 17)) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g_gemm_trace[d * 8 + i] = tr_t[i];
+    }
+  }
+#endif
 }
 
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
@@ -1999,3 +2031,19 @@ extern "C" int sdmi_gemm_grouped(const sdmi_gemm_desc* d, int ngroups, void* wor
   if (!d) return -1;
   return run_gemm(d, ngroups, workspace, ws_bytes, (hipStream_t)stream);
 }
+
+#ifdef SDMI_GEMM_TRACE
+// probe build only: copy the first n_u64 words of the phase-timestamp buffer to host memory (device synchronised)
+extern "C" int sdmi_gemm_trace_clear(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_gemm_trace)) != hipSuccess) return -1;
+  return hipMemset(p, 0, sizeof(g_gemm_trace)) == hipSuccess ? 0 : -2;
+}
+
+extern "C" int sdmi_gemm_trace_copy(void* host_dst, long long n_u64) {
+  if (!host_dst || n_u64 < 0 || n_u64 > (1 << 20)) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_gemm_trace), (size_t)n_u64 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0 : -3;
+}
+#endif

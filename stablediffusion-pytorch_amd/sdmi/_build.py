@@ -36,8 +36,11 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
+def build(force=False, verbose=False, out=None, defines=()):
+    """out / defines: a probe variant of the library (e.g. SDMI_GEMM_TRACE into libsdmi_trace.so), loaded through
+    SDMI_LIB_PATH by scripts only -- never the product library."""
+    lib_out = out or LIB
+    if not force and out is None and not needs_build():
         return LIB
     objs = []
     procs = []
@@ -46,6 +49,7 @@ def build(force=False, verbose=False):
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
                "-I", os.path.join(REPO, "include"), "-Rpass-analysis=kernel-resource-usage"]
         cmd += EXTRA_FLAGS.get(os.path.basename(src), [])
+        cmd += [f"-D{d}" for d in defines]
         procs.append((subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), src, cmd))
         objs.append(obj)
     spills = []
@@ -76,15 +80,15 @@ def build(force=False, verbose=False):
             sys.stderr.write("\n".join(l for l in txt.splitlines() if "remark" not in l))
     if spills:
         raise RuntimeError(f"kernels use scratch memory (register spill / dynamic indexing): {spills}")
-    tmp = LIB + f".tmp{os.getpid()}"
+    tmp = lib_out + f".tmp{os.getpid()}"
     subprocess.check_call(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib_out)
     for o in objs:
         try:
             os.remove(o)
         except OSError:
             pass
-    return LIB
+    return lib_out
 
 
 def source_digest():
@@ -122,5 +126,7 @@ def build_cabi_check():
 if __name__ == "__main__":
     if "--digest" in sys.argv:
         print(source_digest())
+    elif "--trace" in sys.argv:  # the GEMM phase-timestamp probe library (scripts/gemm_phase_probe.py)
+        print(build(force=True, out=os.path.join(HERE, "libsdmi_trace.so"), defines=("SDMI_GEMM_TRACE",)))
     else:
         print(build(force="--force" in sys.argv, verbose=True))
