@@ -80,3 +80,39 @@ def test_rccl_bucket_allreduce_in_replayed_plan(native):
     if native == "1":
         assert out["reducer_callouts"] == 0  # the exchange replays natively
     assert out["ok"]
+
+
+def _wire_worker(rank, port, out):
+    """bf16 gradient wire through RCCL, both issue paths: one rank makes the all-reduce an identity, so the library's
+    communicator (ncclBfloat16) and torch.distributed must leave bitwise the same trainer state."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from oracle import sd_oracle as O
+    from tests.golden.configs import SMALL_COND
+    from sdmi.trainer import DDPMTrainer
+    sd = O.deterministic_state(O.unet_param_shapes(SMALL_COND), seed=4)
+    trs = {}
+    for native in ("1", "0"):
+        os.environ["SDMI_NATIVE_COMM"] = native
+        trs[native] = DDPMTrainer(SMALL_COND, sd, "cuda", lr=1e-3, group=dist.group.WORLD, force_reducer=True,
+                                  bucket_bytes=1 << 20, grad_wire="bf16")
+    assert trs["1"].reducer.comm is not None and trs["0"].reducer.comm is None
+    for s in range(3):
+        inp = _inputs(s)
+        for tr in trs.values():
+            tr.step(*inp)
+    for tr in trs.values():
+        tr.sync_optimizer()
+    torch.cuda.synchronize()
+    a, b = trs["1"], trs["0"]
+    out["ok"] = (torch.equal(a.store.params, b.store.params) and torch.equal(a.m, b.m) and torch.equal(a.v, b.v)
+                 and torch.equal(a.state, b.state))
+    dist.destroy_process_group()
+
+
+def test_rccl_bf16_wire_native_matches_torch_distributed():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_wire_worker, args=(_port(), out), nprocs=1, join=True)
+    assert out["ok"]
