@@ -116,3 +116,46 @@ def test_rccl_bf16_wire_native_matches_torch_distributed():
     out = mgr.dict()
     mp.spawn(_wire_worker, args=(_port(), out), nprocs=1, join=True)
     assert out["ok"]
+
+
+def _dit_worker(rank, port, out):
+    """The DiT trainer (one weight-gradient stream, no context stream: the reducer takes a stream of its own) with the
+    bucket reducer forced on over the library's RCCL communicator, recorded once and replayed: bit-identical to the
+    reducer-free DiT trainer fed the same inputs."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SDMI_NATIVE_COMM="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from oracle import sd_oracle as O, dit_oracle as DO
+    from tests.golden.configs import SMALL_DIT
+    from sdmi.trainer import DDPMTrainer
+    from sdmi.plan import StepPlan
+    sd = O.deterministic_state(DO.dit_param_shapes(SMALL_DIT), seed=5)
+    red = DDPMTrainer(SMALL_DIT, sd, "cuda", base="dit", lr=1e-3, ema_decay=None, group=dist.group.WORLD,
+                      force_reducer=True, bucket_bytes=1 << 18)
+    assert red.reducer is not None and red.reducer.comm is not None
+    ref = DDPMTrainer(SMALL_DIT, sd, "cuda", base="dit", lr=1e-3, ema_decay=None)
+    bufs = [torch.empty_like(v) for v in _inputs(0)]
+    plan = None
+    for s in range(4):
+        for b, v in zip(bufs, _inputs(s)):
+            b.copy_(v)
+        ref.step(*bufs)
+        if plan is None:
+            plan = StepPlan(lambda: red.step(*bufs))
+        else:
+            plan.replay()
+    red.sync_optimizer()
+    ref.sync_optimizer()
+    torch.cuda.synchronize()
+    out["ok"] = (torch.equal(red.store.params, ref.store.params) and torch.equal(red.m, ref.m)
+                 and torch.equal(red.v, ref.v) and torch.equal(red.state, ref.state))
+    out["collectives"] = plan.collectives()
+    dist.destroy_process_group()
+
+
+def test_rccl_dit_reducer_in_replayed_plan():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_dit_worker, args=(_port(), out), nprocs=1, join=True)
+    assert out["collectives"] >= 2
+    assert out["ok"]
