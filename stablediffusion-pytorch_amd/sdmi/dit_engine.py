@@ -14,6 +14,7 @@ HIP kernels of libsdmi.so, planned for MI355X:
 Parameters are referenced by the reference's state-dict keys; gradients go to caller-owned fp32 views.
 """
 import contextlib
+import os
 
 import torch
 
@@ -194,6 +195,10 @@ class DiTEngine:
             self._pos[key] = position_embedding(self.L["D"], gh, gw).to(torch.bfloat16).to(self.device)
         return self._pos[key]
 
+    # residual stream (and its gradient) dtype: fp32, or bf16 as the reference's autocast keeps it
+    # (SDMI_DIT_STREAM=bf16; Model_DiT_12L_train.py:281-283, 345)
+    SDT = torch.bfloat16 if os.environ.get("SDMI_DIT_STREAM", "fp32") == "bf16" else torch.float32
+
     def _new(self, rows, C, dtype=torch.bfloat16):
         return torch.empty(rows, C, dtype=dtype, device=self.device)
 
@@ -246,7 +251,7 @@ class DiTEngine:
         st.update(xin=xin, mask=m, keep=mask_keep)
         # the residual stream is kept in fp32 (the reference's autocast stream is bf16; fp32 is strictly closer
         # to its fp32 forward and costs only row-kernel bandwidth -- the stream is never a GEMM operand)
-        tok = self._new(M, D, torch.float32)
+        tok = self._new(M, D, self.SDT)
         g = K.conv_geom(H, W, self.cpad, self.cpad, p, p, gh, gw, p, p, 0, 0)
         K.gemm(M, D, p * p * self.cpad, xin, _lib.A_CONV, 0, self.W("pe"), _lib.B_NK, p * p * self.cpad, tok, D,
                geom=g, bias=P["patch_embed_layer.patch_embed.0.bias"], rowbias=self.pos_table(gh, gw), rb_ld=D,
@@ -302,7 +307,7 @@ class DiTEngine:
                 xl = xs
                 self._ln_fwd(xs, y1, m1, r1, shift=mcol(i, 0), scale=mcol(i, 1), N=N)
             else:
-                xl = self._new(M, D, torch.float32)
+                xl = self._new(M, D, self.SDT)
                 self._ln_fwd(xs, y1, m1, r1, v=pend[0], gate=pend[1], xo=xl, shift=mcol(i, 0), scale=mcol(i, 1), N=N)
             qkv = self._new(M, 3 * A)
             K.linear(y1, self.W(q + "attn_block.qkv_proj.weight"), qkv, bias=P[q + "attn_block.qkv_proj.bias"])
@@ -311,11 +316,11 @@ class DiTEngine:
             v1 = self._new(M, D)
             K.linear(o, self.W(q + "attn_block.output_proj.0.weight"), v1, bias=P[q + "attn_block.output_proj.0.bias"])
             c.update(xl=xl, y1=y1, m1=m1, r1=r1, qkv=qkv, o=o, lse=lse, v1=v1)
-            x2, y2 = self._new(M, D, torch.float32), self._new(M, D)
+            x2, y2 = self._new(M, D, self.SDT), self._new(M, D)
             m2, r2 = self._new(M, 1, torch.float32), self._new(M, 1, torch.float32)
             if L["text"]:
                 # out = x + gate*attn ; out = out + cross_attn(LN(out), ctx_proj) (ungated, transformer_layer.py:93-102)
-                xc, yc = self._new(M, D, torch.float32), self._new(M, D)
+                xc, yc = self._new(M, D, self.SDT), self._new(M, D)
                 mc, rc = self._new(M, 1, torch.float32), self._new(M, 1, torch.float32)
                 self._ln_fwd(xl, yc, mc, rc, v=v1, gate=mcol(i, 2), xo=xc, N=N)
                 S = st["S"]
@@ -343,7 +348,7 @@ class DiTEngine:
             xs, pend = x2, (v2, mcol(i, 5))
         # ---- final adaLN-modulated norm + proj_out (transformer.py:203-207) ----
         of = 6 * D * L["n_layers"]
-        xf, yf = self._new(M, D, torch.float32), self._new(M, D)
+        xf, yf = self._new(M, D, self.SDT), self._new(M, D)
         mf, rf = self._new(M, 1, torch.float32), self._new(M, 1, torch.float32)
         self._ln_fwd(xs, yf, mf, rf, v=pend[0], gate=pend[1], xo=xf, shift=mod[:, of:of + D],
                      scale=mod[:, of + D:of + 2 * D], N=N)
@@ -478,7 +483,7 @@ class DiTEngine:
         dy = self._new(M, D)
         K.linear_dgrad(dpred, self.W("proj_out.weight"), dy)
         of = 6 * D * L["n_layers"]
-        dxs = self._new(M, D, torch.float32)  # gradient of the fp32 residual stream, updated in place
+        dxs = self._new(M, D, self.SDT)  # gradient of the residual stream, updated in place
         dv2 = self._new(M, D)
         last = st["layers"][-1]
         self._ln_bwd(st["xf"], st["mf"], st["rf"], dy, dxs, scale=mod[:, of + D:of + 2 * D], psh=ws[:, of:],
