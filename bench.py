@@ -221,6 +221,68 @@ def _cpu_result(per, ts, threads, what):
                        f"{', '.join(f'{t:.2f}' for t in ts)}), torch CPU {torch.__version__} with {threads} threads")
 
 
+def gemm_roofline(prof, PROF_STEPS, workload):
+    """Dominant-kernel roofline from PROF_STEPS profiled steps' sdmi GEMM launches (K.PROFILE records: HIP events on
+    the launch's own stream): the kernel instantiation with the largest event time, its achieved TFLOP/s over its
+    unsplit launches (or all of them, each then including its split-K reducer), algorithmic bytes per launch, and the
+    HBM traffic per launch from the committed rocprofv3 --pmc evidence of this workload."""
+    by, per_kernel = {}, {}
+    for tag, fl, e0, e1, sp in prof:
+        if not tag.startswith("gemm"):
+            continue
+        ms = e0.elapsed_time(e1)
+        a = by.setdefault(tag, [0.0, 0.0, 0])
+        a[0] += fl
+        a[1] += ms
+        a[2] += 1
+        kern = kernel_name(tag, sp)
+        split = int(re.search(r"splits=(\d+)", sp).group(1)) > 1
+        k = per_kernel.setdefault(kern, {"fl": 0.0, "ms": 0.0, "n": 0, "fl1": 0.0, "ms1": 0.0, "n1": 0, "mode": tag,
+                                         "by": 0.0, "by1": 0.0})
+        nb = re.search(r"bytes=(\d+)", sp)
+        nb = float(nb.group(1)) if nb else 0.0
+        k["fl"] += fl
+        k["ms"] += ms
+        k["n"] += 1
+        k["by"] += nb
+        if not split:  # the event brackets the kernel alone (split launches add a reducer launch)
+            k["fl1"] += fl
+            k["ms1"] += ms
+            k["n1"] += 1
+            k["by1"] += nb
+    tot_fl = sum(v[0] for v in by.values())
+    tot_ms = sum(v[1] for v in by.values())
+    dname, d = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
+    # the unsplit launches (events bracket the kernel alone) represent the kernel when they carry most of its work;
+    # otherwise (e.g. DiT weight gradients, whose few unsplit launches are the tiny t-emb GEMMs) all launches count,
+    # each event then including its split-K reducer (a lower bound on the kernel's own rate)
+    use1 = d["n1"] > 0 and d["fl1"] >= 0.5 * d["fl"]
+    dfl, dms, dn, dby = (d["fl1"], d["ms1"], d["n1"], d["by1"]) if use1 else (d["fl"], d["ms"], d["n"], d["by"])
+    traffic, traffic_src = pmc_traffic(workload, dname, use1)
+    algo = dby / dn if dn else None  # algorithmic bytes per launch (sdmi.kernels.algo_bytes over the same launches)
+    return {"kernel_id": dname, "launch_set": "unsplit" if use1 else "all",
+            "bound": "mfma", "kernel": f"sdmi {dname} ({d['mode']}: implicit-GEMM conv fwd/dgrad)"
+            if d["mode"] == "gemm_a1b0" else f"sdmi {dname} ({d['mode']})",
+            "achieved": dfl / (dms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
+            "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic,
+            "traffic_unit": traffic_src.get("unit"), "traffic_source": traffic_src,
+            "algorithmic_bytes": algo,
+            "algorithmic_bytes_note": "per launch: unique operand bytes at their dtypes (conv im2col = the gathered "
+                                      "activation), output and fused epilogue reads, averaged over the same launches",
+            "traffic_ratio": traffic / algo if traffic and algo else None,
+            "launches": dn // PROF_STEPS,
+            "launches_note": f"unsplit launches of the kernel per step (HIP events on its stream, {PROF_STEPS} "
+                             "profiled steps averaged)" if use1 else "all launches (each includes its split-K reducer)",
+            "avg_launch_us": dms * 1e3 / dn, "flop_per_launch": dfl / dn,
+            "kernel_ms_per_step": d["ms"] / PROF_STEPS, "kernel_launches_per_step": d["n"] // PROF_STEPS,
+            "all_gemm": {"tflops": tot_fl / (tot_ms * 1e-3) / 1e12, "ms_per_step": tot_ms / PROF_STEPS,
+                         "launches": sum(v[2] for v in by.values()) // PROF_STEPS},
+            "per_mode": {k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms": v[1] / PROF_STEPS,
+                             "launches": v[2] // PROF_STEPS} for k, v in by.items()},
+            "per_kernel": {k: {"tflops": v["fl"] / (v["ms"] * 1e-3) / 1e12, "ms": v["ms"] / PROF_STEPS,
+                               "launches": v["n"] // PROF_STEPS} for k, v in per_kernel.items()}}
+
+
 def cpu_baseline_dit(cfg, B=32):
     """The DiT oracle's fp32 training step (Model_DiT_12L_train.py:300-375) on the host cores."""
     from oracle import sd_oracle as O, dit_oracle as DO
@@ -330,12 +392,13 @@ def main_vqvae(args, wl, world, rank, device):
         elapsed = e.item()
     sps = args.steps / elapsed
     from sdmi import kernels as K
+    PROF_STEPS = 3
     K.PROFILE = []
-    step()
+    for _ in range(PROF_STEPS):
+        step()
     torch.cuda.synchronize()
     prof, K.PROFILE = K.PROFILE, None
-    fl = sum(p[1] for p in prof if p[0].startswith("gemm"))
-    ms = sum(p[2].elapsed_time(p[3]) for p in prof if p[0].startswith("gemm"))
+    roof = gemm_roofline(prof, PROF_STEPS, args.workload)
     result = {"metric": wl["metric"], "value": sps * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
               "warmup": args.warmup, "ms_per_step": 1000.0 / sps, "higher_is_better": True, "scaling": "weak",
               "vs_baseline": None, "dtype": "bf16", "data": "synthetic 256x256 images, random-init weights",
@@ -343,9 +406,7 @@ def main_vqvae(args, wl, world, rank, device):
                          "per_gpu_batch": B, "image": [3, 256, 256], "latent": [4, 32, 32],
                          "parallelism": f"replicas{world}"},
               "images_per_s": sps * B * world, "model_flops_utilization": wl["flop"] * sps / PEAK_BF16,
-              "roofline": {"bound": "mfma", "kernel": "sdmi gemm_kernel (all implicit-GEMM conv launches of one step)",
-                           "achieved": fl / (ms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
-                           "frac": fl / (ms * 1e-3) / PEAK_BF16, "traffic": None, "gemm_ms_per_step": ms}}
+              "roofline": roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_vqvae(cfg)
     if rank == 0:
@@ -402,6 +463,15 @@ def main_vqvae_train(args, wl, world, rank, device):
         elapsed = e.item()
     sps = args.steps / elapsed
     losses = tr.losses()
+    # dominant-kernel roofline: eager steps with the GEMM launches timed by HIP events on their own streams
+    from sdmi import kernels as K
+    PROF_STEPS = 3
+    K.PROFILE = []
+    for _ in range(PROF_STEPS):
+        tr.step(x)
+    torch.cuda.synchronize()
+    prof, K.PROFILE = K.PROFILE, None
+    roof = gemm_roofline(prof, PROF_STEPS, args.workload)
     result = {"metric": wl["metric"], "value": sps * world, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
               "warmup": args.warmup, "ms_per_step": 1000.0 / sps, "higher_is_better": True, "scaling": "weak",
               "vs_baseline": None, "dtype": "bf16", "data": "synthetic 256x256 images, random-init weights",
@@ -410,7 +480,7 @@ def main_vqvae_train(args, wl, world, rank, device):
                          "model": "VQVAE 22.0M", "per_gpu_batch": B, "image": [3, 256, 256], "latent": [4, 32, 32],
                          "parallelism": f"dp{world}", "issue": args.issue},
               "images_per_s": sps * B * world, "model_flops_utilization": wl["flop"] * sps / PEAK_BF16,
-              "last_losses": losses}
+              "last_losses": losses, "roofline": roof}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_vqvae_train(cfg)
     if rank == 0:
@@ -552,7 +622,7 @@ def main():
     # (sdmi/streams.py: HIP binds a stream to a queue at first use, rotating once all four exist)
     if os.environ.get("SDMI_RESERVE_STREAMS", "1") == "1":
         from sdmi import streams
-        streams.reserve(device)
+        streams.reserve(device, n=streams.workload_streams(args.workload, world))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
@@ -675,61 +745,7 @@ def main():
         trainer.measure_exchange_tail(False)
         torch.cuda.synchronize()
         prof, K.PROFILE = K.PROFILE, None
-        by, per_kernel = {}, {}
-        for tag, fl, e0, e1, sp in prof:
-            if not tag.startswith("gemm"):
-                continue
-            ms = e0.elapsed_time(e1)
-            a = by.setdefault(tag, [0.0, 0.0, 0])
-            a[0] += fl
-            a[1] += ms
-            a[2] += 1
-            kern = kernel_name(tag, sp)
-            split = int(re.search(r"splits=(\d+)", sp).group(1)) > 1
-            k = per_kernel.setdefault(kern, {"fl": 0.0, "ms": 0.0, "n": 0, "fl1": 0.0, "ms1": 0.0, "n1": 0, "mode": tag,
-                                             "by": 0.0, "by1": 0.0})
-            nb = re.search(r"bytes=(\d+)", sp)
-            nb = float(nb.group(1)) if nb else 0.0
-            k["fl"] += fl
-            k["ms"] += ms
-            k["n"] += 1
-            k["by"] += nb
-            if not split:  # the event brackets the kernel alone (split launches add a reducer launch)
-                k["fl1"] += fl
-                k["ms1"] += ms
-                k["n1"] += 1
-                k["by1"] += nb
-        tot_fl = sum(v[0] for v in by.values())
-        tot_ms = sum(v[1] for v in by.values())
-        dname, d = max(per_kernel.items(), key=lambda kv: kv[1]["ms"])
-        # the unsplit launches (events bracket the kernel alone) represent the kernel when they carry most of its work;
-        # otherwise (e.g. DiT weight gradients, whose few unsplit launches are the tiny t-emb GEMMs) all launches count,
-        # each event then including its split-K reducer (a lower bound on the kernel's own rate)
-        use1 = d["n1"] > 0 and d["fl1"] >= 0.5 * d["fl"]
-        dfl, dms, dn, dby = (d["fl1"], d["ms1"], d["n1"], d["by1"]) if use1 else (d["fl"], d["ms"], d["n"], d["by"])
-        traffic, traffic_src = pmc_traffic(args.workload, dname, use1)
-        algo = dby / dn if dn else None  # algorithmic bytes per launch (sdmi.kernels.algo_bytes over the same launches)
-        roof = {"kernel_id": dname, "launch_set": "unsplit" if use1 else "all",
-                "bound": "mfma", "kernel": f"sdmi {dname} ({d['mode']}: implicit-GEMM conv fwd/dgrad)"
-                if d["mode"] == "gemm_a1b0" else f"sdmi {dname} ({d['mode']})",
-                "achieved": dfl / (dms * 1e-3) / 1e12, "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
-                "frac": dfl / (dms * 1e-3) / PEAK_BF16, "traffic": traffic,
-                "traffic_unit": traffic_src.get("unit"), "traffic_source": traffic_src,
-                "algorithmic_bytes": algo,
-                "algorithmic_bytes_note": "per launch: unique operand bytes at their dtypes (conv im2col = the gathered "
-                                          "activation), output and fused epilogue reads, averaged over the same launches",
-                "traffic_ratio": traffic / algo if traffic and algo else None,
-                "launches": dn // PROF_STEPS,
-                "launches_note": f"unsplit launches of the kernel per step (HIP events on its stream, {PROF_STEPS} "
-                                 "profiled steps averaged)" if use1 else "all launches (each includes its split-K reducer)",
-                "avg_launch_us": dms * 1e3 / dn, "flop_per_launch": dfl / dn,
-                "kernel_ms_per_step": d["ms"] / PROF_STEPS, "kernel_launches_per_step": d["n"] // PROF_STEPS,
-                "all_gemm": {"tflops": tot_fl / (tot_ms * 1e-3) / 1e12, "ms_per_step": tot_ms / PROF_STEPS,
-                             "launches": sum(v[2] for v in by.values()) // PROF_STEPS},
-                "per_mode": {k: {"tflops": v[0] / (v[1] * 1e-3) / 1e12, "ms": v[1] / PROF_STEPS,
-                                 "launches": v[2] // PROF_STEPS} for k, v in by.items()},
-                "per_kernel": {k: {"tflops": v["fl"] / (v["ms"] * 1e-3) / 1e12, "ms": v["ms"] / PROF_STEPS,
-                                   "launches": v["n"] // PROF_STEPS} for k, v in per_kernel.items()}}
+        roof = gemm_roofline(prof, PROF_STEPS, args.workload)
 
     FLOP = wl["flop"]
     result = {

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of the whole tree (python + libsdmi.so) against the copy in ab_old/ (a previous commit's package and
+# Same-box A/B of the whole tree (python + libsdmi.so) against the copy in abprev/ (a previous commit's package and
 # bench.py, library prebuilt): the GPU suite first, then the headline bench alternating old / new; AB_ENV_NEW adds env
 # settings to extra "new" arms, e.g. AB_ENV_NEW="SDMI_GRAD_WIRE=bf16".
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -8,7 +8,7 @@ if [ "${AB_TESTS:-1}" = 1 ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_ab.log 2>&1
   rc=$?; tail -3 gpurun_out/t_ab.log; [ $rc -eq 0 ] || exit 1
 fi
-rm -rf /tmp/abold && mkdir -p /tmp/abold && cp -r ab_old/stablediffusion-pytorch_amd ab_old/bench.py /tmp/abold/ && cp -r tests oracle profiles /tmp/abold/
+rm -rf /tmp/abold && mkdir -p /tmp/abold && cp -r abprev/stablediffusion-pytorch_amd abprev/bench.py /tmp/abold/ && cp -r tests oracle profiles /tmp/abold/
 ms() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(round(d['ms_per_step'],3))" $1; }
 W=${AB_WORKLOAD:-cond-unet}
 for r in 1 2; do

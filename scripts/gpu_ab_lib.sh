@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of two libraries under the SAME Python tree: ab_old/libsdmi.so (a previous build) vs the tree's, the
+# Same-box A/B of two libraries under the SAME Python tree: abprev/libsdmi.so (a previous build) vs the tree's, the
 # bench alternating old / new per workload (WLS, default cond-unet), two rounds; optional GPU tests first (TESTS) and
 # extra env arms on the new library (ENV1 / ENV2, e.g. ENV1="SDMI_TUNED_GEMM=gpurun_out/t.json").
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
@@ -8,7 +8,7 @@ if [ -n "$TESTS" ]; then
   rc=$?; tail -2 gpurun_out/t_ablib.log; [ $rc -eq 0 ] || exit 1
 fi
 ms() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(round(d['ms_per_step'],3))" $1; }
-OLD=$GRAFT_REPO_ROOT/ab_old/libsdmi.so
+OLD=$GRAFT_REPO_ROOT/abprev/libsdmi.so
 for W in ${WLS:-cond-unet}; do
   for r in 1 2; do
     if [ -e "$OLD" ]; then

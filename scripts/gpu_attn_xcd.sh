@@ -1,9 +1,9 @@
 #!/bin/bash
-# Attention A/B of two libraries (ab_old/libsdmi.so vs the tree's): isolated timing at every shape, then PMC HBM
+# Attention A/B of two libraries (abprev/libsdmi.so vs the tree's): isolated timing at every shape, then PMC HBM
 # traffic (FETCH_SIZE / WRITE_SIZE passes) per attention kernel at the 32^2 d = 24 self-attention (shape 2).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out
 T=${TAG:-attn}
-OLD=$GRAFT_REPO_ROOT/ab_old/libsdmi.so
+OLD=$GRAFT_REPO_ROOT/abprev/libsdmi.so
 for r in 1 2; do
   SDMI_LIB_PATH=$OLD timeout -k 10 120 python -u scripts/attn_bench.py > gpurun_out/${T}_old$r.txt 2>&1 || exit 1
   timeout -k 10 120 python -u scripts/attn_bench.py > gpurun_out/${T}_new$r.txt 2>&1 || exit 1

@@ -16,15 +16,38 @@ def tag(stream, n):
     torch.cuda.synchronize()
 
 
+_HIP = None
+_CUMASK = []  # raw hipStream_t handles this probe created (destroyed by release_cumask_streams)
+
+
 def cu_mask_stream():
-    hip = ctypes.CDLL("libamdhip64.so")
+    global _HIP
+    hip = _HIP = _HIP or ctypes.CDLL("libamdhip64.so")
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
     words = (ncu + 31) // 32
     mask = (ctypes.c_uint32 * words)(*([0xFFFFFFFF] * words))
     s = ctypes.c_void_p()
     rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(words), mask)
     assert rc == 0, rc
+    _CUMASK.append(s.value)
     return torch.cuda.ExternalStream(s.value)
+
+
+def release_cumask_streams(ss):
+    """Round-5 finding (gpurun_out/qp_cumask.log: SIGSEGV in __cxa_finalize after the profiler's finalisation): the
+    CU-masked streams were foreign hipStream_t's wrapped in torch.cuda.ExternalStream and never destroyed, so static
+    teardown ran with them -- and caching-allocator blocks recorded on them -- still live. Drain them, drop every
+    torch reference and the allocator's cached blocks, then hipStreamDestroy each one while the runtime is intact."""
+    import gc
+    for s in ss:
+        s.synchronize()
+    torch.cuda.synchronize()
+    ss.clear()
+    gc.collect()
+    torch.cuda.empty_cache()
+    while _CUMASK:
+        rc = _HIP.hipStreamDestroy(ctypes.c_void_p(_CUMASK.pop()))
+        assert rc == 0, rc
 
 
 def main():
@@ -58,6 +81,9 @@ def main():
             dist.all_reduce(x)
         torch.cuda.synchronize()
         dist.destroy_process_group()
+    if case.endswith("cumask"):
+        release_cumask_streams(ss)
+        print("cu-masked streams destroyed", flush=True)
 
 
 if __name__ == "__main__":

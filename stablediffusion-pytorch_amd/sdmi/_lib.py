@@ -6,7 +6,10 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("SDMI_LIB_PATH") or os.path.join(_HERE, "libsdmi.so")  # override: A/B timing only
+DEFAULT_LIB_PATH = os.path.join(_HERE, "libsdmi.so")
+# SDMI_LIB_PATH: A/B timing of two builds only. It is announced on stderr when it takes effect, and the test suite
+# refuses to run under it (tests/conftest.py), so a leaked variable cannot make the parity tests bind a stale library.
+LIB_PATH = os.environ.get("SDMI_LIB_PATH") or DEFAULT_LIB_PATH
 
 # ---- enums (include/sdmi.h) ----
 A_ROWMAJOR, A_CONV, A_COLMAJOR = 0, 1, 2
@@ -204,6 +207,9 @@ def lib():
         # torch must bring in its HIP runtime first: libsdmi.so's libamdhip64.so.7 dependency then binds
         # to that same (already loaded, same SONAME) runtime instead of loading a second copy.
         import torch  # noqa: F401
+        if os.path.abspath(LIB_PATH) != DEFAULT_LIB_PATH:
+            import sys
+            print(f"sdmi: SDMI_LIB_PATH override in effect, loading {LIB_PATH} (A/B timing only)", file=sys.stderr)
         _lib = _Lib(ctypes.CDLL(LIB_PATH))
     return _lib
 

@@ -106,6 +106,10 @@ class DiTEngine:
         self.Gd = grads
         self.im_channels = im_channels
         self.device = next(iter(params.values())).device
+        # residual stream (and its gradient) dtype, read per engine: fp32 (default), or bf16 as the reference's autocast
+        # keeps it (SDMI_DIT_STREAM=bf16; Model_DiT_12L_train.py:281-283, 345) -- a DIAGNOSTIC only: with the bf16 stream
+        # the DiT-12L forward misses the north star's MSE <= 1e-4 against the fp32 reference
+        self.SDT = torch.bfloat16 if os.environ.get("SDMI_DIT_STREAM", "fp32") == "bf16" else torch.float32
         # weight-gradient GEMMs of the backward run round-robin on side streams, overlapped with the data-gradient
         # chain on the current stream: one side stream (measured 0 / 1 / 2 / 3 streams -> 4.47 / 4.00 / 4.08 / 4.11 ms/step)
         self.sides = [streams.new_stream(self.device)] if self.device.type == "cuda" and not single_stream else []
@@ -195,9 +199,6 @@ class DiTEngine:
             self._pos[key] = position_embedding(self.L["D"], gh, gw).to(torch.bfloat16).to(self.device)
         return self._pos[key]
 
-    # residual stream (and its gradient) dtype: fp32, or bf16 as the reference's autocast keeps it
-    # (SDMI_DIT_STREAM=bf16; Model_DiT_12L_train.py:281-283, 345)
-    SDT = torch.bfloat16 if os.environ.get("SDMI_DIT_STREAM", "fp32") == "bf16" else torch.float32
 
     def _new(self, rows, C, dtype=torch.bfloat16):
         return torch.empty(rows, C, dtype=dtype, device=self.device)
@@ -249,8 +250,8 @@ class DiTEngine:
                      L.get("im_out", 0),
                      xin, self.cpad, mask_keep)
         st.update(xin=xin, mask=m, keep=mask_keep)
-        # the residual stream is kept in fp32 (the reference's autocast stream is bf16; fp32 is strictly closer
-        # to its fp32 forward and costs only row-kernel bandwidth -- the stream is never a GEMM operand)
+        # the residual stream is self.SDT: fp32 by default (the reference's autocast stream is bf16; fp32 is strictly
+        # closer to its fp32 forward and costs only row-kernel bandwidth -- the stream is never a GEMM operand)
         tok = self._new(M, D, self.SDT)
         g = K.conv_geom(H, W, self.cpad, self.cpad, p, p, gh, gw, p, p, 0, 0)
         K.gemm(M, D, p * p * self.cpad, xin, _lib.A_CONV, 0, self.W("pe"), _lib.B_NK, p * p * self.cpad, tok, D,
@@ -455,7 +456,16 @@ class DiTEngine:
             plan.wait_stream(torch.cuda.current_stream(self.device), side)
 
     def backward(self, ctx, dpred, grads=None, on_progress=None):
-        """dpred: bf16 token-major [B*N, p*p*C]. Writes every parameter gradient (fully overwritten)."""
+        """dpred: bf16 token-major [B*N, p*p*C]. Writes every parameter gradient (fully overwritten). on_progress(i)
+        runs once layer i's gradients (and proj_out's) have all been issued."""
+        for i in self.backward_steps(ctx, dpred, grads):
+            if on_progress is not None:
+                on_progress(i)
+
+    def backward_steps(self, ctx, dpred, grads=None):
+        """The backward as a generator: yields layer index i once layers i..L-1 and proj_out are final (their grouped
+        weight gradients issued); the adaLN / t_proj / patch-embedding tail and the side-stream join run when it is
+        exhausted (sdmi.module_glue.StagedBackward drives it segment by segment)."""
         if grads is not None:
             self.Gd = grads
         assert self.Gd is not None, "engine built without gradient buffers"
@@ -553,8 +563,8 @@ class DiTEngine:
             # layers in one launch each); the layers are reported final only once their gradients are issued
             if self._pending_wg and self._flush_after(L["n_layers"] - i):
                 self._flush_wg()
-            if on_progress is not None and not self._pending_wg:
-                on_progress(i)
+            if not self._pending_wg:
+                yield i
         self._flush_wg()
         # ---- adaLN tables of every layer: one reduction, one weight-gradient GEMM ----
         dmod = self._new(B, L["mod_w"])

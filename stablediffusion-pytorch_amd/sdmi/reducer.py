@@ -108,39 +108,109 @@ def rccl_path():
     return p if os.path.exists(p) else "librccl.so"
 
 
+def agree(ok, group, device):
+    """True on every rank iff `ok` holds on every rank of `group` (MIN all-reduce of a flag over the torch group): a
+    decision all ranks take together, so no rank waits in a collective its peers have given up on."""
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item())
+
+
+def allreduce_selfcheck(all_reduce, rank, world, device, n=1031):
+    """One-time correctness check of an in-place SUM all-reduce `all_reduce(buf)` (collective: every rank calls it):
+    an odd-length fp32 and bf16 bucket whose closed-form sum is exact in both types -- rank r contributes (r + 1) * w_i
+    with w_i = 1 + i % 7, the sum is world (world + 1) / 2 * w_i (exact in bf16 up to world 16). A wrong count, dtype,
+    buffer or rank mapping shows up at any world size > 1. Returns this rank's verdict (combine it with agree())."""
+    w = 1.0 + torch.arange(n, device=device, dtype=torch.float32).remainder(7)
+    want = w * (world * (world + 1) / 2)
+    ok = True
+    for dt in (torch.float32, torch.bfloat16):
+        buf = (w * (rank + 1)).to(dt)
+        all_reduce(buf)
+        ok = ok and bool(torch.equal(buf.float(), want.to(dt).float()))
+    return ok
+
+
 class NativeComm:
     """An RCCL communicator owned by libsdmi over the ranks of `group` (rank 0's unique id broadcast through the
-    group), used for in-place SUM all-reduces on a given stream (sdmi_allreduce)."""
+    group), used for in-place SUM all-reduces on a given stream (sdmi_allreduce).
 
-    def __init__(self, group, device):
-        lib = _lib.lib()
-        _lib.check(lib.sdmi_comm_load(rccl_path().encode()), "sdmi_comm_load")
-        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+    create() is the collective constructor the reducer uses: every step of the setup that can fail on one rank alone
+    (binding librccl, rank 0's unique id, the communicator init) is followed by agree() over the torch group, and the
+    finished communicator must pass allreduce_selfcheck() on every rank; otherwise EVERY rank gets None and the
+    bucket all-reduces go through torch.distributed on all of them (never a mix, never a rank left waiting)."""
+
+    def __init__(self, handle, rank, world, lib=None):
+        self.handle, self.rank, self.world = handle, rank, world
+        self.lib = lib or _lib.lib()
+
+    @classmethod
+    def create(cls, group, device, lib=None):
+        import sys
+        lib = lib or _lib.lib()
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        flag_dev = torch.device(device)
+
+        def say(why):
+            if rank == 0:
+                print(f"sdmi.reducer: library RCCL communicator unavailable ({why}); bucket all-reduces go through "
+                      f"torch.distributed on every rank", file=sys.stderr)
+            return None
+
         uid = (ctypes.c_ubyte * 128)()
-        if self.rank == 0:
-            _lib.check(lib.sdmi_comm_unique_id(uid), "sdmi_comm_unique_id")
+        try:
+            ok = lib.sdmi_comm_load(rccl_path().encode()) == 0
+            if ok and rank == 0:
+                ok = lib.sdmi_comm_unique_id(uid) == 0
+        except Exception:  # noqa: BLE001 -- any local failure becomes this rank's vote
+            ok = False
+        if not agree(ok, group, flag_dev):
+            return say("librccl not bound or no unique id on some rank")
         box = [bytes(uid)]
         dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         uid = (ctypes.c_ubyte * 128).from_buffer_copy(box[0])
         h = ctypes.c_void_p()
-        with torch.cuda.device(device):
-            _lib.check(lib.sdmi_comm_init(uid, self.world, self.rank, ctypes.byref(h)), "sdmi_comm_init")
-        self.handle = h
+        cuda = flag_dev.type == "cuda"
+        try:
+            if cuda:
+                with torch.cuda.device(flag_dev):
+                    ok = lib.sdmi_comm_init(uid, world, rank, ctypes.byref(h)) == 0 and bool(h.value)
+            else:  # (the CPU test of this protocol, with a stand-in library)
+                ok = lib.sdmi_comm_init(uid, world, rank, ctypes.byref(h)) == 0 and bool(h.value)
+        except Exception:  # noqa: BLE001
+            ok = False
+        comm = cls(h if ok else None, rank, world, lib)
+        if not agree(ok, group, flag_dev):
+            comm.close()
+            return say("communicator init failed on some rank")
+        stream = torch.cuda.current_stream(flag_dev) if cuda else None
+        try:
+            ok = allreduce_selfcheck(lambda b: comm.all_reduce(b, stream), rank, world, flag_dev)
+        except RuntimeError:
+            ok = False
+        if not agree(ok, group, flag_dev):
+            comm.close()
+            return say("all-reduce self-check failed on some rank")
+        return comm
 
     def all_reduce(self, buf, stream):
         dt = {torch.float32: 0, torch.bfloat16: 1}[buf.dtype]
-        _lib.check(_lib.lib().sdmi_allreduce(self.handle, buf.data_ptr(), buf.numel(), dt, stream.cuda_stream),
-                   "sdmi_allreduce")
+        _lib.check(self.lib.sdmi_allreduce(self.handle, buf.data_ptr(), buf.numel(), dt,
+                                           stream.cuda_stream if stream is not None else None), "sdmi_allreduce")
+
+    def close(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                self.lib.sdmi_comm_destroy(h)
+            except Exception:  # noqa: BLE001
+                pass
+        self.handle = None
 
     def __del__(self):
         import sys
-        h = getattr(self, "handle", None)
-        if h is not None and h.value and not sys.is_finalizing():  # (at exit the process ends the communicator)
-            try:
-                _lib.lib().sdmi_comm_destroy(h)
-            except Exception:
-                pass
-            self.handle = None
+        if not sys.is_finalizing():  # (at exit the process ends the communicator)
+            self.close()
 
 
 class BucketReducer:
@@ -163,12 +233,8 @@ class BucketReducer:
         self.producers = []  # extra streams that write gradients (the engine's weight-gradient stream)
         self.comm = None
         if self.cuda and dist.get_backend(group) == "nccl" and os.environ.get("SDMI_NATIVE_COMM", "1") != "0":
-            try:
-                self.comm = NativeComm(group, flat.device)
-            except RuntimeError as e:  # RCCL not bindable / init refused: the torch.distributed path, said out loud
-                import sys
-                print(f"sdmi.reducer: library RCCL communicator unavailable ({e}); bucket all-reduces go through "
-                      f"torch.distributed", file=sys.stderr)
+            # collective decision (NativeComm.create): every rank gets the library communicator, or none does
+            self.comm = NativeComm.create(group, flat.device)
         self.reset()
 
     def reset(self):
@@ -234,6 +300,8 @@ class BucketReducer:
         i = self.nb
         self.nb += 1
         if self.comm is not None:  # recorded into a plan by the library itself
+            if plan.KEEP is not None:  # the plan's native op holds the raw communicator: keep its owner alive with it
+                plan.KEEP.append(self.comm)
             self._issue(i, lo, hi)
         else:
             plan.record(self._issue, i, lo, hi)

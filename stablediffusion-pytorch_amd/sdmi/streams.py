@@ -17,6 +17,18 @@ import torch
 
 _RESERVED = {}  # device index -> [streams not yet taken]
 
+# streams each bench workload's step takes through new_stream(), in order. UNet trainer: weight-gradient A / B and the
+# context stream (which also carries the norm pieces or the reducer). DiT trainer: one weight-gradient side stream, then
+# the norm-piece stream (N = 1) or the reducer stream (N > 1). VQVAE trainer: one side stream. Inference workloads
+# (vqvae, sample) run on the null stream only. Reserving more than a workload takes would leave a reserved stream
+# holding one of the four hardware queues, and RCCL's streams would then rotate onto the step's own queues.
+WORKLOAD_STREAMS = {"cond-unet": 3, "uncond-unet": 3, "dit": 2, "vqvae-train": 1, "vqvae": 0, "sample": 0}
+
+
+def workload_streams(workload, world=1):
+    n = WORKLOAD_STREAMS.get(workload, 3)
+    return n + 1 if workload == "vqvae-train" and world > 1 else n  # + its bucket reducer's stream
+
 
 def reserve(device, n=3):
     """First-use the null stream and n fresh streams on `device`, in that order (call before RCCL initialises)."""

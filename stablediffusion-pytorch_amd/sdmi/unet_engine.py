@@ -1210,7 +1210,17 @@ class UNetEngine:
     # ------------------------------------------------------------------------------------------
     def backward(self, ctx, dpred, grads=None, on_progress=None):
         """dpred: NHWC bf16 [B*H*W, 8] (zero in padded channels). Writes every parameter gradient into
-        `grads` ({key: fp32 view}, default: the engine's own) -- each is fully overwritten."""
+        `grads` ({key: fp32 view}, default: the engine's own) -- each is fully overwritten. on_progress(tape, k) runs
+        after tape entry k (going backwards) and, at a block's end, its grouped weight gradients have been issued."""
+        tape = ctx["tape"]
+        for k in self.backward_steps(ctx, dpred, grads):
+            if on_progress is not None:
+                on_progress(tape, k)
+
+    def backward_steps(self, ctx, dpred, grads=None):
+        """The backward as a generator: yields tape position k once entry k (and, when it ends a block, the block's
+        grouped weight gradients) has been issued; the final flush / side-stream join run when it is exhausted. The
+        module path drives it segment by segment from several autograd nodes (sdmi.module_glue.StagedBackward)."""
         if grads is not None:
             self.Gd = grads
         assert self.Gd is not None, "engine built without gradient buffers"
@@ -1236,8 +1246,7 @@ class UNetEngine:
             fn(c, grads)
             if (self._pending_wg or self._pending_gn) and (k == 0 or tape[k - 1][1].get("label") != c.get("label")):
                 self._flush_wg()  # the block's grouped weight gradients, before its gradients are reported final
-            if on_progress is not None:
-                on_progress(tape, k)
+            yield k
         self._flush_wg()
         self._join()
         self._keep = []

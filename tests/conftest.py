@@ -11,6 +11,10 @@ for p in (PKG, REPO):
 
 
 def pytest_configure(config):
+    if os.environ.get("SDMI_LIB_PATH"):
+        # the override exists for A/B timing scripts; parity results must come from the in-tree build
+        raise pytest.UsageError(f"SDMI_LIB_PATH={os.environ['SDMI_LIB_PATH']} is set: the tests run only against the "
+                                "in-tree libsdmi.so (unset it)")
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built libsdmi.so")
     config.addinivalue_line("markers", "slow: long-running CPU test")
 

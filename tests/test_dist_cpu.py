@@ -157,3 +157,62 @@ def test_reducer_norm_pieces_equal_whole_buffer_norm(wire):
         nb, same, _ = out[r]
         assert nb == 6 and same, (r, nb, same)
     assert torch.equal(out[0][2], out[1][2])
+
+
+class _StandInRccl:
+    """Stand-in for libsdmi's RCCL entry points (CPU protocol test of NativeComm.create): `fail` names the entry point
+    that fails on rank `bad`; sdmi_allreduce is an identity (a wrong collective) unless `sum_group` is given, in which
+    case it all-reduces through gloo (a correct one)."""
+
+    def __init__(self, rank, bad, fail, sum_group=None):
+        self.rank, self.bad, self.fail, self.sum_group = rank, bad, fail, sum_group
+        self.destroyed = 0
+
+    def _rc(self, name):
+        return 1 if (name == self.fail and self.rank == self.bad) else 0
+
+    def sdmi_comm_load(self, path):
+        return self._rc("load")
+
+    def sdmi_comm_unique_id(self, uid):
+        uid[0] = 7
+        return self._rc("uid")
+
+    def sdmi_comm_init(self, uid, world, rank, h):
+        h._obj.value = 1 if self._rc("init") == 0 else 0
+        return self._rc("init")
+
+    def sdmi_allreduce(self, h, ptr, n, dt, stream):
+        return 0
+
+    def sdmi_comm_destroy(self, h):
+        self.destroyed += 1
+        return 0
+
+
+def _comm_worker(rank, world, port, fail, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sdmi import reducer as R
+    lib = _StandInRccl(rank, bad=0 if fail == "uid" else world - 1, fail=fail)
+    comm = R.NativeComm.create(None, "cpu", lib=lib)
+    # the self-check on its own: a correct all-reduce passes on every rank, an identity fails on every rank
+    good = R.agree(R.allreduce_selfcheck(lambda b: dist.all_reduce(b), rank, world, "cpu"), None, "cpu")
+    bad = R.agree(R.allreduce_selfcheck(lambda b: None, rank, world, "cpu"), None, "cpu")
+    out[rank] = (comm is None, good, bad)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", ["load", "uid", "init", "selfcheck"])
+def test_native_comm_fallback_is_collective(fail):
+    """the library-communicator decision is taken by all ranks together. A failure on ONE rank (binding
+    librccl, rank 0's unique id, the communicator init, or an all-reduce that does not sum) makes EVERY rank fall
+    back to torch.distributed -- no rank hangs in a broadcast or an init its peers abandoned, no mix of paths."""
+    world = 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    # (fail == "uid" fails on rank 0 -- the only rank that makes an id; "selfcheck": the stand-in's identity
+    # all-reduce is wrong on every rank at world > 1)
+    mp.spawn(_comm_worker, args=(world, _free_port(), fail, out), nprocs=world, join=True)
+    assert all(out[r] == (True, True, False) for r in range(world)), dict(out)
