@@ -63,6 +63,12 @@ struct Args {
   // epilogue's local EpiArgs copy is never indexed dynamically -- that would put it in scratch)
   void* Cg[SDMI_GEMM_GROUP_MAX];
   float* sum_g[SDMI_GEMM_GROUP_MAX];
+  // in-launch split-K combine (FIX instantiations of gemm_dma_kernel, fixup_combine): 1-D grid of 8 x fix_tq x nsplit
+  // workgroups, XCD band x owning tiles [x fix_tq, (x + 1) fix_tq) of the fix_gx-wide tile grid (fix_tiles real tiles),
+  // the slices of one tile consecutive in its XCD's dispatch order; fix_cnt: this stream's arrival counters (one per
+  // tile); fix_sl: the slab lanes of splitk_reduce_n8_kernel for the same launch (its summation order is kept)
+  int fix_tq, fix_gx, fix_tiles, fix_sl;
+  unsigned long long* fix_cnt;
 };
 
 __device__ __forceinline__ void pixel_coords(const Args& g, int m, int& b, int& oy, int& ox) {
@@ -458,6 +464,121 @@ __device__ __forceinline__ EpiArgs epi_args_late() {
   __builtin_memcpy(&r, ka + off, sizeof(EpiArgs));
 #endif
   return r;
+}
+
+// ---- in-launch split-K combine ----------------------------------------------------------------------------------
+// A split-K launch normally writes fp32 slabs [nsplit][M][N] and a second kernel (splitk_reduce_n8_kernel) sums them
+// and applies the epilogue. In the FIX form every slice of a tile, after storing its slab part, waits until all the
+// tile's slices have stored theirs and then combines a 1/nsplit share of the tile's 8-column items itself: no second
+// launch, no launch gap, every slice busy in the combine (the last-arriver combine measured slower in round 3: one
+// workgroup read every slab of its tile alone).
+// Hand-off (MI355X guide, inter-workgroup visibility; cdna_hip_programming.md split-K recipe): write-through (sc1)
+// slab stores -> every wave's vmcnt(0) -> workgroup barrier -> one relaxed agent-scope ticket add per workgroup; the
+// consumer polls the ticket with relaxed agent loads, then one agent-scope acquire + vmcnt(0) + barrier, and reads the
+// slabs with sc1 loads.
+// Progress: a slice waits only for the slices of its own tile, which sit right next to it in its XCD's dispatch
+// sequence (fix_tile below), so at most one tile per XCD and launch is partly dispatched while its first slices wait;
+// the host limits nsplit to FIX_MAX_SPLIT, keeping those waiting slices a small fraction of an XCD's workgroup slots
+// even with the other streams' launches beside it. Every wait is bounded (FIX_TIMEOUT): a launch that would wait
+// longer sets g_fix_err (sdmi_gemm_fix_status) and goes on, so a broken assumption shows up as a failed check, never
+// as a hung GPU.
+// Counters: 64-bit, never reset. Every launch adds exactly FIX_SMAX to each of its tiles' counters (nsplit arrivals,
+// and the last arriver pads the rest), so a slice finds its launch's base as ticket - ticket % FIX_SMAX. Launches
+// that share a counter region run one after another (one region per stream, assigned by the host).
+constexpr unsigned long long FIX_SMAX = 64;
+constexpr int FIX_MAX_SPLIT = 8;
+constexpr int FIX_REGIONS = 32, FIX_REGION_TILES = 4096;
+constexpr unsigned long long FIX_TIMEOUT = 20000000ull;  // s_memrealtime ticks (100 MHz): 200 ms
+__device__ unsigned long long g_fix_cnt[FIX_REGIONS * FIX_REGION_TILES];
+__device__ unsigned g_fix_err;
+
+// the tile and slice of this workgroup in a FIX launch (1-D grid); false for the padding workgroups of the last band
+__device__ __forceinline__ bool fix_tile(const Args& g, int tbm, int tbn, int& m0, int& n0, int& z, int& tile) {
+  const int d = blockIdx.x, i = d >> 3;
+  const int q = i / g.nsplit;
+  tile = (d & 7) * g.fix_tq + q;
+  if (tile >= g.fix_tiles) return false;
+  z = i - q * g.nsplit;
+  const int mt = tile / g.fix_gx;
+  m0 = mt * tbm;
+  n0 = (tile - mt * g.fix_gx) * tbn;
+  return true;
+}
+
+// Combine of a FIX launch, after this workgroup's slab part has been stored (write-through). ev: the launch's epilogue
+// arguments with raw = 0 (the final epilogue, exactly as the reducer applies it). Items of the tile: its rows x its
+// 8-column chunks of the produced columns [n0, n0 + TBN) (and, for column tile 0 of a launch with reduction columns,
+// the reduction chunks [n_x0, N)); slice z takes items [z I / S, (z + 1) I / S). Each item is the sum of the S slabs in
+// splitk_reduce_n8_kernel<fix_sl>'s order (lane l sums slabs l, l + SL, ... from +0; the lanes are added in lane
+// order), so the result is bitwise the two-launch form's.
+template <int TBN, int TBM, int NTH, int RED>
+__device__ __forceinline__ void fixup_combine(const Args& g, const EpiArgs& ev, int m0, int n0, int z, int tile) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
+  __syncthreads();
+  const int S = g.nsplit;
+  if (threadIdx.x == 0) {
+    unsigned long long* c = g.fix_cnt + tile;
+    const unsigned long long t = __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long base = t - t % FIX_SMAX;
+    if (t - base == (unsigned long long)(S - 1))
+      __hip_atomic_fetch_add(c, FIX_SMAX - (unsigned long long)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < base + (unsigned long long)S) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > FIX_TIMEOUT) {
+        __hip_atomic_store(&g_fix_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const int rows = min(TBM, ev.M - m0);
+  const int cch = max(0, min(TBN, ev.n_gemm - n0)) >> 3;
+  const int xch = (RED != 0 && n0 == 0) ? (ev.N - ev.n_x0) >> 3 : 0;
+  const int C = cch + xch;
+  const int I = rows * C;
+  const int i0 = (int)((long long)z * I / S), i1 = (int)((long long)(z + 1) * I / S);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)ev.ws, (short)0, 0x7fffffff, 0x00020000);
+  const int zs = (int)ev.split_stride * 4;
+  const int SL = g.fix_sl;
+#pragma unroll 1
+  for (int i = i0 + (int)threadIdx.x; i < i1; i += NTH) {
+    const int r = i / C, cc = i - r * C;
+    const int row = m0 + r;
+    const int col = cc < cch ? n0 + cc * 8 : ev.n_x0 + (cc - cch) * 8;
+    const int off = (row * ev.N + col) * 4;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+#pragma unroll 1
+    for (int l = 0; l < SL; ++l) {
+      float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
+#pragma unroll 1
+      for (int zz = l; zz < S; zz += SL) {
+        const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + zz * zs, 0, CPOL_SC1));
+        const float4 y =
+            __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + zz * zs + 16, 0, CPOL_SC1));
+        pa.x += x.x; pa.y += x.y; pa.z += x.z; pa.w += x.w;
+        pb.x += y.x; pb.y += y.y; pb.z += y.z; pb.w += y.w;
+      }
+      if (l == 0) {
+        a = pa;
+        b = pb;
+      } else {
+        a.x += pa.x; a.y += pa.y; a.z += pa.z; a.w += pa.w;
+        b.x += pb.x; b.y += pb.y; b.z += pb.z; b.w += pb.w;
+      }
+    }
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    if (ev.n_x0 && col >= ev.n_x0) {
+      Epi::extra(ev, row, col, v, 8);
+    } else if (ev.vec) {
+      if (row < ev.m_store && col < ev.n_store) Epi::finish8(ev, row, col, v);
+    } else {
+#pragma unroll 1
+      for (int e = 0; e < 8; ++e) Epi::store_final(ev, row, col + e, v[e]);
+    }
+  }
 }
 
 // XCD-aware tile order. Workgroups are dispatched round-robin over the 8 XCDs (dispatch id d runs on XCD d % 8,
@@ -909,7 +1030,7 @@ __device__ unsigned long long g_gemm_trace[1 << 20];
 #endif
 
 template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0, int KBK = BK,
-          bool GNE = false, int KG = 1>
+          bool GNE = false, int KG = 1, bool FIX = false>
 __global__ __launch_bounds__((dma_threads<TBM, NWN>() * KG),
                              (dma_min_waves<TBM, NWN, KG>(STAGES * (TBM + TBN) * KBK * 2)))
 void gemm_dma_kernel(const Args g, const EpiArgs e) {
@@ -944,7 +1065,12 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   unsigned long long tr_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   SDMI_TRACE_T(0);
-  const TileId tl = tile_id<TBN, TBM>();
+  TileId tl;
+  if constexpr (FIX) {  // in-launch split-K combine: tile / slice from the 1-D grid (fix_tile)
+    if (!fix_tile(g, TBM, TBN, tl.m0, tl.n0, tl.z, tl.tile)) return;
+  } else {
+    tl = tile_id<TBN, TBM>();
+  }
   const int m0 = tl.m0, n0 = tl.n0;
   const int grp = g.ngroups > 1 ? tl.z / g.nsplit : 0;  // grouped launch: problem index, then the split within it
   const int z = tl.z - grp * g.nsplit;
@@ -1406,14 +1532,25 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
           const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + q;
           if (row >= ep->M) continue;
           const float v = accr[rr][i][q];
-          if (ep->raw) ((float*)ep->ws)[(long long)z * ep->split_stride + (long long)row * ep->N + ep->n_x0 + col] = v;
-          else Epi::extra(*ep, row, ep->n_x0 + col, &v, 1);
+          if (ep->raw) {  // write-through like the tile's slab part (read back in-launch by a FIX combine)
+            const __amdgpu_buffer_rsrc_t rw =
+                __builtin_amdgcn_make_buffer_rsrc((void*)ep->ws, (short)0, 0x7fffffff, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(
+                __float_as_uint(v), rw,
+                (int)(((long long)z * ep->split_stride + (long long)row * ep->N + ep->n_x0 + col) * 4), 0, CPOL_SC1);
+          } else {
+            Epi::extra(*ep, row, ep->n_x0 + col, &v, 1);
+          }
         }
     }
   }
   // only k-group 0 holds the tile (wm = -1: the other groups' waves stage nothing, but share the stores)
   SDMI_TRACE_T(5);
   gemm_epilogue<TBN, false, TBM, NJ, NTH, GNE>(*ep, acc, smem, m0, n0, kg == 0 ? wm : -1, wn, lane, z);
+  if constexpr (FIX) {
+    ev.raw = 0;
+    fixup_combine<TBN, TBM, NTH, RED>(g, ev, m0, n0, z, tl.tile);
+  }
 #ifdef SDMI_GEMM_TRACE
   SDMI_TRACE_T(3);
   if (threadIdx.x == 0) {
@@ -1703,14 +1840,31 @@ hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s)
     }
   }
   if (e.gn_part && !e.raw) return hipErrorInvalidValue;
+  // in-launch split-K combine (Args::fix_tq > 0, set by run_gemm): weight-gradient (col-major A) instantiations only
+  constexpr bool FIXABLE = AM == SDMI_A_COLMAJOR;
+  if (a.fix_tq > 0 && !FIXABLE) return hipErrorInvalidValue;
   if constexpr (KG > 1) {
     // + the k-group hand-off of the accumulators: (4 NJ + 4 RPW) float4 per lane, per wave of one group
     constexpr int NJ = TBN / NWN / 16, RPW = RED == 0 ? 1 : (RED == 1 ? 1 : (3 + NWN - 1) / NWN);
     constexpr size_t xs = (size_t)(4 * NJ + 4 * RPW) * 16 * NTH;
     static_assert(std::max(ring, std::max(epi, xs)) <= 160 * 1024, "LDS");
+    if constexpr (FIXABLE) {
+      if (a.fix_tq > 0) {
+        sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK, false, KG, true>), grid,
+                        dim3(NTH * KG), std::max(ring, std::max(epi, xs)), s, a, e);
+        return hipGetLastError();
+      }
+    }
     sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK, false, KG>), grid, dim3(NTH * KG),
                     std::max(ring, std::max(epi, xs)), s, a, e);
     return hipGetLastError();
+  }
+  if constexpr (FIXABLE) {
+    if (a.fix_tq > 0) {
+      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK, false, 1, true>), grid, dim3(NTH),
+                      std::max(ring, epi), s, a, e);
+      return hipGetLastError();
+    }
   }
   sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid, dim3(NTH), std::max(ring, epi), s,
                   a, e);
@@ -1926,6 +2080,47 @@ extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) 
 }
 
 namespace {
+int g_last_fused = 0;  // the last sdmi_gemm launch used the in-launch split-K combine (sdmi_gemm_last_fused)
+
+// SDMI_SPLITK_FIX=0: every split-K launch keeps its separate reducer launch (A/B timing); sdmi_gemm_fix_enable
+// switches it at run time (tests compare both forms in one process)
+std::atomic<int> g_fix_on{-1};
+bool fix_enabled() {
+  int on = g_fix_on.load(std::memory_order_relaxed);
+  if (on < 0) {
+    const char* v = getenv("SDMI_SPLITK_FIX");
+    on = !(v && v[0] == '0');
+    g_fix_on.store(on, std::memory_order_relaxed);
+  }
+  return on == 1;
+}
+
+// the arrival-counter region of `stream` on the current device: one region per stream (launches on one stream never
+// overlap, so they can share counters), assigned on first use; nullptr once FIX_REGIONS streams hold one
+unsigned long long* fix_region(hipStream_t stream) {
+  static std::atomic<int> lock{0};
+  static hipStream_t keys[64][FIX_REGIONS];
+  static int used[64];
+  static unsigned long long* base[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  while (lock.exchange(1, std::memory_order_acquire)) {
+  }
+  unsigned long long* r = nullptr;
+  if (!base[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fix_cnt)) == hipSuccess) base[dev] = (unsigned long long*)p;
+  }
+  if (base[dev]) {
+    int i = 0;
+    while (i < used[dev] && keys[dev][i] != stream) ++i;
+    if (i == used[dev] && i < FIX_REGIONS) keys[dev][used[dev]++] = stream;
+    if (i < FIX_REGIONS) r = base[dev] + (size_t)i * FIX_REGION_TILES;
+  }
+  lock.store(0, std::memory_order_release);
+  return r;
+}
+
 // descriptors that may share one grouped launch: identical in every field but the operand / output pointers
 bool same_problem_shape(const sdmi_gemm_desc* a, const sdmi_gemm_desc* b) {
   sdmi_gemm_desc x = *a, y = *b;
@@ -1982,6 +2177,25 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
     run.split_stride = slab;
     run.ws_gstride = (long long)splits * slab;
   }
+  // in-launch split-K combine (fixup_combine): weight gradients on the LDS-DMA mainloops, one problem, 16-B slab rows,
+  // no GroupNorm statistics, at most FIX_MAX_SPLIT slices, a counter region for this stream
+  g_last_fused = 0;
+  if (splits > 1 && G == 1 && e.n8 && !e.gn_part && variant != 0 && d->a_mode == SDMI_A_COLMAJOR &&
+      splits <= FIX_MAX_SPLIT && fix_enabled()) {
+    const int tiles = (int)(grid.x * grid.y);
+    unsigned long long* cnt = tiles <= FIX_REGION_TILES ? fix_region(s) : nullptr;
+    if (cnt) {
+      EpiArgs red = e;
+      red.nsplit = splits;
+      a.fix_tq = (tiles + 7) / 8;
+      a.fix_gx = (int)grid.x;
+      a.fix_tiles = tiles;
+      a.fix_sl = reduce_lanes(red);
+      a.fix_cnt = cnt;
+      grid = dim3((unsigned)(8 * a.fix_tq * splits), 1, 1);
+      g_last_fused = 1;
+    }
+  }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
   switch (key) {
@@ -1993,7 +2207,7 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
     default: return -6;
   }
   if (err != hipSuccess) return (int)err;
-  if (splits > 1) {
+  if (splits > 1 && !a.fix_tq) {
     EpiArgs red = e;
     red.raw = 0;
     red.nsplit = splits;
@@ -2006,6 +2220,24 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
   return 0;
 }
 }  // namespace
+
+extern "C" int sdmi_gemm_last_fused(void) { return g_last_fused; }
+
+extern "C" int sdmi_gemm_fix_enable(int on) {
+  const int was = fix_enabled() ? 1 : 0;
+  g_fix_on.store(on ? 1 : 0, std::memory_order_relaxed);
+  return was;
+}
+
+extern "C" int sdmi_gemm_fix_status(int* timed_out) {
+  unsigned v = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_fix_err), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess) return -3;
+  const unsigned zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_fix_err), &zero, sizeof(zero), 0, hipMemcpyHostToDevice) != hipSuccess) return -4;
+  if (timed_out) *timed_out = (int)v;
+  return 0;
+}
 
 extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_bytes, sdmi_stream_t stream) {
   if (!d) return -1;
