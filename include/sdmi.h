@@ -132,16 +132,6 @@ typedef struct sdmi_gemm_desc {
 int sdmi_gemm_kernel_info(const sdmi_gemm_desc* d, int* variant, int* tile_n);
 int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* workspace_bytes);
 int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t workspace_bytes, sdmi_stream_t stream);
-/* Split-K weight gradients (col-major A, LDS-DMA mainloops, <= 8 slices, one problem, no GroupNorm statistics) combine
- * their slices INSIDE the launch: every slice stores its fp32 slab part, waits (bounded) for the other slices of its
- * tile and finishes a 1/splits share of the tile's outputs -- no second reducer launch, bitwise the two-launch result
- * (the reducer's summation order is kept). SDMI_SPLITK_FIX=0 keeps the reducer launch. The workspace is still the
- * sdmi_gemm_plan size. sdmi_gemm_last_fused: 1 if the calling thread's last sdmi_gemm took this form (profiling
- * attribution). sdmi_gemm_fix_status: synchronises the device and reports (and clears) whether any in-launch combine
- * gave up waiting for a slice (*timed_out = 1: its outputs are not valid; never expected). */
-int sdmi_gemm_last_fused(void);
-int sdmi_gemm_fix_enable(int on); /* switch the in-launch combine on (1) / off (0); returns the previous setting */
-int sdmi_gemm_fix_status(int* timed_out);
 
 /* Grouped launch: ngroups (<= SDMI_GEMM_GROUP_MAX) independent problems d[0..ngroups) that are identical in every
  * descriptor field but the a / b / c / sum_out pointers (e.g. the same-shape weight gradients of one UNet block's

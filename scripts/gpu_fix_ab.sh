@@ -10,10 +10,14 @@ if [ "${SUITE:-1}" = 1 ]; then
   tail -1 gpurun_out/t_$TAG.log
 fi
 ms() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(round(d['ms_per_step'],3))" $1; }
+# MODES: SDMI_SPLITK_FIX values to compare (0 = reducer launches, wg / dg / 1 = in-launch combine for weight gradients /
+# forward and data gradients / both); sample = the captured B = 1 DDPM loop (single stream)
 for W in ${WLS:-cond-unet dit}; do
+  EXTRA="--steps 30"
+  [ "$W" = sample ] && EXTRA="--steps 100 --warmup 10"
   for r in 1 2; do
-    for F in 0 1; do
-      SDMI_SPLITK_FIX=$F timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 30 --workload $W > gpurun_out/ab_${TAG}_${W}_f$F$r.log 2>&1 || { tail -5 gpurun_out/ab_${TAG}_${W}_f$F$r.log; exit 1; }
+    for F in ${MODES:-0 1}; do
+      SDMI_SPLITK_FIX=$F timeout -k 10 200 python -u bench.py --no-cpu-baseline $EXTRA --workload $W > gpurun_out/ab_${TAG}_${W}_f$F$r.log 2>&1 || { tail -5 gpurun_out/ab_${TAG}_${W}_f$F$r.log; exit 1; }
       echo "$W fix=$F run$r $(ms gpurun_out/ab_${TAG}_${W}_f$F$r.log) ms"
     done
   done

@@ -63,12 +63,6 @@ struct Args {
   // epilogue's local EpiArgs copy is never indexed dynamically -- that would put it in scratch)
   void* Cg[SDMI_GEMM_GROUP_MAX];
   float* sum_g[SDMI_GEMM_GROUP_MAX];
-  // in-launch split-K combine (FIX instantiations of gemm_dma_kernel, fixup_combine): 1-D grid of 8 x fix_tq x nsplit
-  // workgroups, XCD band x owning tiles [x fix_tq, (x + 1) fix_tq) of the fix_gx-wide tile grid (fix_tiles real tiles),
-  // the slices of one tile consecutive in its XCD's dispatch order; fix_cnt: this stream's arrival counters (one per
-  // tile); fix_sl: the slab lanes of splitk_reduce_n8_kernel for the same launch (its summation order is kept)
-  int fix_tq, fix_gx, fix_tiles, fix_sl;
-  unsigned long long* fix_cnt;
 };
 
 __device__ __forceinline__ void pixel_coords(const Args& g, int m, int& b, int& oy, int& ox) {
@@ -464,121 +458,6 @@ __device__ __forceinline__ EpiArgs epi_args_late() {
   __builtin_memcpy(&r, ka + off, sizeof(EpiArgs));
 #endif
   return r;
-}
-
-// ---- in-launch split-K combine ----------------------------------------------------------------------------------
-// A split-K launch normally writes fp32 slabs [nsplit][M][N] and a second kernel (splitk_reduce_n8_kernel) sums them
-// and applies the epilogue. In the FIX form every slice of a tile, after storing its slab part, waits until all the
-// tile's slices have stored theirs and then combines a 1/nsplit share of the tile's 8-column items itself: no second
-// launch, no launch gap, every slice busy in the combine (the last-arriver combine measured slower in round 3: one
-// workgroup read every slab of its tile alone).
-// Hand-off (MI355X guide, inter-workgroup visibility; cdna_hip_programming.md split-K recipe): write-through (sc1)
-// slab stores -> every wave's vmcnt(0) -> workgroup barrier -> one relaxed agent-scope ticket add per workgroup; the
-// consumer polls the ticket with relaxed agent loads, then one agent-scope acquire + vmcnt(0) + barrier, and reads the
-// slabs with sc1 loads.
-// Progress: a slice waits only for the slices of its own tile, which sit right next to it in its XCD's dispatch
-// sequence (fix_tile below), so at most one tile per XCD and launch is partly dispatched while its first slices wait;
-// the host limits nsplit to FIX_MAX_SPLIT, keeping those waiting slices a small fraction of an XCD's workgroup slots
-// even with the other streams' launches beside it. Every wait is bounded (FIX_TIMEOUT): a launch that would wait
-// longer sets g_fix_err (sdmi_gemm_fix_status) and goes on, so a broken assumption shows up as a failed check, never
-// as a hung GPU.
-// Counters: 64-bit, never reset. Every launch adds exactly FIX_SMAX to each of its tiles' counters (nsplit arrivals,
-// and the last arriver pads the rest), so a slice finds its launch's base as ticket - ticket % FIX_SMAX. Launches
-// that share a counter region run one after another (one region per stream, assigned by the host).
-constexpr unsigned long long FIX_SMAX = 64;
-constexpr int FIX_MAX_SPLIT = 8;
-constexpr int FIX_REGIONS = 32, FIX_REGION_TILES = 4096;
-constexpr unsigned long long FIX_TIMEOUT = 20000000ull;  // s_memrealtime ticks (100 MHz): 200 ms
-__device__ unsigned long long g_fix_cnt[FIX_REGIONS * FIX_REGION_TILES];
-__device__ unsigned g_fix_err;
-
-// the tile and slice of this workgroup in a FIX launch (1-D grid); false for the padding workgroups of the last band
-__device__ __forceinline__ bool fix_tile(const Args& g, int tbm, int tbn, int& m0, int& n0, int& z, int& tile) {
-  const int d = blockIdx.x, i = d >> 3;
-  const int q = i / g.nsplit;
-  tile = (d & 7) * g.fix_tq + q;
-  if (tile >= g.fix_tiles) return false;
-  z = i - q * g.nsplit;
-  const int mt = tile / g.fix_gx;
-  m0 = mt * tbm;
-  n0 = (tile - mt * g.fix_gx) * tbn;
-  return true;
-}
-
-// Combine of a FIX launch, after this workgroup's slab part has been stored (write-through). ev: the launch's epilogue
-// arguments with raw = 0 (the final epilogue, exactly as the reducer applies it). Items of the tile: its rows x its
-// 8-column chunks of the produced columns [n0, n0 + TBN) (and, for column tile 0 of a launch with reduction columns,
-// the reduction chunks [n_x0, N)); slice z takes items [z I / S, (z + 1) I / S). Each item is the sum of the S slabs in
-// splitk_reduce_n8_kernel<fix_sl>'s order (lane l sums slabs l, l + SL, ... from +0; the lanes are added in lane
-// order), so the result is bitwise the two-launch form's.
-template <int TBN, int TBM, int NTH, int RED>
-__device__ __forceinline__ void fixup_combine(const Args& g, const EpiArgs& ev, int m0, int n0, int z, int tile) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores have left
-  __syncthreads();
-  const int S = g.nsplit;
-  if (threadIdx.x == 0) {
-    unsigned long long* c = g.fix_cnt + tile;
-    const unsigned long long t = __hip_atomic_fetch_add(c, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long base = t - t % FIX_SMAX;
-    if (t - base == (unsigned long long)(S - 1))
-      __hip_atomic_fetch_add(c, FIX_SMAX - (unsigned long long)S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < base + (unsigned long long)S) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > FIX_TIMEOUT) {
-        __hip_atomic_store(&g_fix_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  const int rows = min(TBM, ev.M - m0);
-  const int cch = max(0, min(TBN, ev.n_gemm - n0)) >> 3;
-  const int xch = (RED != 0 && n0 == 0) ? (ev.N - ev.n_x0) >> 3 : 0;
-  const int C = cch + xch;
-  const int I = rows * C;
-  const int i0 = (int)((long long)z * I / S), i1 = (int)((long long)(z + 1) * I / S);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)ev.ws, (short)0, 0x7fffffff, 0x00020000);
-  const int zs = (int)ev.split_stride * 4;
-  const int SL = g.fix_sl;
-#pragma unroll 1
-  for (int i = i0 + (int)threadIdx.x; i < i1; i += NTH) {
-    const int r = i / C, cc = i - r * C;
-    const int row = m0 + r;
-    const int col = cc < cch ? n0 + cc * 8 : ev.n_x0 + (cc - cch) * 8;
-    const int off = (row * ev.N + col) * 4;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-#pragma unroll 1
-    for (int l = 0; l < SL; ++l) {
-      float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa;
-#pragma unroll 1
-      for (int zz = l; zz < S; zz += SL) {
-        const float4 x = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + zz * zs, 0, CPOL_SC1));
-        const float4 y =
-            __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + zz * zs + 16, 0, CPOL_SC1));
-        pa.x += x.x; pa.y += x.y; pa.z += x.z; pa.w += x.w;
-        pb.x += y.x; pb.y += y.y; pb.z += y.z; pb.w += y.w;
-      }
-      if (l == 0) {
-        a = pa;
-        b = pb;
-      } else {
-        a.x += pa.x; a.y += pa.y; a.z += pa.z; a.w += pa.w;
-        b.x += pb.x; b.y += pb.y; b.z += pb.z; b.w += pb.w;
-      }
-    }
-    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    if (ev.n_x0 && col >= ev.n_x0) {
-      Epi::extra(ev, row, col, v, 8);
-    } else if (ev.vec) {
-      if (row < ev.m_store && col < ev.n_store) Epi::finish8(ev, row, col, v);
-    } else {
-#pragma unroll 1
-      for (int e = 0; e < 8; ++e) Epi::store_final(ev, row, col + e, v[e]);
-    }
-  }
 }
 
 // XCD-aware tile order. Workgroups are dispatched round-robin over the 8 XCDs (dispatch id d runs on XCD d % 8,
@@ -1030,7 +909,7 @@ __device__ unsigned long long g_gemm_trace[1 << 20];
 #endif
 
 template <int AM, int BMODE, int STAGES, int TBN = BN, int TBM = BM, int NWN = 2, int RED = 0, int KBK = BK,
-          bool GNE = false, int KG = 1, bool FIX = false>
+          bool GNE = false, int KG = 1>
 __global__ __launch_bounds__((dma_threads<TBM, NWN>() * KG),
                              (dma_min_waves<TBM, NWN, KG>(STAGES * (TBM + TBN) * KBK * 2)))
 void gemm_dma_kernel(const Args g, const EpiArgs e) {
@@ -1065,12 +944,7 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
   unsigned long long tr_t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   SDMI_TRACE_T(0);
-  TileId tl;
-  if constexpr (FIX) {  // in-launch split-K combine: tile / slice from the 1-D grid (fix_tile)
-    if (!fix_tile(g, TBM, TBN, tl.m0, tl.n0, tl.z, tl.tile)) return;
-  } else {
-    tl = tile_id<TBN, TBM>();
-  }
+  const TileId tl = tile_id<TBN, TBM>();
   const int m0 = tl.m0, n0 = tl.n0;
   const int grp = g.ngroups > 1 ? tl.z / g.nsplit : 0;  // grouped launch: problem index, then the split within it
   const int z = tl.z - grp * g.nsplit;
@@ -1532,25 +1406,14 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
           const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + q;
           if (row >= ep->M) continue;
           const float v = accr[rr][i][q];
-          if (ep->raw) {  // write-through like the tile's slab part (read back in-launch by a FIX combine)
-            const __amdgpu_buffer_rsrc_t rw =
-                __builtin_amdgcn_make_buffer_rsrc((void*)ep->ws, (short)0, 0x7fffffff, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(
-                __float_as_uint(v), rw,
-                (int)(((long long)z * ep->split_stride + (long long)row * ep->N + ep->n_x0 + col) * 4), 0, CPOL_SC1);
-          } else {
-            Epi::extra(*ep, row, ep->n_x0 + col, &v, 1);
-          }
+          if (ep->raw) ((float*)ep->ws)[(long long)z * ep->split_stride + (long long)row * ep->N + ep->n_x0 + col] = v;
+          else Epi::extra(*ep, row, ep->n_x0 + col, &v, 1);
         }
     }
   }
   // only k-group 0 holds the tile (wm = -1: the other groups' waves stage nothing, but share the stores)
   SDMI_TRACE_T(5);
   gemm_epilogue<TBN, false, TBM, NJ, NTH, GNE>(*ep, acc, smem, m0, n0, kg == 0 ? wm : -1, wn, lane, z);
-  if constexpr (FIX) {
-    ev.raw = 0;
-    fixup_combine<TBN, TBM, NTH, RED>(g, ev, m0, n0, z, tl.tile);
-  }
 #ifdef SDMI_GEMM_TRACE
   SDMI_TRACE_T(3);
   if (threadIdx.x == 0) {
@@ -1561,6 +1424,155 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
     }
   }
 #endif
+}
+
+// ---- persistent streaming GEMM (mainloop variants 12-15) --------------------------------------------------------
+// The short-K GEMMs of the step (K = 128-1536: the UNet's attention projections and 1x1 convolutions, every DiT
+// projection at K = 288 / 1152) ran as ONE lockstep wave of workgroups per launch: operand fill (1.5-2.3 us), a
+// latency-bound main loop of 2-6 k-tiles behind a 2-stage ring, then a synchronized HBM-bound output burst
+// (GEMM phase probe). Here one workgroup per CU walks a sequence of output tiles, and its LDS-DMA
+// ring runs on across tile boundaries: the first k-tiles of the next tile are in flight while the current tile's last
+// MFMAs and its epilogue (staged through an LDS area of its own) run, so the fill latency is paid once per launch
+// and the output stores of one tile overlap the operand loads of the next.
+// A row-major [M][K] (lda), B [N][K] (ldb), K % 8 == 0 (a ragged last k-tile is zero-filled by the buffer
+// descriptor's range check), no split-K, any plain epilogue (bias, row bias, residual, activation, remap; bf16 or
+// fp32 C). TBM x TBN tiles on 4 waves (64 rows x TBN / NWN columns each), STAGES k-tiles of KBK in flight.
+template <int TBM, int TBN, int STAGES, int KBK>
+constexpr size_t stream_lds() {
+  return (size_t)STAGES * (TBM + TBN) * KBK * 2 + (size_t)64 * (TBN + 4) * 4;
+}
+
+template <int TBM, int TBN, int STAGES, int KBK>
+__global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const Args g, const EpiArgs e) {
+  constexpr int NTH = 256, NW = 4;
+  constexpr int NWN = NW / (TBM / 64);  // waves along N (TBM / 64 along M)
+  constexpr int WTN = TBN / NWN, NJ = WTN / 16;
+  constexpr int KS = KBK / 32, RB = KBK * 2, RPI = 1024 / RB, CPR = KBK / 8;
+  constexpr int A_BYTES = TBM * KBK * 2, B_BYTES = TBN * KBK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int A_PW = A_BYTES / 1024 / NW, B_PW = B_BYTES / 1024 / NW, P = A_PW + B_PW;
+  static_assert(KBK == 64 || KBK == 32, "staged k depth");
+  static_assert(TBM == 64 || TBM == 128, "tile rows");
+  static_assert(A_PW * NW * 1024 == A_BYTES && B_PW * NW * 1024 == B_BYTES, "DMA pieces per wave");
+  static_assert(WTN % 16 == 0 && STAGES >= 2, "wave tile / ring");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const ring = smem;                                  // [STAGES][A | B]
+  char* const epi_lds = smem + STAGES * STAGE_BYTES;        // the epilogue's fp32 staging rows
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wave / NWN) * 64, wn = (wave % NWN) * WTN;
+  const int gx = (g.N + TBN - 1) / TBN;
+  const int T = ((g.M + TBM - 1) / TBM) * gx;
+  const int nk = (g.K + KBK - 1) / KBK;
+  // persistent slot -> logical slot, XCD-banded (tile_id's bijection for a 1-D grid): in every round the workgroups of
+  // one XCD take consecutive tiles, i.e. the column tiles of the same A rows share that XCD's L2
+  const int G = gridDim.x, w = blockIdx.x;
+  const int xcd = w & 7, q8 = G >> 3, r8 = G & 7;
+  const int lw = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w >> 3);
+  const int ntiles = lw < T ? (T - lw + G - 1) / G : 0;
+  const int nsteps = ntiles * nk;
+  constexpr int OOB = (int)0x80000000;
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, 0x7fffffff, 0x00020000);
+
+  // per-lane constants of the K-contiguous images: DMA instruction q = wave * PW + j writes 1 KiB, rows q * RPI ..,
+  // lane -> row q * RPI + lane / CPR, physical slot lane % CPR holding logical chunk c (kc_off_k's involution)
+  int a_r[A_PW], a_kk[A_PW], b_r[B_PW], b_kk[B_PW];
+#pragma unroll
+  for (int j = 0; j < A_PW; ++j) {
+    const int r = (wave * A_PW + j) * RPI + lane / CPR;
+    a_r[j] = r;
+    a_kk[j] = ((kc_off_k<KBK>(r, lane % CPR) - r * RB) >> 4) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < B_PW; ++j) {
+    const int r = (wave * B_PW + j) * RPI + lane / CPR;
+    b_r[j] = r;
+    b_kk[j] = ((kc_off_k<KBK>(r, lane % CPR) - r * RB) >> 4) * 8;
+  }
+  // issue cursor: the step (tile round is_r, k-tile is_kt) issued next, and the byte offsets of its tile's rows
+  int is_r = 0, is_kt = 0, is_s = 0;
+  int a_v[A_PW], b_v[B_PW];
+  auto set_issue_tile = [&](int r) __attribute__((always_inline)) {
+    const int tile = lw + r * G, mt = tile / gx;
+    const int m0 = mt * TBM, n0 = (tile - mt * gx) * TBN;
+#pragma unroll
+    for (int j = 0; j < A_PW; ++j) a_v[j] = m0 + a_r[j] < g.M ? ((m0 + a_r[j]) * g.lda + a_kk[j]) * 2 : OOB;
+#pragma unroll
+    for (int j = 0; j < B_PW; ++j) b_v[j] = n0 + b_r[j] < g.N ? ((n0 + b_r[j]) * g.ldb + b_kk[j]) * 2 : OOB;
+  };
+  auto issue_next = [&]() __attribute__((always_inline)) {
+    char* sa = ring + (is_s % STAGES) * STAGE_BYTES;
+    char* sb = sa + A_BYTES;
+    const int k0 = is_kt * KBK;
+    if (k0 + KBK <= g.K) {  // full k-tile: an add per piece (OOB rows stay out of range)
+#pragma unroll
+      for (int j = 0; j < A_PW; ++j) dma16(rsA, sa + (wave * A_PW + j) * 1024, a_v[j] + k0 * 2);
+#pragma unroll
+      for (int j = 0; j < B_PW; ++j) dma16(rsB, sb + (wave * B_PW + j) * 1024, b_v[j] + k0 * 2);
+    } else {  // ragged last k-tile: chunks at k >= K read as zeros
+#pragma unroll
+      for (int j = 0; j < A_PW; ++j)
+        dma16(rsA, sa + (wave * A_PW + j) * 1024, k0 + a_kk[j] < g.K ? a_v[j] + k0 * 2 : OOB);
+#pragma unroll
+      for (int j = 0; j < B_PW; ++j)
+        dma16(rsB, sb + (wave * B_PW + j) * 1024, k0 + b_kk[j] < g.K ? b_v[j] + k0 * 2 : OOB);
+    }
+    ++is_s;
+    if (++is_kt == nk) {
+      is_kt = 0;
+      if (++is_r < ntiles) set_issue_tile(is_r);
+    }
+  };
+
+  f32x4 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (ntiles > 0) set_issue_tile(0);
+#pragma unroll
+  for (int p = 0; p < STAGES - 1; ++p)
+    if (p < nsteps) issue_next();
+  int c_r = 0, c_kt = 0;  // consume cursor
+#pragma unroll 1
+  for (int s = 0; s < nsteps; ++s) {
+    // step s landed for this wave: at most (steps issued after s) x P DMA instructions outstanding. An epilogue's
+    // stores, issued after those, count as younger too: the wait then also covers them (conservative, never early).
+    if (STAGES > 2 && s + STAGES - 2 < nsteps)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((STAGES > 2 ? STAGES - 2 : 0) * P) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for step s done; every wave done reading step s - 1's stage
+    if (s + STAGES - 1 < nsteps) issue_next();
+    const char* ta = ring + (s % STAGES) * STAGE_BYTES;
+    const char* tb = ta + A_BYTES;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      s16x8 fa[4], fb[NJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_kc_k<KBK>(ta, wm + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = frag_kc_k<KBK>(tb, wn + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (++c_kt == nk) {  // tile c_r complete: its epilogue, while the next tile's first k-tiles are in flight
+      const int tile = lw + c_r * G, mt = tile / gx;
+      EpiArgs ev = epi_args_late();
+      gemm_epilogue<TBN, false, TBM, NJ, NTH>(ev, acc, epi_lds, mt * TBM, (tile - mt * gx) * TBN, wm, wn, lane, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      c_kt = 0;
+      ++c_r;
+    }
+  }
 }
 
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
@@ -1769,7 +1781,7 @@ int gemm_variant() {
   if (v == -2) {
     const char* s = getenv("SDMI_GEMM_VARIANT");
     v = s ? atoi(s) : -1;
-    if (v != 0 && (v < 2 || v > 11)) v = -1;
+    if (v != 0 && (v < 2 || v > 15)) v = -1;
   }
   return v;
 }
@@ -1783,7 +1795,11 @@ bool dma_reductions_ok(const sdmi_gemm_desc* d) {
 
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 11) v = d->variant_hint == 1 ? 0 : d->variant_hint;
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 15) v = d->variant_hint == 1 ? 0 : d->variant_hint;
+  // persistent streaming kernel (12-15): row-major A, [n][k] B, plain epilogue, no split-K
+  if (v >= 12 && !(d->a_mode == SDMI_A_ROWMAJOR && d->b_mode == SDMI_B_NK && !has_reductions(d) && !d->gn_part && !d->a2))
+    v = 2;
+  if (v >= 12) return v;
   if (v < 0) v = 2;  // (col-major A with [n][k] B has no DMA instantiation: register staging below)
   if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
   if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
@@ -1799,7 +1815,9 @@ int pick_variant(const sdmi_gemm_desc* d) {
   return v;
 }
 
-int tile_m(const sdmi_gemm_desc*, int variant) { return variant >= 7 && variant <= 10 ? 64 : BM; }
+int tile_m(const sdmi_gemm_desc*, int variant) {
+  return (variant >= 7 && variant <= 10) || variant == 13 || variant == 14 ? 64 : BM;
+}
 
 // columns the grid covers: the DMA kernels compute the reduction columns outside the column tiles
 int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total(d) : d->n; }
@@ -1807,6 +1825,7 @@ int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total
 // Column-tile width: 192 (2-stage DMA, B_NK, N % 192 == 0) when it needs fewer rounds x columns of the
 // 512 workgroup slots (2 per CU) than 128 -- e.g. 32768 x 384: 768 tiles = 1.5 rounds at 128, 512 = 1 at 192.
 int pick_tbn(const sdmi_gemm_desc* d, int variant) {
+  if (variant >= 12) return BN;
   if (variant == 4) return d->n % 384 == 0 ? 384 : 256;
   if (variant == 7) return 64;
   if (variant >= 8 || variant == 6) return BN;  // incl. 11 (k-groups)
@@ -1840,31 +1859,14 @@ hipError_t launch_dma(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s)
     }
   }
   if (e.gn_part && !e.raw) return hipErrorInvalidValue;
-  // in-launch split-K combine (Args::fix_tq > 0, set by run_gemm): weight-gradient (col-major A) instantiations only
-  constexpr bool FIXABLE = AM == SDMI_A_COLMAJOR;
-  if (a.fix_tq > 0 && !FIXABLE) return hipErrorInvalidValue;
   if constexpr (KG > 1) {
     // + the k-group hand-off of the accumulators: (4 NJ + 4 RPW) float4 per lane, per wave of one group
     constexpr int NJ = TBN / NWN / 16, RPW = RED == 0 ? 1 : (RED == 1 ? 1 : (3 + NWN - 1) / NWN);
     constexpr size_t xs = (size_t)(4 * NJ + 4 * RPW) * 16 * NTH;
     static_assert(std::max(ring, std::max(epi, xs)) <= 160 * 1024, "LDS");
-    if constexpr (FIXABLE) {
-      if (a.fix_tq > 0) {
-        sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK, false, KG, true>), grid,
-                        dim3(NTH * KG), std::max(ring, std::max(epi, xs)), s, a, e);
-        return hipGetLastError();
-      }
-    }
     sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK, false, KG>), grid, dim3(NTH * KG),
                     std::max(ring, std::max(epi, xs)), s, a, e);
     return hipGetLastError();
-  }
-  if constexpr (FIXABLE) {
-    if (a.fix_tq > 0) {
-      sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK, false, 1, true>), grid, dim3(NTH),
-                      std::max(ring, epi), s, a, e);
-      return hipGetLastError();
-    }
   }
   sdmi_rt::launch((gemm_dma_kernel<AM, BMODE, STAGES, TBN, TBM, NWN, RED, KBK>), grid, dim3(NTH), std::max(ring, epi), s,
                   a, e);
@@ -1933,6 +1935,37 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, i
     if (a.rowsum) return launch_dma_red<AM, BMODE, 1>(a, e, grid, s, v, tbn);
   }
   return launch_dma_red<AM, BMODE, 0>(a, e, grid, s, v, tbn);
+}
+
+template <int TBM, int TBN, int STAGES, int KBK>
+hipError_t launch_stream_t(const Args& a, const EpiArgs& e, int ctas, hipStream_t s) {
+  constexpr size_t lds = stream_lds<TBM, TBN, STAGES, KBK>();
+  static_assert(lds <= 160 * 1024, "LDS");
+  sdmi_rt::launch((gemm_stream_kernel<TBM, TBN, STAGES, KBK>), dim3((unsigned)ctas), dim3(256), lds, s, a, e);
+  return hipGetLastError();
+}
+
+int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      n = c;
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+// the persistent streaming kernels: one workgroup per CU (their LDS), at most one per tile
+hipError_t launch_stream(const Args& a, const EpiArgs& e, int variant, int tiles, hipStream_t s) {
+  const int ctas = std::min(tiles, cu_count());
+  switch (variant) {
+    case 12: return launch_stream_t<128, 128, 3, 64>(a, e, ctas, s);
+    case 13: return launch_stream_t<64, 128, 5, 64>(a, e, ctas, s);
+    case 14: return launch_stream_t<64, 128, 8, 32>(a, e, ctas, s);
+    case 15: return launch_stream_t<128, 128, 6, 32>(a, e, ctas, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
@@ -2046,6 +2079,7 @@ int plan_splits(const sdmi_gemm_desc* d) {
   const int v = pick_variant(d), tbn = pick_tbn(d, v), tbm = tile_m(d, v);
   const long long tiles = (long long)((d->m + tbm - 1) / tbm) * ((n_grid(d, v) + tbn - 1) / tbn);
   const int nkt = (d->k + BK - 1) / BK;
+  if (v >= 12) return 1;  // the persistent streaming kernel covers the whole K per tile
   if (d->splits_hint > 0) {
     int s = std::min(d->splits_hint, nkt);
     while (s > 1 && (long long)s * d->m * slab_n(d) * 4 >= (1LL << 31)) s >>= 1;
@@ -2080,47 +2114,6 @@ extern "C" int sdmi_gemm_plan(const sdmi_gemm_desc* d, int* splits, size_t* ws) 
 }
 
 namespace {
-int g_last_fused = 0;  // the last sdmi_gemm launch used the in-launch split-K combine (sdmi_gemm_last_fused)
-
-// SDMI_SPLITK_FIX=0: every split-K launch keeps its separate reducer launch (A/B timing); sdmi_gemm_fix_enable
-// switches it at run time (tests compare both forms in one process)
-std::atomic<int> g_fix_on{-1};
-bool fix_enabled() {
-  int on = g_fix_on.load(std::memory_order_relaxed);
-  if (on < 0) {
-    const char* v = getenv("SDMI_SPLITK_FIX");
-    on = !(v && v[0] == '0');
-    g_fix_on.store(on, std::memory_order_relaxed);
-  }
-  return on == 1;
-}
-
-// the arrival-counter region of `stream` on the current device: one region per stream (launches on one stream never
-// overlap, so they can share counters), assigned on first use; nullptr once FIX_REGIONS streams hold one
-unsigned long long* fix_region(hipStream_t stream) {
-  static std::atomic<int> lock{0};
-  static hipStream_t keys[64][FIX_REGIONS];
-  static int used[64];
-  static unsigned long long* base[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  while (lock.exchange(1, std::memory_order_acquire)) {
-  }
-  unsigned long long* r = nullptr;
-  if (!base[dev]) {
-    void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fix_cnt)) == hipSuccess) base[dev] = (unsigned long long*)p;
-  }
-  if (base[dev]) {
-    int i = 0;
-    while (i < used[dev] && keys[dev][i] != stream) ++i;
-    if (i == used[dev] && i < FIX_REGIONS) keys[dev][used[dev]++] = stream;
-    if (i < FIX_REGIONS) r = base[dev] + (size_t)i * FIX_REGION_TILES;
-  }
-  lock.store(0, std::memory_order_release);
-  return r;
-}
-
 // descriptors that may share one grouped launch: identical in every field but the operand / output pointers
 bool same_problem_shape(const sdmi_gemm_desc* a, const sdmi_gemm_desc* b) {
   sdmi_gemm_desc x = *a, y = *b;
@@ -2177,24 +2170,10 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
     run.split_stride = slab;
     run.ws_gstride = (long long)splits * slab;
   }
-  // in-launch split-K combine (fixup_combine): weight gradients on the LDS-DMA mainloops, one problem, 16-B slab rows,
-  // no GroupNorm statistics, at most FIX_MAX_SPLIT slices, a counter region for this stream
-  g_last_fused = 0;
-  if (splits > 1 && G == 1 && e.n8 && !e.gn_part && variant != 0 && d->a_mode == SDMI_A_COLMAJOR &&
-      splits <= FIX_MAX_SPLIT && fix_enabled()) {
-    const int tiles = (int)(grid.x * grid.y);
-    unsigned long long* cnt = tiles <= FIX_REGION_TILES ? fix_region(s) : nullptr;
-    if (cnt) {
-      EpiArgs red = e;
-      red.nsplit = splits;
-      a.fix_tq = (tiles + 7) / 8;
-      a.fix_gx = (int)grid.x;
-      a.fix_tiles = tiles;
-      a.fix_sl = reduce_lanes(red);
-      a.fix_cnt = cnt;
-      grid = dim3((unsigned)(8 * a.fix_tq * splits), 1, 1);
-      g_last_fused = 1;
-    }
+  if (variant >= 12) {  // persistent streaming kernel (whole K per tile: splits == 1 by plan_splits)
+    if (splits != 1 || G != 1) return -18;
+    const hipError_t es = launch_stream(a, run, variant, (int)(grid.x * grid.y), s);
+    return es == hipSuccess ? 0 : (int)es;
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;
@@ -2207,7 +2186,7 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
     default: return -6;
   }
   if (err != hipSuccess) return (int)err;
-  if (splits > 1 && !a.fix_tq) {
+  if (splits > 1) {
     EpiArgs red = e;
     red.raw = 0;
     red.nsplit = splits;
@@ -2220,24 +2199,6 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
   return 0;
 }
 }  // namespace
-
-extern "C" int sdmi_gemm_last_fused(void) { return g_last_fused; }
-
-extern "C" int sdmi_gemm_fix_enable(int on) {
-  const int was = fix_enabled() ? 1 : 0;
-  g_fix_on.store(on ? 1 : 0, std::memory_order_relaxed);
-  return was;
-}
-
-extern "C" int sdmi_gemm_fix_status(int* timed_out) {
-  unsigned v = 0;
-  if (hipDeviceSynchronize() != hipSuccess) return -2;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_fix_err), sizeof(v), 0, hipMemcpyDeviceToHost) != hipSuccess) return -3;
-  const unsigned zero = 0;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_fix_err), &zero, sizeof(zero), 0, hipMemcpyHostToDevice) != hipSuccess) return -4;
-  if (timed_out) *timed_out = (int)v;
-  return 0;
-}
 
 extern "C" int sdmi_gemm(const sdmi_gemm_desc* d, void* workspace, size_t ws_bytes, sdmi_stream_t stream) {
   if (!d) return -1;

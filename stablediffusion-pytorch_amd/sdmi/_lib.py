@@ -89,9 +89,6 @@ SIGNATURES = {
     "sdmi_gemm_grouped_plan": ([ctypes.POINTER(GemmDesc), _I, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_size_t)], _I),
     "sdmi_gemm_grouped": ([ctypes.POINTER(GemmDesc), _I, _P, _SZ, _P], _I),
-    "sdmi_gemm_last_fused": ([], _I),
-    "sdmi_gemm_fix_enable": ([_I], _I),
-    "sdmi_gemm_fix_status": ([ctypes.POINTER(ctypes.c_int)], _I),
     "sdmi_gemm_kernel_info": ([ctypes.POINTER(GemmDesc), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
                               _I),
     "sdmi_attn_fwd": ([_P, _I, _P, _I, _P, _I, _P, _I, _P, _I, _I, _I, _I, _I, _P], _I),

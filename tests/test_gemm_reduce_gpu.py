@@ -199,79 +199,3 @@ def test_kgroup_mainloop_rowmajor_and_conv(monkeypatch, splits):
     torch.cuda.synchronize()
     assert _relerr(y.permute(0, 3, 1, 2), ref) < 2e-3
 
-
-def _fix(L, on):
-    return L.sdmi_gemm_fix_enable(1 if on else 0)
-
-
-FIX_SPLITS = (2, 3, 4, 6, 8)
-
-
-@pytest.mark.parametrize("variant", (2, 5, 6, 11))
-@pytest.mark.parametrize("shape", CONV_SHAPES + [(8, 16, 128, 128), (4, 32, 64, 96)],
-                         ids=lambda s: "B{}H{}C{}O{}".format(*s))
-def test_conv_wgrad_inlaunch_combine_bitwise(monkeypatch, shape, variant):
-    """Split-K weight gradients combined INSIDE the launch (every slice waits for its tile's other slices, then finishes
-    a share of the tile: csrc/gemm.hip fixup_combine) against the two-launch form (slabs + splitk_reduce_n8_kernel):
-    bitwise equal weight, bias and per-sample group-sum gradients at every split count, and no combine timed out."""
-    import ctypes
-    from sdmi import kernels as K, _lib
-    L = _lib.lib()
-    B, H, C, O = shape
-    g = torch.Generator().manual_seed(11 + B * H + C)
-    x = torch.randn(B * H * H, C, generator=g).to(torch.bfloat16).cuda()
-    dy = (torch.randn(B * H * H, O, generator=g) * 0.5).to(torch.bfloat16).cuda()
-    try:
-        for sp in FIX_SPLITS:
-            _forced(monkeypatch, K, sp, variant)
-            res = []
-            for on in (False, True):
-                _fix(L, on)
-                dw = torch.full((O, C, 3, 3), float("nan"), device="cuda")
-                bg = torch.full((O,), float("nan"), device="cuda")
-                gs = torch.full((B, O), float("nan"), device="cuda", dtype=torch.bfloat16)
-                K.conv_wgrad(dy, O, x, B, H, H, C, C, O, 3, 3, 1, 1, dw, H, H, bias_grad=bg, group_sums=gs)
-                res.append((dw, bg, gs, L.sdmi_gemm_last_fused()))
-            torch.cuda.synchronize()
-            tag = f"splits={sp} variant={variant}"
-            assert res[0][3] == 0, tag
-            for a, b in zip(res[0][:3], res[1][:3]):
-                assert torch.equal(a, b), tag
-    finally:
-        _fix(L, True)
-    err = ctypes.c_int(-1)
-    _lib.check(L.sdmi_gemm_fix_status(ctypes.byref(err)), "sdmi_gemm_fix_status")
-    assert err.value == 0
-
-
-@pytest.mark.parametrize("variant", (2, 11))
-@pytest.mark.parametrize("M,N,K", [(32768, 384, 384), (2048, 288, 1152), (512, 136, 264), (8192, 512, 1536)])
-def test_linear_wgrad_inlaunch_combine_bitwise(monkeypatch, M, N, K, variant):
-    """Linear weight gradients with a bias (VALU row-sum chunk) through the in-launch combine: bitwise the two-launch
-    form, and the in-launch form is the one taken (sdmi_gemm_last_fused) whenever splits > 1."""
-    import ctypes
-    from sdmi import kernels as Kn, _lib
-    L = _lib.lib()
-    g = torch.Generator().manual_seed(M + 3 * N + K)
-    dy = (torch.randn(M, N, generator=g) * 0.5).to(torch.bfloat16).cuda()
-    x = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
-    try:
-        for sp in FIX_SPLITS:
-            _forced(monkeypatch, Kn, sp, variant)
-            res = []
-            for on in (False, True):
-                _fix(L, on)
-                out = torch.full((N, K), float("nan"), device="cuda")
-                bg = torch.full((N,), float("nan"), device="cuda")
-                Kn.linear_wgrad(dy, x, out, bias_grad=bg)
-                res.append((out, bg, L.sdmi_gemm_last_fused()))
-            torch.cuda.synchronize()
-            tag = f"splits={sp} variant={variant}"
-            assert res[0][2] == 0 and res[1][2] == 1, tag
-            assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]), tag
-            assert _relerr(res[1][0], dy.float().t() @ x.float()) < 2e-3, tag
-    finally:
-        _fix(L, True)
-    err = ctypes.c_int(-1)
-    _lib.check(L.sdmi_gemm_fix_status(ctypes.byref(err)), "sdmi_gemm_fix_status")
-    assert err.value == 0
