@@ -55,8 +55,6 @@ DMA_VARIANTS = {2: (2, None, 128, 2, 64, 1), 3: (3, 128, 128, 2, 64, 1), 4: (4, 
                 5: (3, None, 128, 2, 32, 1), 6: (4, 128, 128, 2, 64, 1), 7: (6, 64, 64, 4, 64, 1),
                 8: (6, 128, 64, 4, 64, 1), 9: (3, 128, 64, 4, 64, 1), 10: (2, 128, 64, 4, 64, 1),
                 11: (2, 128, 128, 2, 64, 2)}
-# persistent streaming kernels gemm_stream_kernel<TBM, TBN, STAGES, KBK> (variants 12-15)
-STREAM_VARIANTS = {12: (128, 128, 3, 64), 13: (64, 128, 5, 64), 14: (64, 128, 8, 32), 15: (128, 128, 6, 32)}
 
 
 def kernel_name(tag, info):
@@ -67,8 +65,6 @@ def kernel_name(tag, info):
     tn = int(re.search(r"tile_n=(\d+)", info).group(1))
     if v == 0:
         return f"gemm_kernel<{a}, {b}, *>"
-    if v in STREAM_VARIANTS:
-        return "gemm_stream_kernel<{}, {}, {}, {}>".format(*STREAM_VARIANTS[v])
     st, tbn, tbm, nwn, kbk, kg = DMA_VARIANTS[v]
     return f"gemm_dma_kernel<{a}, {b}, {st}, {tbn or tn}, {tbm}, {nwn}, *, {kbk}, *, {kg}>"
 

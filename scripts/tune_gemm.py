@@ -136,14 +136,11 @@ def main():
         # mainloops: register staging (1) and the LDS-DMA rings (2, 3, 6: 2 / 3 / 4 stages of 64-deep K; 7, 8: 64-row
         # tiles with 6 stages; 4: 8-wave
         # 128 x {256, 384} tiles; 5: 3 stages of 32-deep K); the library downgrades a request the mode cannot take
-        # 11: two k-groups of 4 waves per 128 x 128 weight-gradient tile (fewer split-K slabs); 12-15: the persistent
-        # streaming kernel (row-major A, [n][k] B: one workgroup per CU walking its tiles, ring across tile boundaries)
+        # 11: two k-groups of 4 waves per 128 x 128 weight-gradient tile (fewer split-K slabs)
         variants = tuple(int(v) for v in os.environ.get("SDMI_TUNE_VARIANTS", "1,2,3,4,5,6,7,8,9,10,11").split(","))
         for v in variants:
             for s in SPLITS:
                 if s > nkt or s * d.m * d.n * 4 >= min(ws.numel() * 4, 1 << 31):
-                    continue
-                if v >= 12 and s > 1:  # 12-15: the persistent streaming kernel (whole K per tile, never split)
                     continue
                 d.splits_hint, d.variant_hint = s, v
                 ts = time_launch(L, d, ws, stream)

@@ -1426,155 +1426,6 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
 #endif
 }
 
-// ---- persistent streaming GEMM (mainloop variants 12-15) --------------------------------------------------------
-// The short-K GEMMs of the step (K = 128-1536: the UNet's attention projections and 1x1 convolutions, every DiT
-// projection at K = 288 / 1152) ran as ONE lockstep wave of workgroups per launch: operand fill (1.5-2.3 us), a
-// latency-bound main loop of 2-6 k-tiles behind a 2-stage ring, then a synchronized HBM-bound output burst
-// (GEMM phase probe). Here one workgroup per CU walks a sequence of output tiles, and its LDS-DMA
-// ring runs on across tile boundaries: the first k-tiles of the next tile are in flight while the current tile's last
-// MFMAs and its epilogue (staged through an LDS area of its own) run, so the fill latency is paid once per launch
-// and the output stores of one tile overlap the operand loads of the next.
-// A row-major [M][K] (lda), B [N][K] (ldb), K % 8 == 0 (a ragged last k-tile is zero-filled by the buffer
-// descriptor's range check), no split-K, any plain epilogue (bias, row bias, residual, activation, remap; bf16 or
-// fp32 C). TBM x TBN tiles on 4 waves (64 rows x TBN / NWN columns each), STAGES k-tiles of KBK in flight.
-template <int TBM, int TBN, int STAGES, int KBK>
-constexpr size_t stream_lds() {
-  return (size_t)STAGES * (TBM + TBN) * KBK * 2 + (size_t)64 * (TBN + 4) * 4;
-}
-
-template <int TBM, int TBN, int STAGES, int KBK>
-__global__ __launch_bounds__(256, 1) void gemm_stream_kernel(const Args g, const EpiArgs e) {
-  constexpr int NTH = 256, NW = 4;
-  constexpr int NWN = NW / (TBM / 64);  // waves along N (TBM / 64 along M)
-  constexpr int WTN = TBN / NWN, NJ = WTN / 16;
-  constexpr int KS = KBK / 32, RB = KBK * 2, RPI = 1024 / RB, CPR = KBK / 8;
-  constexpr int A_BYTES = TBM * KBK * 2, B_BYTES = TBN * KBK * 2, STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int A_PW = A_BYTES / 1024 / NW, B_PW = B_BYTES / 1024 / NW, P = A_PW + B_PW;
-  static_assert(KBK == 64 || KBK == 32, "staged k depth");
-  static_assert(TBM == 64 || TBM == 128, "tile rows");
-  static_assert(A_PW * NW * 1024 == A_BYTES && B_PW * NW * 1024 == B_BYTES, "DMA pieces per wave");
-  static_assert(WTN % 16 == 0 && STAGES >= 2, "wave tile / ring");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const ring = smem;                                  // [STAGES][A | B]
-  char* const epi_lds = smem + STAGES * STAGE_BYTES;        // the epilogue's fp32 staging rows
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = (wave / NWN) * 64, wn = (wave % NWN) * WTN;
-  const int gx = (g.N + TBN - 1) / TBN;
-  const int T = ((g.M + TBM - 1) / TBM) * gx;
-  const int nk = (g.K + KBK - 1) / KBK;
-  // persistent slot -> logical slot, XCD-banded (tile_id's bijection for a 1-D grid): in every round the workgroups of
-  // one XCD take consecutive tiles, i.e. the column tiles of the same A rows share that XCD's L2
-  const int G = gridDim.x, w = blockIdx.x;
-  const int xcd = w & 7, q8 = G >> 3, r8 = G & 7;
-  const int lw = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w >> 3);
-  const int ntiles = lw < T ? (T - lw + G - 1) / G : 0;
-  const int nsteps = ntiles * nk;
-  constexpr int OOB = (int)0x80000000;
-  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, 0x7fffffff, 0x00020000);
-
-  // per-lane constants of the K-contiguous images: DMA instruction q = wave * PW + j writes 1 KiB, rows q * RPI ..,
-  // lane -> row q * RPI + lane / CPR, physical slot lane % CPR holding logical chunk c (kc_off_k's involution)
-  int a_r[A_PW], a_kk[A_PW], b_r[B_PW], b_kk[B_PW];
-#pragma unroll
-  for (int j = 0; j < A_PW; ++j) {
-    const int r = (wave * A_PW + j) * RPI + lane / CPR;
-    a_r[j] = r;
-    a_kk[j] = ((kc_off_k<KBK>(r, lane % CPR) - r * RB) >> 4) * 8;
-  }
-#pragma unroll
-  for (int j = 0; j < B_PW; ++j) {
-    const int r = (wave * B_PW + j) * RPI + lane / CPR;
-    b_r[j] = r;
-    b_kk[j] = ((kc_off_k<KBK>(r, lane % CPR) - r * RB) >> 4) * 8;
-  }
-  // issue cursor: the step (tile round is_r, k-tile is_kt) issued next, and the byte offsets of its tile's rows
-  int is_r = 0, is_kt = 0, is_s = 0;
-  int a_v[A_PW], b_v[B_PW];
-  auto set_issue_tile = [&](int r) __attribute__((always_inline)) {
-    const int tile = lw + r * G, mt = tile / gx;
-    const int m0 = mt * TBM, n0 = (tile - mt * gx) * TBN;
-#pragma unroll
-    for (int j = 0; j < A_PW; ++j) a_v[j] = m0 + a_r[j] < g.M ? ((m0 + a_r[j]) * g.lda + a_kk[j]) * 2 : OOB;
-#pragma unroll
-    for (int j = 0; j < B_PW; ++j) b_v[j] = n0 + b_r[j] < g.N ? ((n0 + b_r[j]) * g.ldb + b_kk[j]) * 2 : OOB;
-  };
-  auto issue_next = [&]() __attribute__((always_inline)) {
-    char* sa = ring + (is_s % STAGES) * STAGE_BYTES;
-    char* sb = sa + A_BYTES;
-    const int k0 = is_kt * KBK;
-    if (k0 + KBK <= g.K) {  // full k-tile: an add per piece (OOB rows stay out of range)
-#pragma unroll
-      for (int j = 0; j < A_PW; ++j) dma16(rsA, sa + (wave * A_PW + j) * 1024, a_v[j] + k0 * 2);
-#pragma unroll
-      for (int j = 0; j < B_PW; ++j) dma16(rsB, sb + (wave * B_PW + j) * 1024, b_v[j] + k0 * 2);
-    } else {  // ragged last k-tile: chunks at k >= K read as zeros
-#pragma unroll
-      for (int j = 0; j < A_PW; ++j)
-        dma16(rsA, sa + (wave * A_PW + j) * 1024, k0 + a_kk[j] < g.K ? a_v[j] + k0 * 2 : OOB);
-#pragma unroll
-      for (int j = 0; j < B_PW; ++j)
-        dma16(rsB, sb + (wave * B_PW + j) * 1024, k0 + b_kk[j] < g.K ? b_v[j] + k0 * 2 : OOB);
-    }
-    ++is_s;
-    if (++is_kt == nk) {
-      is_kt = 0;
-      if (++is_r < ntiles) set_issue_tile(is_r);
-    }
-  };
-
-  f32x4 acc[4][NJ];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  if (ntiles > 0) set_issue_tile(0);
-#pragma unroll
-  for (int p = 0; p < STAGES - 1; ++p)
-    if (p < nsteps) issue_next();
-  int c_r = 0, c_kt = 0;  // consume cursor
-#pragma unroll 1
-  for (int s = 0; s < nsteps; ++s) {
-    // step s landed for this wave: at most (steps issued after s) x P DMA instructions outstanding. An epilogue's
-    // stores, issued after those, count as younger too: the wait then also covers them (conservative, never early).
-    if (STAGES > 2 && s + STAGES - 2 < nsteps)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((STAGES > 2 ? STAGES - 2 : 0) * P) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's DMA for step s done; every wave done reading step s - 1's stage
-    if (s + STAGES - 1 < nsteps) issue_next();
-    const char* ta = ring + (s % STAGES) * STAGE_BYTES;
-    const char* tb = ta + A_BYTES;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      s16x8 fa[4], fb[NJ];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag_kc_k<KBK>(ta, wm + 16 * i, ks, lane);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) fb[j] = frag_kc_k<KBK>(tb, wn + 16 * j, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    if (++c_kt == nk) {  // tile c_r complete: its epilogue, while the next tile's first k-tiles are in flight
-      const int tile = lw + c_r * G, mt = tile / gx;
-      EpiArgs ev = epi_args_late();
-      gemm_epilogue<TBN, false, TBM, NJ, NTH>(ev, acc, epi_lds, mt * TBM, (tile - mt * gx) * TBN, wm, wn, lane, 0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      c_kt = 0;
-      ++c_r;
-    }
-  }
-}
-
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
 // 8-column items; its SL slab lanes sum disjoint slab subsets (a wave reads 64 consecutive items of ONE slab:
 // contiguous 2 KiB) and are merged in LDS in a fixed order, so the result is deterministic. SL > 1 spreads the
@@ -1781,7 +1632,7 @@ int gemm_variant() {
   if (v == -2) {
     const char* s = getenv("SDMI_GEMM_VARIANT");
     v = s ? atoi(s) : -1;
-    if (v != 0 && (v < 2 || v > 15)) v = -1;
+    if (v != 0 && (v < 2 || v > 11)) v = -1;
   }
   return v;
 }
@@ -1795,11 +1646,7 @@ bool dma_reductions_ok(const sdmi_gemm_desc* d) {
 
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 15) v = d->variant_hint == 1 ? 0 : d->variant_hint;
-  // persistent streaming kernel (12-15): row-major A, [n][k] B, plain epilogue, no split-K
-  if (v >= 12 && !(d->a_mode == SDMI_A_ROWMAJOR && d->b_mode == SDMI_B_NK && !has_reductions(d) && !d->gn_part && !d->a2))
-    v = 2;
-  if (v >= 12) return v;
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 11) v = d->variant_hint == 1 ? 0 : d->variant_hint;
   if (v < 0) v = 2;  // (col-major A with [n][k] B has no DMA instantiation: register staging below)
   if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
   if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
@@ -1815,9 +1662,7 @@ int pick_variant(const sdmi_gemm_desc* d) {
   return v;
 }
 
-int tile_m(const sdmi_gemm_desc*, int variant) {
-  return (variant >= 7 && variant <= 10) || variant == 13 || variant == 14 ? 64 : BM;
-}
+int tile_m(const sdmi_gemm_desc*, int variant) { return variant >= 7 && variant <= 10 ? 64 : BM; }
 
 // columns the grid covers: the DMA kernels compute the reduction columns outside the column tiles
 int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total(d) : d->n; }
@@ -1825,7 +1670,6 @@ int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total
 // Column-tile width: 192 (2-stage DMA, B_NK, N % 192 == 0) when it needs fewer rounds x columns of the
 // 512 workgroup slots (2 per CU) than 128 -- e.g. 32768 x 384: 768 tiles = 1.5 rounds at 128, 512 = 1 at 192.
 int pick_tbn(const sdmi_gemm_desc* d, int variant) {
-  if (variant >= 12) return BN;
   if (variant == 4) return d->n % 384 == 0 ? 384 : 256;
   if (variant == 7) return 64;
   if (variant >= 8 || variant == 6) return BN;  // incl. 11 (k-groups)
@@ -1935,37 +1779,6 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, i
     if (a.rowsum) return launch_dma_red<AM, BMODE, 1>(a, e, grid, s, v, tbn);
   }
   return launch_dma_red<AM, BMODE, 0>(a, e, grid, s, v, tbn);
-}
-
-template <int TBM, int TBN, int STAGES, int KBK>
-hipError_t launch_stream_t(const Args& a, const EpiArgs& e, int ctas, hipStream_t s) {
-  constexpr size_t lds = stream_lds<TBM, TBN, STAGES, KBK>();
-  static_assert(lds <= 160 * 1024, "LDS");
-  sdmi_rt::launch((gemm_stream_kernel<TBM, TBN, STAGES, KBK>), dim3((unsigned)ctas), dim3(256), lds, s, a, e);
-  return hipGetLastError();
-}
-
-int cu_count() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0, c = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      n = c;
-    if (n <= 0) n = 256;
-  }
-  return n;
-}
-
-// the persistent streaming kernels: one workgroup per CU (their LDS), at most one per tile
-hipError_t launch_stream(const Args& a, const EpiArgs& e, int variant, int tiles, hipStream_t s) {
-  const int ctas = std::min(tiles, cu_count());
-  switch (variant) {
-    case 12: return launch_stream_t<128, 128, 3, 64>(a, e, ctas, s);
-    case 13: return launch_stream_t<64, 128, 5, 64>(a, e, ctas, s);
-    case 14: return launch_stream_t<64, 128, 8, 32>(a, e, ctas, s);
-    case 15: return launch_stream_t<128, 128, 6, 32>(a, e, ctas, s);
-    default: return hipErrorInvalidValue;
-  }
 }
 
 int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
@@ -2079,7 +1892,6 @@ int plan_splits(const sdmi_gemm_desc* d) {
   const int v = pick_variant(d), tbn = pick_tbn(d, v), tbm = tile_m(d, v);
   const long long tiles = (long long)((d->m + tbm - 1) / tbm) * ((n_grid(d, v) + tbn - 1) / tbn);
   const int nkt = (d->k + BK - 1) / BK;
-  if (v >= 12) return 1;  // the persistent streaming kernel covers the whole K per tile
   if (d->splits_hint > 0) {
     int s = std::min(d->splits_hint, nkt);
     while (s > 1 && (long long)s * d->m * slab_n(d) * 4 >= (1LL << 31)) s >>= 1;
@@ -2169,11 +1981,6 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
     run.nsplit = splits;
     run.split_stride = slab;
     run.ws_gstride = (long long)splits * slab;
-  }
-  if (variant >= 12) {  // persistent streaming kernel (whole K per tile: splits == 1 by plan_splits)
-    if (splits != 1 || G != 1) return -18;
-    const hipError_t es = launch_stream(a, run, variant, (int)(grid.x * grid.y), s);
-    return es == hipSuccess ? 0 : (int)es;
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;

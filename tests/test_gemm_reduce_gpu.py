@@ -198,4 +198,3 @@ def test_kgroup_mainloop_rowmajor_and_conv(monkeypatch, splits):
     Kn.conv_fwd(xn, B, H, H, cin, cin, wcat, cout, 3, 3, 1, 1, y, cout, x2=x2n.view(-1, cin2), cin2=cin2)
     torch.cuda.synchronize()
     assert _relerr(y.permute(0, 3, 1, 2), ref) < 2e-3
-
