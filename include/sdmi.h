@@ -478,6 +478,7 @@ int sdmi_plan_destroy(void* plan);
  * LDS bytes;
  * and the average device time of launch op i re-issued alone (iters times after warm untimed issues). */
 int sdmi_plan_op_info(const void* plan, int i, int* kind, const char** name, int* grid, int* block, int* shmem);
+int sdmi_plan_op_stream(const void* plan, int i, sdmi_stream_t* stream); /* the stream op i was recorded on */
 int sdmi_plan_time_op(void* plan, int i, int warm, int iters, float* us);
 
 /* ---------------------------------------------------------------------------------------------

@@ -184,6 +184,14 @@ extern "C" int sdmi_plan_replay(void* plan, int start, int* callout, int* next) 
   return 0;
 }
 
+// the stream an op was recorded on (launches, event records, waits, all-reduces; nullptr for callouts)
+extern "C" int sdmi_plan_op_stream(const void* plan, int i, sdmi_stream_t* stream) {
+  const Plan* p = (const Plan*)plan;
+  if (!p || i < 0 || i >= (int)p->ops.size() || !stream) return -1;
+  *stream = (sdmi_stream_t)p->ops[i].stream;
+  return 0;
+}
+
 // Per-op inspection for profiling tools (scripts/plan_profile.py): op kind (0 launch, 1 event record, 2 stream wait,
 // 3 callout, 4 all-reduce), kernel name, grid / block, LDS bytes.
 extern "C" int sdmi_plan_op_info(const void* plan, int i, int* kind, const char** name, int* grid, int* block,

@@ -171,6 +171,7 @@ SIGNATURES = {
     "sdmi_plan_info": ([_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
     "sdmi_plan_replay": ([_P, _I, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
     "sdmi_plan_destroy": ([_P], _I),
+    "sdmi_plan_op_stream": ([_P, _I, ctypes.POINTER(ctypes.c_void_p)], _I),
     "sdmi_plan_op_info": ([_P, _I, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_char_p),
                            ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], _I),
     "sdmi_plan_time_op": ([_P, _I, _I, _I, ctypes.POINTER(ctypes.c_float)], _I),
