@@ -34,9 +34,10 @@ def main():
     rec, wait = P.record_event, P.wait_event
 
     def rec_hook(ev, stream):
+        r = rec(ev, stream)  # (a torch event gets its HIP handle at its first record)
         if P.RECORDING is not None:
             log.append(("rec", stream.cuda_stream, ev.cuda_event))
-        return rec(ev, stream)
+        return r
 
     def wait_hook(stream, ev):
         if P.RECORDING is not None:
