@@ -1426,198 +1426,6 @@ void gemm_dma_kernel(const Args g, const EpiArgs e) {
 #endif
 }
 
-// ---- warp-specialised persistent GEMM (mainloop variants 12 / 13) -------------------------------------------------
-// The step's short-K GEMMs (K = 128-1152: the UNet's attention projections and 1x1 convolutions, every DiT projection)
-// run as ONE lockstep wave of workgroups per launch (operand fill, a main loop of 2-18 k-tiles that waits on every
-// k-tile's LDS-DMA, then a synchronised output burst: DESIGN.md section 9, GEMM phase probe). A persistent kernel in
-// which the SAME waves load and compute cannot overlap those phases: vmcnt is one in-order counter per wave, so an
-// epilogue's addend loads and stores drain the ring's prefetches at every tile boundary (round 6).
-// Here the roles are split over the waves of one workgroup per CU, each with its own vmcnt: 4 LOADER waves only move
-// k-tiles into a ring of SLOTS LDS stages (LDS-DMA) and publish each behind a counted vmcnt wait, D k-tiles in flight
-// per loader wave; 4 CONSUMER waves (2 x 2, 64 x 64 each) take a stage once every loader has published it, read their
-// fragments, release the stage, run the MFMAs and -- at a tile's last k-tile -- its epilogue through a wave-private LDS
-// staging area while the loaders already fill the next tile's stages. Handshake: per stage a FULL word per loader wave
-// and a FREE word per consumer wave in LDS, phase-counted (MI355X guide, 'ring-gemm').
-// The workgroup walks output tiles lw, lw + G, ... (G = grid = at most one per CU; lw XCD-banded as tile_id's order).
-// A row-major [M][K], B [N][K]; K % 8 == 0 (ragged k-tiles zero-filled by the buffer range check); no split-K; the
-// 16-B epilogue path (EpiArgs::vec: bias, bias2, row bias, residual, activation, remap; bf16 or fp32 C).
-// Every wait on a handshake word is bounded (WS_SPIN polls, ~0.2 s): a broken handshake ends the launch with wrong
-// outputs -- which the parity tests catch -- instead of a hung GPU.
-constexpr int WS_SPIN = 1 << 21;
-
-template <int SLOTS, int KBK>
-constexpr size_t ws_lds() {
-  return (size_t)SLOTS * 256 * KBK * 2 + (size_t)4 * 64 * 68 * 4 + (size_t)SLOTS * 8 * 4;
-}
-
-template <int SLOTS, int KBK, int D>
-__global__ __launch_bounds__(512, 2) void gemm_ws_kernel(const Args g, const EpiArgs e) {
-  constexpr int TBM = 128, TBN = 128, NC = 4, NL = 4, SROW = 64 + 4;
-  constexpr int KS = KBK / 32, RB = KBK * 2, RPI = 1024 / RB, CPR = KBK / 8;
-  constexpr int A_BYTES = TBM * KBK * 2, B_BYTES = TBN * KBK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_PW = A_BYTES / 1024 / NL, B_PW = B_BYTES / 1024 / NL, P = A_PW + B_PW;
-  static_assert(KBK == 64 || KBK == 32, "staged k depth");
-  static_assert(D >= 1 && D <= SLOTS, "k-tiles in flight per loader wave: at most the ring");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const ring = smem;                                          // [SLOTS][A | B]
-  float* const stg = (float*)(smem + SLOTS * STAGE);                // [NC][64][SROW] fp32 epilogue staging
-  volatile int* const full = (volatile int*)(stg + NC * 64 * SROW);  // [SLOTS][NL]
-  volatile int* const freew = full + SLOTS * NL;                     // [SLOTS][NC]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  for (int i = tid; i < SLOTS * (NL + NC); i += 512) full[i] = 0;
-  __syncthreads();  // (the only workgroup barrier: from here on the roles synchronise through the words above)
-  const int gx = (g.N + TBN - 1) / TBN;
-  const int T = ((g.M + TBM - 1) / TBM) * gx;
-  const int nk = (g.K + KBK - 1) / KBK;
-  const int G = gridDim.x, w = blockIdx.x;
-  const int xcd = w & 7, q8 = G >> 3, r8 = G & 7;
-  const int lw = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (w >> 3);
-  const int ntiles = lw < T ? (T - lw + G - 1) / G : 0;
-  const int nsteps = ntiles * nk;
-
-  if (wave >= NC) {  // ---------------- loader waves ----------------
-    const int lv = wave - NC;
-    constexpr int OOB = (int)0x80000000;
-    const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, 0x7fffffff, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, 0x7fffffff, 0x00020000);
-    // this wave's DMA instructions q = lv * PW + j of the 4-wave K-contiguous image layout (kc_off_k's involution)
-    int a_r[A_PW], a_kk[A_PW], b_r[B_PW], b_kk[B_PW], a_v[A_PW], b_v[B_PW];
-#pragma unroll
-    for (int j = 0; j < A_PW; ++j) {
-      const int r = (lv * A_PW + j) * RPI + lane / CPR;
-      a_r[j] = r;
-      a_kk[j] = ((kc_off_k<KBK>(r, lane % CPR) - r * RB) >> 4) * 8;
-    }
-#pragma unroll
-    for (int j = 0; j < B_PW; ++j) {
-      const int r = (lv * B_PW + j) * RPI + lane / CPR;
-      b_r[j] = r;
-      b_kk[j] = ((kc_off_k<KBK>(r, lane % CPR) - r * RB) >> 4) * 8;
-    }
-    int kt = 0, rr = 0;
-#pragma unroll 1
-    for (int s = 0; s < nsteps; ++s) {
-      const int slot = s % SLOTS, ph = s / SLOTS;
-      if (kt == 0) {  // first k-tile of the next tile: its rows' byte offsets
-        const int tile = lw + rr * G, mt = tile / gx;
-        const int m0 = mt * TBM, n0 = (tile - mt * gx) * TBN;
-#pragma unroll
-        for (int j = 0; j < A_PW; ++j) a_v[j] = m0 + a_r[j] < g.M ? ((m0 + a_r[j]) * g.lda + a_kk[j]) * 2 : OOB;
-#pragma unroll
-        for (int j = 0; j < B_PW; ++j) b_v[j] = n0 + b_r[j] < g.N ? ((n0 + b_r[j]) * g.ldb + b_kk[j]) * 2 : OOB;
-      }
-      if (ph > 0) {  // every consumer wave has taken this stage's previous k-tile
-#pragma unroll 1
-        for (int c = 0; c < NC; ++c)
-          for (int n = 0; freew[slot * NC + c] < ph && n < WS_SPIN; ++n) __builtin_amdgcn_s_sleep(1);
-        asm volatile("" ::: "memory");  // (the stage's DMA writes stay behind the polls)
-      }
-      char* sa = ring + slot * STAGE;
-      char* sb = sa + A_BYTES;
-      const int k0 = kt * KBK;
-      if (k0 + KBK <= g.K) {
-#pragma unroll
-        for (int j = 0; j < A_PW; ++j) dma16(rsA, sa + (lv * A_PW + j) * 1024, a_v[j] + k0 * 2);
-#pragma unroll
-        for (int j = 0; j < B_PW; ++j) dma16(rsB, sb + (lv * B_PW + j) * 1024, b_v[j] + k0 * 2);
-      } else {
-#pragma unroll
-        for (int j = 0; j < A_PW; ++j)
-          dma16(rsA, sa + (lv * A_PW + j) * 1024, k0 + a_kk[j] < g.K ? a_v[j] + k0 * 2 : OOB);
-#pragma unroll
-        for (int j = 0; j < B_PW; ++j)
-          dma16(rsB, sb + (lv * B_PW + j) * 1024, k0 + b_kk[j] < g.K ? b_v[j] + k0 * 2 : OOB);
-      }
-      // publish k-tile s - D + 1: at most (D - 1) k-tiles of this wave's DMA still outstanding
-      if (s >= D - 1) {
-        if constexpr (D > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"i"((D > 1 ? D - 1 : 0) * P) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int sp = s - D + 1;
-        full[(sp % SLOTS) * NL + lv] = sp / SLOTS + 1;
-      }
-      if (++kt == nk) {
-        kt = 0;
-        ++rr;
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll 1
-    for (int sp = nsteps - D + 1 > 0 ? nsteps - D + 1 : 0; sp < nsteps; ++sp) full[(sp % SLOTS) * NL + lv] = sp / SLOTS + 1;
-    return;
-  }
-
-  // ---------------- consumer waves ----------------
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float* const st = stg + wave * 64 * SROW;
-  int kt = 0, rr = 0;
-#pragma unroll 1
-  for (int s = 0; s < nsteps; ++s) {
-    const int slot = s % SLOTS, ph = s / SLOTS + 1;
-#pragma unroll 1
-    for (int l = 0; l < NL; ++l)
-      for (int n = 0; full[slot * NL + l] < ph && n < WS_SPIN; ++n) __builtin_amdgcn_s_sleep(0);
-    asm volatile("" ::: "memory");  // (the fragment reads stay behind the polls)
-    const char* ta = ring + slot * STAGE;
-    const char* tb = ta + A_BYTES;
-    s16x8 fa[KS][4], fb[KS][4];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[ks][i] = frag_kc_k<KBK>(ta, wm + 16 * i, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[ks][j] = frag_kc_k<KBK>(tb, wn + 16 * j, ks, lane);
-    }
-    // the fragments are in registers: release the stage to the loaders before the MFMAs
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(fa[ks][i]));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(fb[ks][j]));
-    }
-    freew[slot * NC + wave] = ph;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (++kt < nk) continue;
-    // ---- this wave's 64 x 64 part of the tile: staged (wave-private LDS rows), then 16-B row stores ----
-    const int tile = lw + rr * G, mt = tile / gx;
-    const int m0 = mt * TBM + wm, n0 = (tile - mt * gx) * TBN + wn;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) st[(16 * i + 4 * (lane >> 4) + q) * SROW + 16 * j + (lane & 15)] = acc[i][j][q];
-    EpiArgs ev = epi_args_late();
-#pragma unroll 1
-    for (int it = 0; it < 8; ++it) {
-      const int row = it * 8 + (lane >> 3), c8 = (lane & 7) * 8;
-      const float4 lo = *(const float4*)(st + row * SROW + c8), hi = *(const float4*)(st + row * SROW + c8 + 4);
-      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      if (m0 + row < ev.m_store && n0 + c8 < ev.n_store) Epi::finish8(ev, m0 + row, n0 + c8, v);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    kt = 0;
-    ++rr;
-  }
-}
-
 // Sum split-K slabs and apply the epilogue, N % 8 == 0 (16-B slab reads). A workgroup owns 256/SL consecutive
 // 8-column items; its SL slab lanes sum disjoint slab subsets (a wave reads 64 consecutive items of ONE slab:
 // contiguous 2 KiB) and are merged in LDS in a fixed order, so the result is deterministic. SL > 1 spreads the
@@ -1824,7 +1632,7 @@ int gemm_variant() {
   if (v == -2) {
     const char* s = getenv("SDMI_GEMM_VARIANT");
     v = s ? atoi(s) : -1;
-    if (v != 0 && (v < 2 || v > 13)) v = -1;
+    if (v != 0 && (v < 2 || v > 11)) v = -1;
   }
   return v;
 }
@@ -1838,12 +1646,7 @@ bool dma_reductions_ok(const sdmi_gemm_desc* d) {
 
 int pick_variant(const sdmi_gemm_desc* d) {
   int v = gemm_variant();
-  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 13) v = d->variant_hint == 1 ? 0 : d->variant_hint;
-  // warp-specialised persistent kernel (12 / 13): row-major A, [n][k] B, the plain 16-B epilogue, no split-K
-  if (v >= 12 && !(d->a_mode == SDMI_A_ROWMAJOR && d->b_mode == SDMI_B_NK && !has_reductions(d) && !d->gn_part && !d->a2 &&
-                   !d->perm && d->n % 8 == 0))
-    v = 2;
-  if (v >= 12) return v;
+  if (v < 0 && d->variant_hint >= 1 && d->variant_hint <= 11) v = d->variant_hint == 1 ? 0 : d->variant_hint;
   if (v < 0) v = 2;  // (col-major A with [n][k] B has no DMA instantiation: register staging below)
   if (has_reductions(d) && (v == 3 || !dma_reductions_ok(d))) v = v == 3 ? 2 : 0;
   if (has_reductions(d) && v != 0 && d->a_mode != SDMI_A_COLMAJOR) v = 0;
@@ -1867,7 +1670,6 @@ int n_grid(const sdmi_gemm_desc* d, int variant) { return variant == 0 ? n_total
 // Column-tile width: 192 (2-stage DMA, B_NK, N % 192 == 0) when it needs fewer rounds x columns of the
 // 512 workgroup slots (2 per CU) than 128 -- e.g. 32768 x 384: 768 tiles = 1.5 rounds at 128, 512 = 1 at 192.
 int pick_tbn(const sdmi_gemm_desc* d, int variant) {
-  if (variant >= 12) return BN;
   if (variant == 4) return d->n % 384 == 0 ? 384 : 256;
   if (variant == 7) return 64;
   if (variant >= 8 || variant == 6) return BN;  // incl. 11 (k-groups)
@@ -1977,35 +1779,6 @@ hipError_t launch_t(const Args& a, const EpiArgs& e, dim3 grid, hipStream_t s, i
     if (a.rowsum) return launch_dma_red<AM, BMODE, 1>(a, e, grid, s, v, tbn);
   }
   return launch_dma_red<AM, BMODE, 0>(a, e, grid, s, v, tbn);
-}
-
-int cu_count() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0, c = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      n = c;
-    if (n <= 0) n = 256;
-  }
-  return n;
-}
-
-template <int SLOTS, int KBK, int D>
-hipError_t launch_ws_t(const Args& a, const EpiArgs& e, int tiles, hipStream_t s) {
-  constexpr size_t lds = ws_lds<SLOTS, KBK>();
-  static_assert(lds <= 160 * 1024, "LDS");
-  sdmi_rt::launch((gemm_ws_kernel<SLOTS, KBK, D>), dim3((unsigned)std::min(tiles, cu_count())), dim3(512), lds, s, a, e);
-  return hipGetLastError();
-}
-
-// warp-specialised persistent kernels: one 8-wave workgroup per CU (their LDS), at most one per tile
-hipError_t launch_ws(const Args& a, const EpiArgs& e, int variant, int tiles, hipStream_t s) {
-  if (!e.vec) return hipErrorInvalidValue;
-  switch (variant) {
-    case 12: return launch_ws_t<5, 32, 3>(a, e, tiles, s);  // 5 stages of 32-deep k, 3 in flight per loader wave
-    case 13: return launch_ws_t<2, 64, 2>(a, e, tiles, s);  // 2 stages of 64-deep k
-    default: return hipErrorInvalidValue;
-  }
 }
 
 int fill_args(const sdmi_gemm_desc* d, Args& a, EpiArgs& e) {
@@ -2119,7 +1892,6 @@ int plan_splits(const sdmi_gemm_desc* d) {
   const int v = pick_variant(d), tbn = pick_tbn(d, v), tbm = tile_m(d, v);
   const long long tiles = (long long)((d->m + tbm - 1) / tbm) * ((n_grid(d, v) + tbn - 1) / tbn);
   const int nkt = (d->k + BK - 1) / BK;
-  if (v >= 12) return 1;  // the warp-specialised kernel covers the whole K per tile
   if (d->splits_hint > 0) {
     int s = std::min(d->splits_hint, nkt);
     while (s > 1 && (long long)s * d->m * slab_n(d) * 4 >= (1LL << 31)) s >>= 1;
@@ -2209,11 +1981,6 @@ int run_gemm(const sdmi_gemm_desc* d, int G, void* workspace, size_t ws_bytes, h
     run.nsplit = splits;
     run.split_stride = slab;
     run.ws_gstride = (long long)splits * slab;
-  }
-  if (variant >= 12) {  // warp-specialised persistent kernel (whole K per tile: splits == 1 by plan_splits)
-    if (splits != 1 || G != 1) return -18;
-    const hipError_t es = launch_ws(a, run, variant, (int)(grid.x * grid.y), s);
-    return es == hipSuccess ? 0 : (int)es;
   }
   hipError_t err;
   int key = d->a_mode * 3 + d->b_mode;

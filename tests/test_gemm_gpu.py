@@ -265,33 +265,3 @@ def _grouped_check(G, M, N, K, bias, _lib, K_, ctypes):
         assert torch.equal(o1, out)
         if bias:
             assert torch.equal(b1, bg)
-
-
-@pytest.mark.parametrize("variant", [12, 13])
-@pytest.mark.parametrize("M,N,K", [(8192, 1152, 288), (8192, 288, 1152), (32768, 384, 384), (300, 200, 136),
-                                   (2048, 768, 768), (17, 40, 8), (4100, 136, 72), (65536, 128, 128)])
-def test_warp_specialised_kernel_matches_reference(monkeypatch, M, N, K, variant):
-    """The warp-specialised persistent GEMM (variants 12 / 13: one workgroup per CU walking its tiles, 4 loader waves
-    filling an LDS ring by LDS-DMA, 4 consumer waves computing and storing, handshake words in LDS) on row-major A /
-    [n][k] B: several tiles per workgroup, ragged M / N / K, bias + residual + SiLU (bf16 C) and alpha (fp32 C), against
-    torch fp32, and run-to-run bitwise determinism."""
-    k, L = _k()
-    monkeypatch.setattr(k, "TUNED", {"__all__": [1, variant]})
-    monkeypatch.setattr(k, "gemm_key", lambda d: "__all__")
-    g = torch.Generator().manual_seed(M + N + K + variant)
-    a = bf(torch.randn(M, K, generator=g)).cuda()
-    w = bf(torch.randn(N, K, generator=g) * 0.1).cuda()
-    bias = torch.randn(N, generator=g).cuda()
-    res = bf(torch.randn(M, N, generator=g)).cuda()
-    c = torch.full((M, N), float("nan"), device="cuda").to(torch.bfloat16)
-    monkeypatch.setattr(k, "GEMM_LOG", [])
-    k.gemm(M, N, K, a, L.A_ROWMAJOR, K, w, L.B_NK, K, c, N, bias=bias, resid=res, ldr=N, act=1)
-    assert k.GEMM_LOG[-1]["variant"] == variant and k.GEMM_LOG[-1]["splits"] == 1, k.GEMM_LOG[-1]
-    close(c, F.silu(a.float() @ w.float().t() + bias + res.float()))
-    c32 = torch.full((M, N), float("nan"), device="cuda")
-    k.gemm(M, N, K, a, L.A_ROWMAJOR, K, w, L.B_NK, K, c32, N, alpha=0.5)
-    close(c32, 0.5 * (a.float() @ w.float().t()), 2e-3)
-    again = torch.full((M, N), float("nan"), device="cuda")
-    k.gemm(M, N, K, a, L.A_ROWMAJOR, K, w, L.B_NK, K, again, N, alpha=0.5)
-    torch.cuda.synchronize()
-    assert torch.equal(c32, again), "not run-to-run deterministic"
