@@ -92,7 +92,8 @@ def build(force=False, verbose=False, out=None, defines=()):
 
 
 def source_digest():
-    """16-hex-digit sha256 over the library's sources (csrc/*.hip, csrc/*.h, include/sdmi.h, by name): the tree a
+    """16-hex-digit sha256 over the library's sources (csrc/*.hip, csrc/*.h, include/sdmi.h, by name) and the tuned
+    GEMM table (sdmi/tuned_gemm.json: its split counts set every launch's grid and slab traffic): the tree a
     committed profile (profiles/rNN_<workload>_pmc_traffic.json / _roofline_evidence.json) was measured on. bench.py
     compares it with the running tree's, so a stale PMC file is reported as such instead of silently reused."""
     import hashlib
@@ -102,6 +103,7 @@ def source_digest():
         h.update(f.encode())
         h.update(open(os.path.join(CSRC, f), "rb").read())
     h.update(open(os.path.join(REPO, "include", "sdmi.h"), "rb").read())
+    h.update(open(os.path.join(HERE, "tuned_gemm.json"), "rb").read())
     return h.hexdigest()[:16]
 
 
