@@ -21,7 +21,8 @@ if [[ $WL != vqvae* ]]; then  # (the isolated plan profile covers the recorded t
   head -3 gpurun_out/pp_${TAG}_$W.txt
 fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$W -o run -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --workload $WL > gpurun_out/prof_${TAG}_$W.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_$W.log; exit 1; }
-python scripts/trace_summary.py gpurun_out/prof_${TAG}_$W/run_kernel_trace.csv --top 80 > gpurun_out/ts_${TAG}_$W.txt
+MARK=add_noise_kernel; [[ $WL == vqvae* ]] && MARK=prep_input_kernel  # the first launch of a VQVAE step
+python scripts/trace_summary.py gpurun_out/prof_${TAG}_$W/run_kernel_trace.csv --top 80 --marker $MARK > gpurun_out/ts_${TAG}_$W.txt
 head -8 gpurun_out/ts_${TAG}_$W.txt
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d gpurun_out/pmc_${TAG}_${W}_$C -o run -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --issue eager --workload $WL > gpurun_out/pmc_${TAG}_${W}_$C.log 2>&1 || { tail -5 gpurun_out/pmc_${TAG}_${W}_$C.log; exit 1; }

@@ -23,6 +23,7 @@
 namespace {
 
 constexpr int VQ_NT = 1024, VQ_WAVES = VQ_NT / 64, MAXC = 8;
+constexpr int VQ_EN_MAX = 16384;  // codes whose |e|^2 table fits the quantize kernel's LDS (64 KiB)
 
 struct VqArgs {
   const float* z; int ldz;  // encoder_conv_out output, NHWC fp32 [P][ldz], channels < C valid
@@ -35,14 +36,38 @@ struct VqArgs {
   float* partial;  // per-workgroup sum of (q - x)^2
 };
 
+// |e_k|^2 of one code, in the order the distance loop has always summed it (c ascending)
+__device__ __forceinline__ float code_norm(const float* e, int C) {
+  float en = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    if (c < C) {
+      const float ec = e[c];
+      en += ec * ec;
+    }
+  }
+  return en;
+}
+
+// Nearest code per pixel (torch.cdist mm form + argmin, first minimum). A workgroup takes 32 pixels; wave w scans
+// code slice w of 16, its lanes 0-31 the first half of the slice and lanes 32-63 the second half for the same 32
+// pixels, and the halves merge with a strict < (the first minimum, as one ascending scan would keep). 32 pixels per
+// workgroup instead of 64 puts the 8192-pixel latent of a B = 8, 256^2 batch on 256 workgroups (was 128: half the
+// CUs idle); EN: the codes' |e|^2 precomputed once per workgroup into LDS instead of per (pixel, code).
+template <bool EN>
 __global__ __launch_bounds__(VQ_NT) void vq_quantize_kernel(const VqArgs a) {
-  __shared__ float sd[VQ_WAVES][64];
-  __shared__ int si[VQ_WAVES][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  extern __shared__ float sen[];  // EN: |e_k|^2 of every code
+  __shared__ float sd[VQ_WAVES][32];
+  __shared__ int si[VQ_WAVES][32];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, pl = lane & 31;
   const long long P = (long long)a.B * a.HW;
-  const long long pix = (long long)blockIdx.x * 64 + lane;
+  const long long pix = (long long)blockIdx.x * 32 + pl;
   const bool on = pix < P;
   const int C = a.C;
+  if constexpr (EN) {
+    for (int k = threadIdx.x; k < a.K; k += VQ_NT) sen[k] = code_norm(a.codebook + (long long)k * C, C);
+    __syncthreads();
+  }
   float x[MAXC];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) x[c] = 0.f;
@@ -73,42 +98,69 @@ __global__ __launch_bounds__(VQ_NT) void vq_quantize_kernel(const VqArgs a) {
     m2[c] = -2.f * x[c];
   }
   const int per = (a.K + VQ_WAVES - 1) / VQ_WAVES;
-  const int k0 = wave * per, k1 = min(a.K, k0 + per);
+  const int w0 = wave * per, w1 = min(a.K, w0 + per);
+  const int wm = min(w1, w0 + (per + 1) / 2);
+  // step j: lanes 0-31 code w0 + j, lanes 32-63 code wm + j -- both loads wave-uniform (scalar), selected per half
+  const int n0 = wm - w0;
   float best = INFINITY;
-  int bi = k0;
-#pragma unroll 1
-  for (int k = k0; k < k1; ++k) {
-    const float* e = a.codebook + (long long)k * C;  // wave-uniform address
+  int bi = half ? wm : w0;
+#pragma unroll 4
+  for (int j = 0; j < n0; ++j) {
+    const int ka = w0 + j, kb = wm + j;
+    const int kbl = min(kb, a.K - 1);  // (in bounds; the update below is masked when kb is past the slice)
+    const float* ea = a.codebook + (long long)ka * C;
+    const float* eb = a.codebook + (long long)kbl * C;
     float en = 0.f, dot = 0.f;
+    if constexpr (EN) {
+      en = sen[half ? kbl : ka];
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (c < C) {
-        const float ec = e[c];
-        en += ec * ec;
-        dot = fmaf(m2[c], ec, dot);
+      for (int c = 0; c < MAXC; ++c)
+        if (c < C) dot = fmaf(m2[c], half ? eb[c] : ea[c], dot);
+    } else {
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        if (c < C) {
+          const float ec = half ? eb[c] : ea[c];
+          en += ec * ec;
+          dot = fmaf(m2[c], ec, dot);
+        }
       }
     }
     const float d = sqrtf(fmaxf(dot + xn + en, 0.f));
-    if (d < best) {
+    if ((!half || kb < w1) && d < best) {
       best = d;
-      bi = k;
+      bi = half ? kb : ka;
     }
   }
-  sd[wave][lane] = best;
-  si[wave][lane] = bi;
+  {  // the second half's codes all follow the first half's: take them only when strictly nearer
+    const float d2 = __shfl_xor(best, 32);
+    const int i2 = __shfl_xor(bi, 32);
+    if (!half && d2 < best) {
+      best = d2;
+      bi = i2;
+    }
+  }
+  if (!half) {
+    sd[wave][pl] = best;
+    si[wave][pl] = bi;
+  }
   __syncthreads();
   if (wave == 0) {
-    float bd = sd[0][lane];
-    int bk = si[0][lane];
-    for (int w = 1; w < VQ_WAVES; ++w) {  // slices are in ascending k order: strict < keeps the first minimum
-      const float d = sd[w][lane];
-      if (d < bd) {
-        bd = d;
-        bk = si[w][lane];
+    float bd = INFINITY;
+    int bk = 0;
+    float loss = 0.f;
+    if (!half) {
+      bd = sd[0][pl];
+      bk = si[0][pl];
+      for (int w = 1; w < VQ_WAVES; ++w) {  // slices are in ascending k order: strict < keeps the first minimum
+        const float d = sd[w][pl];
+        if (d < bd) {
+          bd = d;
+          bk = si[w][pl];
+        }
       }
     }
-    float loss = 0.f;
-    if (on) {
+    if (on && !half) {
       const float* q = a.codebook + (long long)bk * C;
       const long long b = pix / a.HW, p = pix - b * a.HW;
 #pragma unroll
@@ -265,13 +317,24 @@ __global__ void vq_bwd_finish_kernel(const float* partial, int blocks, int C, fl
   }
 }
 
-// demb[k] = g_codebook * sum over pixels p with idx[p] == k of (q_k - x_p), pixels in order: each workgroup streams
-// the index list once through LDS and every thread (one code) scans it
-__global__ __launch_bounds__(256) void vq_codebook_grad_kernel(const long long* idx, const float* xq, const float* codebook,
-                                                               int K, int B, int HW, int C, float g_codebook,
-                                                               const float* loss_w, float* demb) {
-  __shared__ int sidx[1024];
-  const int k = blockIdx.x * 256 + threadIdx.x;
+// demb[k] = g_codebook * sum over pixels p with idx[p] == k of (q_k - x_p). A workgroup owns 64 codes (one per
+// lane) and streams the index list and the pre-quantisation latent through LDS, 1024 pixels per round; each of its 8
+// waves scans one eighth of every round (four indices per LDS load, a wave-uniform address: broadcast) and
+// accumulates its matches branch-free from LDS, in pixel order; the waves' partial sums are then added in wave order
+// (a fixed order: deterministic). At random init most pixels pick a few codes: the first form (one thread per code
+// scanning every pixel, x_p from global memory per match) serialised those codes' threads on global round trips and
+// took 1.3-1.7 ms of the 256^2 VQVAE training step. Padding entries are -1 and never match a code.
+constexpr int CB_WAVES = 8;
+__global__ __launch_bounds__(64 * CB_WAVES) void vq_codebook_grad_kernel(const long long* idx, const float* xq,
+                                                                        const float* codebook, int K, int B, int HW,
+                                                                        int C, float g_codebook, const float* loss_w,
+                                                                        float* demb) {
+  __shared__ int4 sidx4[256];
+  __shared__ float4 sxa[1024], sxb[1024];  // x_p channels 0-3 and 4-7 of the round's pixels
+  __shared__ float red[CB_WAVES][MAXC + 1][64];
+  int* sidx = (int*)sidx4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
   const long long P = (long long)B * HW;
   float acc[MAXC];
   int cnt = 0;
@@ -279,28 +342,69 @@ __global__ __launch_bounds__(256) void vq_codebook_grad_kernel(const long long* 
   for (int c = 0; c < MAXC; ++c) acc[c] = 0.f;
   for (long long p0 = 0; p0 < P; p0 += 1024) {
     __syncthreads();
-    for (int j = threadIdx.x; j < 1024; j += 256) sidx[j] = p0 + j < P ? (int)idx[p0 + j] : -1;
-    __syncthreads();
-    const int n = (int)min<long long>(1024, P - p0);
-    for (int j = 0; j < n; ++j) {
-      if (sidx[j] != k) continue;
-      const long long pix = p0 + j, bb = pix / HW, p = pix - bb * HW;
-      ++cnt;
+    for (int j = threadIdx.x; j < 1024; j += 64 * CB_WAVES) {
+      const long long pix = p0 + j;
+      int v = -1;
+      float xv[MAXC];
 #pragma unroll
-      for (int c = 0; c < MAXC; ++c)
-        if (c < C) acc[c] -= xq[(bb * C + c) * HW + p];
+      for (int c = 0; c < MAXC; ++c) xv[c] = 0.f;
+      if (pix < P) {
+        v = (int)idx[pix];
+        const long long bb = pix / HW, p = pix - bb * HW;
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c)
+          if (c < C) xv[c] = xq[(bb * C + c) * HW + p];
+      }
+      sidx[j] = v;
+      sxa[j] = make_float4(xv[0], xv[1], xv[2], xv[3]);
+      sxb[j] = make_float4(xv[4], xv[5], xv[6], xv[7]);
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int j4 = wave * 32; j4 < wave * 32 + 32; ++j4) {
+      const int4 v = sidx4[j4];
+      if (v.x != k && v.y != k && v.z != k && v.w != k) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool m = (e == 0 ? v.x : (e == 1 ? v.y : (e == 2 ? v.z : v.w))) == k;
+        const float4 xa = sxa[4 * j4 + e];
+        cnt += m;
+        acc[0] -= m ? xa.x : 0.f;
+        acc[1] -= m ? xa.y : 0.f;
+        acc[2] -= m ? xa.z : 0.f;
+        acc[3] -= m ? xa.w : 0.f;
+        if (C > 4) {
+          const float4 xb = sxb[4 * j4 + e];
+          acc[4] -= m ? xb.x : 0.f;
+          acc[5] -= m ? xb.y : 0.f;
+          acc[6] -= m ? xb.z : 0.f;
+          acc[7] -= m ? xb.w : 0.f;
+        }
+      }
     }
   }
-  if (k >= K) return;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) red[wave][c][lane] = acc[c];
+  red[wave][MAXC][lane] = (float)cnt;  // exact: counts <= 2^24
+  __syncthreads();
+  if (wave != 0 || k >= K) return;
+  float tc = 0.f;
+  for (int c = 0; c < MAXC; ++c) acc[c] = 0.f;
+  for (int w = 0; w < CB_WAVES; ++w) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) acc[c] += red[w][c][lane];
+    tc += red[w][MAXC][lane];
+  }
   if (loss_w) g_codebook *= loss_w[0];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c)
-    if (c < C) demb[(long long)k * C + c] = g_codebook * fmaf((float)cnt, codebook[(long long)k * C + c], acc[c]);
+    if (c < C) demb[(long long)k * C + c] = g_codebook * fmaf(tc, codebook[(long long)k * C + c], acc[c]);
 }
 
 }  // namespace
 
-extern "C" size_t sdmi_vq_workspace(long long pixels) { return (size_t)((pixels + 63) / 64) * sizeof(float); }
+// one loss partial per quantize workgroup (32 pixels)
+extern "C" size_t sdmi_vq_workspace(long long pixels) { return (size_t)((pixels + 31) / 32) * sizeof(float); }
 
 extern "C" int sdmi_vq_quantize(const float* z, int ldz, const float* w, const float* b, const float* codebook, int K,
                                 int B, int HW, int C, float* zq, long long* idx, float* xq, float* ws, float* loss,
@@ -311,8 +415,11 @@ extern "C" int sdmi_vq_quantize(const float* z, int ldz, const float* w, const f
   a.z = z; a.ldz = ldz; a.w = w; a.b = b; a.codebook = codebook; a.K = K; a.B = B; a.HW = HW; a.C = C;
   a.zq = zq; a.idx = idx; a.xq = xq; a.partial = ws;
   const long long P = (long long)B * HW;
-  const int blocks = (int)((P + 63) / 64);
-  sdmi_rt::launch(vq_quantize_kernel, dim3(blocks), dim3(VQ_NT), 0, (hipStream_t)stream, a);
+  const int blocks = (int)((P + 31) / 32);
+  if (K <= VQ_EN_MAX)
+    sdmi_rt::launch(vq_quantize_kernel<true>, dim3(blocks), dim3(VQ_NT), (size_t)K * sizeof(float), (hipStream_t)stream, a);
+  else
+    sdmi_rt::launch(vq_quantize_kernel<false>, dim3(blocks), dim3(VQ_NT), 0, (hipStream_t)stream, a);
   SDMI_CHECK_LAUNCH();
   sdmi_rt::launch(vq_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ws, blocks, 1.0f / (float)(P * C),
                      loss);
@@ -356,7 +463,7 @@ extern "C" int sdmi_vq_bwd(const void* dzin, int ld_dzin, const float* zq, const
   sdmi_rt::launch(vq_bwd_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, (const float*)ws, blocks, C,
                   dw_post, db_post, dw_pre, db_pre);
   SDMI_CHECK_LAUNCH();
-  sdmi_rt::launch(vq_codebook_grad_kernel, dim3((K + 255) / 256), dim3(256), 0, (hipStream_t)stream, idx, xq,
+  sdmi_rt::launch(vq_codebook_grad_kernel, dim3((K + 63) / 64), dim3(64 * CB_WAVES), 0, (hipStream_t)stream, idx, xq,
                   codebook, K, B, HW, C, codebook_weight * 2.0f / n, loss_w, demb);
   SDMI_CHECK_LAUNCH();
   return 0;
