@@ -237,6 +237,7 @@ __global__ void mod_finalize_kernel(const float* ws, int B, int chunks, int ws_l
     const int b = (int)(i / W), c = (int)(i - (long long)b * W);
     const float* p = ws + (long long)b * chunks * ws_ld + c;
     float s = 0.f;
+#pragma unroll 8  // (independent loads in flight; the sum stays in chunk order)
     for (int k = 0; k < chunks; ++k) s += p[(long long)k * ws_ld];
     out[(long long)b * ldo + c] = f2bf(s);
   }
