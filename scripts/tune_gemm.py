@@ -39,7 +39,7 @@ def time_launch(L, d, ws, stream, iters=10, rounds=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "uncond-unet", "dit", "sample"))
+    ap.add_argument("--workload", default="cond-unet", choices=("cond-unet", "uncond-unet", "dit", "sample", "vqvae-train"))
     ap.add_argument("--sample-batch", type=int, default=1)
     ap.add_argument("--only-new", action="store_true", help="tune only shapes the starting table has no entry for")
     ap.add_argument("--against-table", action="store_true",
@@ -97,6 +97,15 @@ def main():
                               cond_input={"text": ts_, "image": ms}, seed=0)
         xT = torch.randn(Bs, 4, 32, 32, device=dev)
         step = lambda: loop.run(xT, steps=1, captured=False)  # noqa: E731
+    if args.workload == "vqvae-train":  # bench.py main_vqvae_train: the VQVAE generator step, B = 8, 256^2
+        from models.vqvae import VQVAE
+        from sdmi.vqvae_train import VQVAETrainer
+        vcfg = bench.vqvae_config()
+        torch.manual_seed(1111)
+        init = VQVAE(3, vcfg).state_dict()
+        xv = (torch.rand(8, 3, 256, 256, generator=torch.Generator().manual_seed(1111)) * 2 - 1).to(dev)
+        vtr = VQVAETrainer(vcfg, {k: v.to(dev) for k, v in init.items()}, dev)
+        step = lambda: vtr.step(xv)  # noqa: E731
     for _ in range(2):
         step()
     K.GEMM_CAPTURE = []
