@@ -51,6 +51,9 @@ def gemm_key(d):
 def _tuned():
     global TUNED
     if TUNED is None:
+        if os.environ.get("SDMI_TUNED_GEMM") and not os.path.exists(_TUNED_PATH):
+            # an explicit table that is not there must not silently become the split heuristic
+            raise FileNotFoundError(f"SDMI_TUNED_GEMM={_TUNED_PATH}: no such file")
         TUNED = json.load(open(_TUNED_PATH)) if os.path.exists(_TUNED_PATH) else {}
     return TUNED
 
