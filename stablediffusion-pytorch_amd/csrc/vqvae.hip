@@ -4,8 +4,9 @@
 //                straight-through output of VQVAE.quantize (vqvae.py:93-126). Distances follow torch.cdist's
 //                matrix-product form (|x|^2 + |e|^2 - 2 x.e, clamped at 0, square-rooted) and the FIRST
 //                minimum wins, like torch.argmin. Codebook (K x C fp32) rows are read with wave-uniform
-//                addresses (broadcast loads); a 1024-thread workgroup owns 64 pixels (one per lane) and its
-//                16 waves scan 16 disjoint codebook slices, merged in LDS with lowest-index tie-break.
+//                addresses (scalar loads, one row per half-wave); a 1024-thread workgroup owns 32 pixels and its
+//                16 waves scan 16 disjoint codebook slices (each half-wave one half of its slice), merged with a
+//                lowest-index tie-break; the codes' |e|^2 come from an LDS table built once per workgroup.
 //                Outputs: z_q = x + (q - x) in NCHW fp32 (the STE forward value), int64 indices, and the
 //                (codebook == commitment) loss mean((q - x)^2).
 //  pointwise_in: post_quant_conv (1x1, fp32) of an NCHW fp32 latent straight into the NHWC bf16 operand of
@@ -15,7 +16,8 @@
 //                the commitment term beta * mean((sg[q] - x)^2), pre_quant_conv backward into the bf16 NHWC
 //                gradient of encoder_conv_out; the 1x1-conv weight / bias gradients as per-block partials summed in
 //                a fixed order (deterministic). vq_codebook_grad: the codebook term w * mean((q - sg[x])^2) into the
-//                embedding rows (index_select backward), one thread per code scanning the pixels in order.
+//                embedding rows (index_select backward): 64 codes per workgroup, the pixels streamed through LDS and
+//                split over 8 waves, per-wave partial sums in pixel order added in wave order (deterministic).
 #include "common.h"
 #include "../../include/sdmi.h"
 #include <algorithm>
