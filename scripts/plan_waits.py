@@ -67,6 +67,17 @@ def main():
     sid = {s: i for i, (s, _) in enumerate(streams_seen.most_common())}
     last_kernel = {}
     event_src = {}  # event -> (stream, last kernel on it when recorded)
+    # events recorded LATER in the plan than a wait on them: the previous replay's record (the optimizer chunks of step
+    # N - 1 that step N's forward waits for); their producers, from a first pass over the plan
+    later_src, lk, lj = {}, {}, 0
+    for k, s, nm in ops:
+        if k == 0:
+            lk[s] = nm
+        elif k in (1, 2):
+            _, _, ev = log[lj]
+            lj += 1
+            if k == 1:
+                later_src[ev] = (sid.get(s, -1), "previous step: " + lk.get(s, "(none)"))
     li = 0
     prev_main = "-"
     pending = []
@@ -90,7 +101,7 @@ def main():
         if k == 1:
             event_src[ev] = (sid.get(s, -1), last_kernel.get(s, "(none)"))
         elif s == main:
-            src = event_src.get(ev, (-1, "(recorded before the plan)"))
+            src = event_src.get(ev) or later_src.get(ev, (-1, "(recorded before the plan)"))
             if src[0] != sid[main]:
                 pending.append(src)
     print(f"{sum(count.values())} cross-stream waits on the main stream")
